@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""Benchmark of the PLONK hot path on MI355X (BASELINE.json metric).
+
+Headline (`value`): G1-MSM Mpoint/s -- the KZG commitment MSM srs_eval_at_s
+(reference src/srs.h:53-68) over 2^22 points per GPU (config "2^22-point G1 MSM"), inputs
+resident in HBM, rotated over > 512 MiB of distinct input sets so no step is served from the
+256 MiB Infinity Cache.  One step = one complete MSM (3 B point + 1 B scalar per point) to a
+finished G1.  With N GPUs every rank owns a 2^22-point shard of one N*2^22-point MSM
+(weak scaling, point-range sharding); the K partial discrete logs of the timed steps are
+summed with ONE RCCL all-reduce and mapped to points inside the timed region.
+
+Also reported (rank 0, `components`): the 2^16-point MSM (config C2), the 2^20 forward NTT
+(config C3, Gelem/s), poly_mul 2^19 x 2^19, and the reference CPU path timed on this host.
+
+    python bench.py [--gpus N --steps K --warmup W --log2n 22]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "plonk.c_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
+MSM_BYTES_PER_POINT = 4  # 3 B G1 + 1 B HF read once
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--log2n", type=int, default=22)
+    ap.add_argument("--rotate-mib", type=int, default=640)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-components", action="store_true")
+    ap.add_argument("--profile-only", action="store_true",
+                    help="just launch the timed MSM loop (for rocprofv3 runs)")
+    return ap.parse_args()
+
+
+def make_msm_sets(torch, n, sets, dev, seed):
+    """Synthetic SRS points kG (k uniform in [1,16], G = (1,2)) and HF scalars in [0,16]."""
+    kg = torch.tensor([[1, 2, 0], [68, 74, 0], [26, 45, 0], [65, 98, 0], [12, 32, 0], [32, 42, 0],
+                       [91, 35, 0], [18, 49, 0], [18, 52, 0], [91, 66, 0], [32, 59, 0],
+                       [12, 69, 0], [65, 3, 0], [26, 56, 0], [68, 27, 0], [1, 99, 0]],
+                      dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    pts = torch.empty((sets, 3 * n), dtype=torch.uint8, device=dev)
+    sc = torch.empty((sets, n), dtype=torch.uint8, device=dev)
+    for s in range(sets):
+        k = torch.randint(0, 16, (n,), generator=g, device=dev)
+        pts[s] = kg[k].reshape(-1)
+        sc[s] = torch.randint(0, 17, (n,), generator=g, device=dev, dtype=torch.int16).to(torch.uint8)
+    return pts, sc
+
+
+def event_avg_ms(torch, st, fn, reps):
+    """Average device duration of fn() measured by an event pair around each call on st."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(reps)]
+    for i in range(reps):
+        evs[i][0].record(st)
+        fn(i)
+        evs[i][1].record(st)
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) for a, b in evs)
+    return sum(ts) / len(ts), ts[len(ts) // 2]
+
+
+def cpu_baseline(pts_np, sc_np, budget_s, gpu_g1):
+    """Reference CPU MSM (oracle/_ref = the unmodified reference srs_eval_at_s, -O2) on this
+    host, 1 thread; falls back to the oracle restatement if the reference build is absent."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import Oracle, Reference
+    if Reference.available():
+        impl, kind = Reference(), "reference"
+    else:
+        impl, kind = Oracle(), "port"
+    t0 = time.perf_counter()
+    out = impl.msm(pts_np, sc_np)
+    dt = time.perf_counter() - t0
+    reps = 1
+    while time.perf_counter() - t0 < budget_s:
+        impl.msm(pts_np, sc_np)
+        reps += 1
+    dt = (time.perf_counter() - t0) / reps
+    n = sc_np.size
+    return {"value": round(n / dt / 1e6, 3), "unit": "Mpoint/s", "cores": 1, "kind": kind,
+            "sample": "srs_eval_at_s over the first timed input set (%d points, subgroup points, "
+                      "scalars in [0,16]), %d repetitions, gcc -O2, single thread" % (n, reps),
+            "seconds_per_msm": round(dt, 4), "matches_gpu": out == gpu_g1}
+
+
+def components(torch, hip, dev, st):
+    out = {}
+    # C2: 2^16-point MSM -- device-resident kernel time and host-buffer call (PCIe incl.)
+    n = 1 << 16
+    pts, sc = make_msm_sets(torch, n, 8, dev, 7)
+    res = torch.zeros((64, 32), dtype=torch.uint8, device=dev)
+    avg, med = event_avg_ms(torch, st, lambda i: hip.msm_g1_dev(pts[i % 8], sc[i % 8], n, res[i], st), 64)
+    ph, sh = pts[0].cpu().numpy(), sc[0].cpu().numpy()
+    hip.msm_g1(ph, sh)
+    t0 = time.perf_counter()
+    for _ in range(20):
+        hip.msm_g1(ph, sh)
+    host_us = (time.perf_counter() - t0) / 20 * 1e6
+    out["msm_2^16"] = {"kernel_us": round(avg * 1e3, 2), "kernel_us_median": round(med * 1e3, 2),
+                       "Mpoint_s_kernel": round(n / (avg * 1e-3) / 1e6, 1),
+                       "host_call_us_incl_pcie": round(host_us, 1)}
+    # C3: forward NTT 2^20 over BabyBear (Montgomery u32, in place, 2 passes)
+    k = 20
+    bufs = [torch.randint(0, 2013265921, (1 << k,), dtype=torch.int64, device=dev).to(torch.int32)
+            for _ in range(4)]
+    for b in bufs:
+        hip.ntt_dev(b, k, False, st)
+    avg, med = event_avg_ms(torch, st, lambda i: hip.ntt_dev(bufs[i % 4], k, False, st), 50)
+    out["ntt_2^20_forward"] = {"ms": round(avg, 4), "Gelem_s": round((1 << k) / (avg * 1e-3) / 1e9, 2),
+                               "passes": 2, "alg_bytes": 2 * 4 * (1 << k) * 2,
+                               "GB_s_alg": round(2 * 8 * (1 << k) / (avg * 1e-3) / 1e9, 1)}
+    # poly_mul 2^19 x 2^19 -> 2^20 - 1 coefficients (device-resident, 3 launches)
+    la = lb = 1 << 19
+    a = torch.randint(0, 17, (la,), dtype=torch.int16, device=dev).to(torch.uint8)
+    b = torch.randint(0, 17, (lb,), dtype=torch.int16, device=dev).to(torch.uint8)
+    o = torch.zeros(la + lb - 1, dtype=torch.uint8, device=dev)
+    nz = torch.zeros(4, dtype=torch.int32, device=dev)
+    work = torch.zeros(hip.poly_mul_workspace(la, lb), dtype=torch.uint8, device=dev)
+    hip.poly_mul_dev(a, la, b, lb, o, nz, work, st)
+    avg, med = event_avg_ms(torch, st, lambda i: hip.poly_mul_dev(a, la, b, lb, o, nz, work, st), 30)
+    out["poly_mul_2^19x2^19"] = {"ms": round(avg, 4), "Gcoeff_s_out": round((la + lb - 1) / (avg * 1e-3) / 1e9, 2)}
+    return out
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import plonkhip as hip
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    hip.init(local)
+    st = torch.cuda.current_stream()
+
+    n = 1 << args.log2n
+    sets = max(2, -(-args.rotate_mib * (1 << 20) // (MSM_BYTES_PER_POINT * n)))
+    pts, sc = make_msm_sets(torch, n, sets, dev, 1234 + rank)
+    K, W = args.steps, args.warmup
+    res = torch.zeros((W + K, 32), dtype=torch.uint8, device=dev)
+    outs = torch.zeros((K, 4), dtype=torch.uint8, device=dev)
+
+    def step(i):
+        s = i % sets
+        hip.msm_g1_dev(pts[s], sc[s], n, res[i], st)
+
+    for i in range(W):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(W, W + K):
+        step(i)
+    logs = res[W:].view(torch.int32)[:, 2].contiguous()
+    if world > 1:
+        dist.all_reduce(logs, op=dist.ReduceOp.SUM)
+    hip.msm_finalize_dev(logs, K, 1, outs, st)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    irregular = int(res[:, 12:16].view(torch.int32).sum().item())
+    if args.profile_only:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    # kernel-level timing for the roofline: an event pair around every launch, same stream
+    reps = max(50, min(400, K))
+    off = W + K
+    res2 = torch.zeros((reps, 32), dtype=torch.uint8, device=dev)
+    avg_ms, med_ms = event_avg_ms(torch, st, lambda i: hip.msm_g1_dev(pts[(off + i) % sets], sc[(off + i) % sets],
+                                                                       n, res2[i], st), reps)
+    alg = MSM_BYTES_PER_POINT * n
+    achieved = alg / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "msm_pmc_latest.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                j = json.load(f)
+            if j.get("log2n") == args.log2n:
+                traffic = j.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    value = world * n * K / elapsed / 1e6
+    line = {
+        "metric": "G1-MSM Mpoint/s + NTT Gelem/s; end-to-end prove ms at 2^20 gates",
+        "value": round(value, 1),
+        "unit": "Mpoint/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": round(elapsed / K * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: SRS points kG (k uniform 1..16), HF scalars uniform 0..16, %d input "
+                "sets (%d MiB) rotated per step, resident in HBM" % (sets, sets * alg >> 20),
+        "config": {"workload": "2^%d-point G1 MSM per GPU (srs_eval_at_s), point-range sharded"
+                               " over %d GPU(s), one RCCL all-reduce of partial logs per batch"
+                               % (args.log2n, world),
+                   "points_per_gpu": n, "parallelism": "dp%d" % world},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel": "msm_dlog_kernel<true>",
+                     "kernel_ms_avg": round(avg_ms, 5), "kernel_ms_median": round(med_ms, 5),
+                     "alg_bytes_per_launch": alg},
+        "irregular_inputs": irregular,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        torch.cuda.synchronize()
+        gpu_g1 = bytes(res[0, 16:19].cpu().numpy())
+        line["cpu_baseline"] = cpu_baseline(pts[0].cpu().numpy(), sc[0].cpu().numpy(),
+                                            args.cpu_seconds, gpu_g1)
+    if rank == 0 and not args.no_components:
+        line["components"] = components(torch, hip, dev, st)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+/*
+ * libplonkhip -- the C ABI between the reference's host code and the gfx950 kernels.
+ *
+ * The reference (kazuakiishiguro/plonk.c) has no plugin/FFI layer: plonk.h calls
+ * srs_eval_at_s() and poly_mul() by name after #include "srs.h" / "poly.h"
+ * (src/plonk.h:8-9).  The drop-in headers in this directory keep those exact signatures and
+ * route the two hot functions through the entry points below; any other host language
+ * binds the same symbols (see INTEGRATION.md for the ctypes / cgo stubs).
+ *
+ * Conventions
+ *   - plain pointers and sizes only; a G1 is 3 bytes {x, y, infinite} exactly as the
+ *     reference struct (src/g1.h:8-11), an HF is 1 byte (src/hf.h:15-17);
+ *   - host-buffer entry points are synchronous: results are complete on return and no
+ *     caller pointer is retained;
+ *   - *_dev entry points take DEVICE pointers and a hipStream_t (as void*; NULL = the HIP
+ *     null stream) and are asynchronous;
+ *   - every entry point returns PLK_OK (0) or a PLK_ERR_* code; plk_last_error() gives text.
+ *     The drop-in headers turn a non-zero code into the reference's convention
+ *     (fprintf(stderr, ...) + exit(EXIT_FAILURE), e.g. src/srs.h:54-57);
+ *   - there is no CPU fallback: without a usable GPU every compute entry point fails
+ *     with PLK_ERR_NODEV.
+ */
+#ifndef PLONKHIP_H
+#define PLONKHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  PLK_OK = 0,
+  PLK_ERR_HIP = 1,    /* a HIP runtime call failed */
+  PLK_ERR_ARG = 2,    /* bad argument (NULL pointer, empty polynomial, ...) */
+  PLK_ERR_RANGE = 3,  /* size outside what the exact algorithm supports */
+  PLK_ERR_NODEV = 4,  /* no usable GPU */
+  PLK_ERR_NOMEM = 5   /* device allocation failed */
+};
+
+/* ---- lifetime ------------------------------------------------------------------------ */
+int plk_init(int device);            /* select device (<0: $PLK_DEVICE or 0); idempotent */
+void plk_shutdown(void);
+const char *plk_last_error(void);
+int plk_device_count(void);
+const char *plk_version(void);
+
+/* ---- host-buffer entry points (what the drop-in headers call) ------------------------ */
+
+/* Replaces the body of srs_eval_at_s (src/srs.h:53-68):
+ *   out = sum_{i<n} g1_mul(points[i], scalars[i]) folded left with g1_add.
+ * points: n x 3 bytes, scalars: n bytes (HF.value, any byte value), out: 3 bytes.
+ * The caller keeps the reference's degree check (vs->len > srs->len) before calling. */
+int plk_msm_g1(const uint8_t *points, const uint8_t *scalars, size_t n, uint8_t out[3]);
+
+/* Replaces the body of poly_mul (src/poly.h:106-122):
+ *   out[0 .. la+lb-1) = a * b over GF(17); *out_len = length after the reference's
+ *   trailing-zero trim (src/poly.h:20-38), >= 1.  out must hold la+lb-1 bytes.
+ *   la == 0 or lb == 0 mirrors the reference: *out_len = (la+lb-1 > 0), out[0] = 0. */
+int plk_poly_mul(const uint8_t *a, size_t la, const uint8_t *b, size_t lb, uint8_t *out,
+                 size_t *out_len);
+
+/* ---- device-resident entry points (bench, multi-GPU, pipelines) ---------------------- */
+
+/* Result record of one MSM, 32 bytes of device memory.  Zero it once
+ * (plk_msm_result_init); the kernel re-arms it for the next launch on the same stream. */
+typedef struct {
+  uint64_t acc;        /* internal: [31:0] partial-log sum, [47:32] ticket, [63:48] irregular */
+  uint32_t log;        /* discrete log of the result w.r.t. plk_dlog_generator(), 0..101 */
+  uint32_t irregular;  /* > 0: some input was not a canonical group element -> g1 invalid,
+                          run plk_msm_g1_serial_dev for the reference's exact raw fold */
+  uint8_t g1[4];       /* {x, y, infinite, 0} */
+  uint32_t pad[3];
+} plk_msm_result_t;
+
+int plk_msm_result_init(plk_msm_result_t *d_res, void *stream);
+int plk_msm_g1_dev(const uint8_t *d_points, const uint8_t *d_scalars, size_t n,
+                   plk_msm_result_t *d_res, void *stream);
+/* A batch of independent MSMs of n points each in ONE launch: MSM b reads
+ * d_points + b * points_stride and d_scalars + b * scalars_stride and writes d_res[b].
+ * (E.g. the commitments of one prover round, or many proofs' commitments at once.) */
+int plk_msm_g1_batch_dev(const uint8_t *d_points, size_t points_stride, const uint8_t *d_scalars,
+                         size_t scalars_stride, size_t n, int batch, plk_msm_result_t *d_res,
+                         void *stream);
+int plk_msm_g1_serial_dev(const uint8_t *d_points, const uint8_t *d_scalars, size_t n,
+                          plk_msm_result_t *d_res, void *stream);
+/* out3 = EXP[(sum of count partial logs) mod 102] -- combines per-shard partials after a
+ * collective sum (multi-GPU point-range sharding). */
+int plk_msm_combine_dev(const uint32_t *d_logs, int count, uint8_t *d_out3, void *stream);
+/* batch of already-summed logs (element i at d_logs[i * stride]) -> d_out4[4 i ..] =
+ * {x, y, infinite, 0} of EXP[log mod 102]; one launch for a whole batch of MSMs. */
+int plk_msm_finalize_dev(const uint32_t *d_logs, int batch, int stride, uint8_t *d_out4,
+                         void *stream);
+/* the order-102 generator the logs refer to (the first affine point of order 102 in (x, y)
+ * order) */
+int plk_dlog_generator(uint8_t out[3]);
+
+/* poly_mul on device buffers: d_out holds la+lb-1 bytes; *d_out_nz receives the trimmed
+ * length (0 = the zero polynomial, i.e. length 1).  d_work: plk_poly_mul_workspace() bytes. */
+size_t plk_poly_mul_workspace(size_t la, size_t lb);
+int plk_poly_mul_dev(const uint8_t *d_a, size_t la, const uint8_t *d_b, size_t lb, uint8_t *d_out,
+                     uint32_t *d_out_nz, void *d_work, void *stream);
+
+/* Radix-2 NTT over BabyBear p = 15*2^27+1 on 2^log_n Montgomery-form u32, in place:
+ * forward = DIF natural -> bit-reversed; inverse = DIT bit-reversed -> natural, unscaled. */
+int plk_ntt_dev(uint32_t *d_data, int log_n, int inverse, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLONKHIP_H */

@@ -1,0 +1,203 @@
+/* Drop-in for the reference's src/poly.h: polynomials over GF(17) (src/poly.h:10-321).
+ * Same guard, POLY layout, names and semantics (constructor trims trailing zeros, results
+ * are freshly malloc'ed and freed with poly_free).  poly_mul -- the prover's hot
+ * polynomial operation (17 calls per proof) -- runs on the GPU through plk_poly_mul
+ * (exact BabyBear NTT / direct convolution, include/plonkhip.h).  The other operations are
+ * O(n) or O(n * small) host code, restated from scratch. */
+#ifndef POLY_H
+#define POLY_H
+
+#include <stdbool.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/types.h>
+#include "hf.h"
+#include "plonkhip.h"
+
+typedef struct {
+  HF *coeffs;
+  size_t len;
+} POLY;
+
+static inline void *poly_xalloc_(size_t n, const char *who) {
+  void *p = calloc(n ? n : 1, 1);
+  if (!p) {
+    fprintf(stderr, "Memory allocation failed in %s\n", who);
+    exit(EXIT_FAILURE);
+  }
+  return p;
+}
+
+/* copy + trim trailing zeros (keeps at least one coefficient) */
+static POLY poly_new_internal(const HF *coeffs, size_t len) {
+  while (len > 1 && coeffs[len - 1].value == 0) len--;
+  POLY p;
+  p.len = len;
+  p.coeffs = (HF *)poly_xalloc_(len, "poly_new_internal");
+  if (len) memcpy(p.coeffs, coeffs, len);
+  return p;
+}
+static inline POLY poly_new(const HF *coeffs, size_t len) { return poly_new_internal(coeffs, len); }
+static inline POLY poly_zero(void) { HF z = {0}; return poly_new(&z, 1); }
+static inline POLY poly_one(void) { HF o = {1}; return poly_new(&o, 1); }
+static inline bool poly_is_zero(const POLY *p) {
+  for (size_t i = 0; i < p->len; i++)
+    if (p->coeffs[i].value) return false;
+  return true;
+}
+
+/* adds b to the constant term IN PLACE and returns the same storage (src/poly.h:67-70) */
+static inline POLY poly_add_hf(POLY *a, const HF b) {
+  a->coeffs[0] = hf_add(a->coeffs[0], b);
+  return *a;
+}
+
+static inline POLY poly_addsub_(const POLY *a, const POLY *b, int sub, const char *who) {
+  size_t n = a->len > b->len ? a->len : b->len;
+  HF *c = (HF *)poly_xalloc_(n, who);
+  for (size_t i = 0; i < n; i++) {
+    HF x = i < a->len ? a->coeffs[i] : hf_zero();
+    HF y = i < b->len ? b->coeffs[i] : hf_zero();
+    c[i] = sub ? hf_sub(x, y) : hf_add(x, y);
+  }
+  POLY r = poly_new(c, n);
+  free(c);
+  return r;
+}
+static inline POLY poly_add(const POLY *a, const POLY *b) { return poly_addsub_(a, b, 0, "poly_add"); }
+static inline POLY poly_sub(const POLY *a, const POLY *b) { return poly_addsub_(a, b, 1, "poly_sub"); }
+
+/* GPU: product over GF(17), trimmed (reference schoolbook src/poly.h:106-122) */
+static inline POLY poly_mul(const POLY *a, const POLY *b) {
+  size_t rl = a->len + b->len - 1;
+  HF *c = (HF *)poly_xalloc_(rl, "poly_mul");
+  size_t n = 0;
+  int rc = plk_poly_mul((const uint8_t *)a->coeffs, a->len, (const uint8_t *)b->coeffs, b->len,
+                        (uint8_t *)c, &n);
+  if (rc != PLK_OK) {
+    fprintf(stderr, "poly_mul failed on the GPU (libplonkhip error %d): %s\n", rc, plk_last_error());
+    exit(EXIT_FAILURE);
+  }
+  POLY r;
+  r.len = n;
+  r.coeffs = c; /* already trimmed to n; the tail of the buffer is unused */
+  return r;
+}
+
+/* long division num = quot * den + rem (src/poly.h:124-177) */
+static inline void poly_divide(const POLY *num, const POLY *den, POLY *quot, POLY *rem) {
+  if (poly_is_zero(den)) {
+    fprintf(stderr, "Division by zero polynomial in poly_divide\n");
+    exit(EXIT_FAILURE);
+  }
+  size_t nl = num->len, dl = den->len;
+  HF *q = (HF *)poly_xalloc_(nl, "poly_divide");
+  HF *r = (HF *)poly_xalloc_(nl, "poly_divide");
+  memcpy(r, num->coeffs, nl);
+  HF lead_inv = hf_inv(den->coeffs[dl - 1]);
+  for (ssize_t i = (ssize_t)nl - 1; i >= (ssize_t)(dl - 1); i--) {
+    HF c = hf_mul(r[i], lead_inv);
+    q[i - (dl - 1)] = c;
+    for (ssize_t j = 0; j < (ssize_t)dl; j++) r[i - j] = hf_sub(r[i - j], hf_mul(c, den->coeffs[dl - 1 - j]));
+  }
+  size_t ql = nl >= dl ? nl - dl + 1 : 1;
+  size_t rl = dl - 1 > nl ? nl : dl - 1;
+  *quot = poly_new(q, ql);
+  *rem = poly_new(r, rl);
+  free(q);
+  free(r);
+}
+
+static inline POLY poly_scale(const POLY *p, HF s) {
+  if (s.value == 0) return poly_zero();
+  HF *c = (HF *)poly_xalloc_(p->len, "poly_scale");
+  for (size_t i = 0; i < p->len; i++) c[i] = hf_mul(p->coeffs[i], s);
+  POLY r = poly_new(c, p->len);
+  free(c);
+  return r;
+}
+
+static inline POLY poly_shift(const POLY *p, size_t shift) {
+  if (poly_is_zero(p)) return poly_zero();
+  HF *c = (HF *)poly_xalloc_(p->len + shift, "poly_shift");
+  memcpy(c + shift, p->coeffs, p->len);
+  POLY r = poly_new(c, p->len + shift);
+  free(c);
+  return r;
+}
+
+static inline POLY poly_slice(const POLY *p, size_t start, size_t end) {
+  if (start >= end || end > p->len) {
+    fprintf(stderr, "Invalid slice indices in poly_slice\n");
+    exit(EXIT_FAILURE);
+  }
+  return poly_new(p->coeffs + start, end - start);
+}
+
+static inline POLY poly_negate(const POLY *p) {
+  HF *c = (HF *)poly_xalloc_(p->len, "poly_negate");
+  for (size_t i = 0; i < p->len; i++) c[i] = hf_neg(p->coeffs[i]);
+  POLY r = poly_new(c, p->len);
+  free(c);
+  return r;
+}
+
+static inline void poly_free(POLY *p) {
+  free(p->coeffs);
+  p->coeffs = NULL;
+  p->len = 0;
+}
+
+/* Horner */
+static inline HF poly_eval(const POLY *p, HF x) {
+  HF y = hf_zero();
+  for (size_t i = p->len; i-- > 0;) y = hf_add(hf_mul(y, x), p->coeffs[i]);
+  return y;
+}
+
+/* prod_i (x - points[i]) */
+static inline POLY poly_z(const HF *points, size_t len) {
+  POLY acc = poly_one();
+  for (size_t i = 0; i < len; i++) {
+    HF c[2] = {hf_neg(points[i]), hf_one()};
+    POLY t = poly_new(c, 2);
+    POLY nxt = poly_mul(&acc, &t);
+    poly_free(&acc);
+    poly_free(&t);
+    acc = nxt;
+  }
+  return acc;
+}
+
+/* sum_j y_j prod_{i != j} (x - x_i) / (x_j - x_i) */
+static inline POLY poly_lagrange(const HF *xs, const HF *ys, size_t len) {
+  POLY l = poly_zero();
+  for (size_t j = 0; j < len; j++) {
+    POLY lj = poly_one();
+    for (size_t i = 0; i < len; i++) {
+      if (i == j) continue;
+      HF dinv = hf_inv(hf_sub(xs[j], xs[i]));
+      if (dinv.value == 0) {
+        fprintf(stderr, "Error: Lagrange polynomial x points must be unique\n");
+        exit(EXIT_FAILURE);
+      }
+      HF c[2] = {hf_neg(hf_mul(dinv, xs[i])), dinv};
+      POLY t = poly_new(c, 2);
+      POLY nxt = poly_mul(&lj, &t);
+      poly_free(&lj);
+      poly_free(&t);
+      lj = nxt;
+    }
+    POLY s = poly_scale(&lj, ys[j]);
+    POLY nl = poly_add(&l, &s);
+    poly_free(&l);
+    poly_free(&lj);
+    poly_free(&s);
+    l = nl;
+  }
+  return l;
+}
+
+#endif /* POLY_H */

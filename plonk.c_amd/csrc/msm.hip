@@ -1,0 +1,365 @@
+// G1 multi-scalar multiplication for srs_eval_at_s (reference src/srs.h:53-68) on gfx950.
+//
+// The reference folds acc = acc + g1_mul(P_i, c_i) serially over GF(101) affine formulas
+// (src/g1.h:37-103).  E(F101) is a cyclic group of order 102 and those formulas are an
+// exact group law on it, so for canonical inputs the fold equals
+//        EXP[ (sum_i c_i * LOG(P_i)) mod 102 ]
+// with LOG/EXP the discrete-log tables of a generator g0 of order 102 (built on the host in
+// capi.hip from the group law).  That turns the MSM into a one-pass, HBM-bound integer
+// reduction: read 3 B of point + 1 B of scalar, one conflict-free LDS table read, a handful
+// of VALU ops.  It is the degenerate case of Pippenger: a single 8-bit window whose
+// "buckets" are the 102 group elements, accumulated as integers.
+//
+// Lookup: 101 = 2 mod 3, so cubing is a bijection of GF(101) and every y has exactly ONE x
+// with y^2 = x^3 + 3.  A point is handled as k = (x << 8 | y << 16 | inf << 24) (one
+// v_perm_b32 out of the loaded words) and looked up at idx = (y | (inf & 1) << 8):
+//     E[y]        = X(y) << 8 | y << 16 | LOG(X(y), y)      y < 101 (the affine points)
+//     E[256]      = 1 << 24                                   the identity {0, 0, 1}, log 0
+//     E[other]    = a value whose y byte differs from idx's     never matches
+// so d = E[idx] - k is the log (< 102) exactly when the encoding is canonical, and >= 256
+// otherwise: one subtract, one compare, and the log feeds the multiply directly.  The
+// table sits in LDS with 32 copies (copy = lane mod 32): the gathers are conflict free.
+//
+// Non-canonical encodings (off-curve points, coordinates >= 101, an infinite flag with
+// coordinates, flag bytes other than 0/1) are not group elements; the reference still
+// folds them with its raw formulas.  The kernel flags them and the host entry point re-runs
+// the exact serial fold on the device (msm_serial_fold_kernel) -- bit-exact either way.
+#include "plk_device.h"
+#include "plk_internal.h"
+
+#include <stdlib.h>
+
+__constant__ uint32_t c_ytab[512];             // E[idx], see above
+__constant__ uint8_t c_exp[PLK_GROUP_ORDER * 4];  // EXP[k] = {x, y, inf, 0}
+__constant__ uint8_t c_inv101[PLK_GF_P];       // a^-1 mod 101 (0 -> 0), for the raw fold
+
+namespace {
+
+constexpr int MSM_MAX_THREADS = 1024;
+constexpr int COPIES = 32;                     // one table copy per LDS bank
+constexpr int TAB_ENTRIES = 512;
+
+// Encoded point j (0..15) of a 48-byte group held in w[0..11]: bytes 3j..3j+2 -> k = byte
+// string shifted up by one byte (x << 8 | y << 16 | inf << 24).
+template <int J>
+__device__ __forceinline__ uint32_t point_bytes(const uint32_t (&w)[12]) {
+  constexpr int o = 3 * J, d = o >> 2, b = o & 3;
+  constexpr int d1 = (b + 2 <= 3) ? d : d + 1;
+  // v_perm_b32: selector bytes 0-3 pick from the 2nd operand, 4-7 from the 1st, 0x0C -> 0
+  constexpr uint32_t sel = 0x0Cu | ((uint32_t)b << 8) | ((uint32_t)(b + 1) << 16) | ((uint32_t)(b + 2) << 24);
+  return __builtin_amdgcn_perm(w[d1], w[d], sel);
+}
+
+__device__ __forceinline__ uint32_t encode(uint32_t x, uint32_t y, uint32_t f) { return x << 8 | y << 16 | f << 24; }
+
+// log(P) * c for one encoded point; flags non-canonical encodings in bad.  The product of
+// a flagged point is garbage, which is fine: the result is then recomputed serially.
+__device__ __forceinline__ uint32_t point_term(uint32_t k, uint32_t c, const uint32_t* tab, uint32_t lane4,
+                                               bool& bad) {
+  const uint32_t idx = (k >> 16) & 0x1FFu;
+  const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + ((idx << 7) | lane4));
+  const uint32_t d = e - k;
+  bad |= d >= 256u;
+  return (d & 0xFFu) * c;
+}
+
+__device__ __forceinline__ void fill_table(uint32_t* tab, uint32_t nthreads) {
+  uint4* t4 = reinterpret_cast<uint4*>(tab);
+  for (uint32_t q = threadIdx.x; q < TAB_ENTRIES * COPIES / 4; q += nthreads) {
+    const uint32_t v = c_ytab[q / (COPIES / 4)];
+    t4[q] = make_uint4(v, v, v, v);
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, PLK_WAVE);
+  return v;
+}
+
+struct Group {
+  uint4 q0, q1, q2, s;
+};
+
+__device__ __forceinline__ Group load_group(const uint4* p4, const uint4* s4, uint64_t g) {
+  Group r;
+  r.q0 = p4[3 * g + 0];
+  r.q1 = p4[3 * g + 1];
+  r.q2 = p4[3 * g + 2];
+  r.s = s4[g];
+  return r;
+}
+
+template <int J>
+__device__ __forceinline__ void group_term(const uint32_t (&w)[12], const uint32_t (&sw)[4], const uint32_t* tab,
+                                           uint32_t lane4, bool& bad, uint32_t& part) {
+  part += point_term(point_bytes<J>(w), (sw[J >> 2] >> (8 * (J & 3))) & 0xFFu, tab, lane4, bad);
+}
+
+__device__ __forceinline__ uint32_t group_sum(const Group& g, const uint32_t* tab, uint32_t lane4, bool& bad) {
+  const uint32_t w[12] = {g.q0.x, g.q0.y, g.q0.z, g.q0.w, g.q1.x, g.q1.y, g.q1.z, g.q1.w,
+                          g.q2.x, g.q2.y, g.q2.z, g.q2.w};
+  const uint32_t sw[4] = {g.s.x, g.s.y, g.s.z, g.s.w};
+  uint32_t part = 0;
+  group_term<0>(w, sw, tab, lane4, bad, part);   group_term<1>(w, sw, tab, lane4, bad, part);
+  group_term<2>(w, sw, tab, lane4, bad, part);   group_term<3>(w, sw, tab, lane4, bad, part);
+  group_term<4>(w, sw, tab, lane4, bad, part);   group_term<5>(w, sw, tab, lane4, bad, part);
+  group_term<6>(w, sw, tab, lane4, bad, part);   group_term<7>(w, sw, tab, lane4, bad, part);
+  group_term<8>(w, sw, tab, lane4, bad, part);   group_term<9>(w, sw, tab, lane4, bad, part);
+  group_term<10>(w, sw, tab, lane4, bad, part);  group_term<11>(w, sw, tab, lane4, bad, part);
+  group_term<12>(w, sw, tab, lane4, bad, part);  group_term<13>(w, sw, tab, lane4, bad, part);
+  group_term<14>(w, sw, tab, lane4, bad, part);  group_term<15>(w, sw, tab, lane4, bad, part);
+  return part;                                   // <= 16 * 101 * 255
+}
+
+}  // namespace
+
+// One launch = a batch of gridDim.y MSMs of n points each (points/scalars of MSM b at
+// pts + b * pstride, sc + b * sstride; result record res[b]).  Every block reduces its
+// points to a partial log (< 102) and adds
+//   partial | 1 << 32 | (irregular ? 1 << 48 : 0)
+// to res[b].acc with ONE 64-bit device-scope atomic.  The block whose ticket field comes back
+// as gridDim.x - 1 owns the complete sum (old + own add) -- no extra fence or re-read -- and
+// writes log / irregular / g1, then re-arms acc for the next launch on the stream.
+template <bool ALIGNED>
+__global__ __launch_bounds__(MSM_MAX_THREADS) void msm_dlog_kernel(const uint8_t* __restrict__ pts_base,
+                                                                   uint64_t pstride,
+                                                                   const uint8_t* __restrict__ sc_base,
+                                                                   uint64_t sstride, uint64_t n,
+                                                                   PlkMsmResult* res_base) {
+  __shared__ __attribute__((aligned(16))) uint32_t tab[TAB_ENTRIES * COPIES];
+  __shared__ uint32_t wsum[MSM_MAX_THREADS / PLK_WAVE];
+  __shared__ uint32_t wbad[MSM_MAX_THREADS / PLK_WAVE];
+  const uint8_t* pts = pts_base + (uint64_t)blockIdx.y * pstride;
+  const uint8_t* sc = sc_base + (uint64_t)blockIdx.y * sstride;
+  PlkMsmResult* res = res_base + blockIdx.y;
+
+  const uint32_t nthreads = blockDim.x;
+  const uint64_t tid = (uint64_t)blockIdx.x * nthreads + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * nthreads;
+  const uint32_t lane4 = (threadIdx.x & 31u) << 2;
+  uint32_t acc = 0;
+  bool bad = false;
+
+  if (ALIGNED) {
+    // 16 points per thread-step: 48 B of points (3 x dwordx4) + 16 B of scalars (1 x dwordx4);
+    // the first group's loads are in flight while the table is built.
+    const uint64_t ngroups = n >> 4;
+    const uint4* p4 = reinterpret_cast<const uint4*>(pts);
+    const uint4* s4 = reinterpret_cast<const uint4*>(sc);
+    uint64_t g = tid;
+    Group cur;
+    if (g < ngroups) cur = load_group(p4, s4, g);
+    fill_table(tab, nthreads);
+    __syncthreads();
+    while (g < ngroups) {
+      const uint64_t nx = g + stride;
+      Group nxt;
+      if (nx < ngroups) nxt = load_group(p4, s4, nx);
+      acc += group_sum(cur, tab, lane4, bad) % PLK_GROUP_ORDER;
+      cur = nxt;
+      g = nx;
+    }
+    // tail (n mod 16 points), one point per thread of the first block
+    const uint64_t base = ngroups << 4;
+    if (blockIdx.x == 0 && base + threadIdx.x < n) {
+      const uint64_t i = base + threadIdx.x;
+      acc += point_term(encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), sc[i], tab, lane4, bad);
+    }
+  } else {
+    fill_table(tab, nthreads);
+    __syncthreads();
+    for (uint64_t i = tid; i < n; i += stride) {
+      acc += point_term(encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), sc[i], tab, lane4, bad);
+      acc %= PLK_GROUP_ORDER;
+    }
+  }
+  acc %= PLK_GROUP_ORDER;
+
+  const uint32_t wave = threadIdx.x / PLK_WAVE;
+  const uint32_t s = wave_sum(acc);
+  const uint64_t anybad = __ballot(bad);
+  if ((threadIdx.x & (PLK_WAVE - 1)) == 0) {
+    wsum[wave] = s;
+    wbad[wave] = anybad != 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t bs = 0, bb_ = 0;
+    for (uint32_t k = 0; k < nthreads / PLK_WAVE; k++) {
+      bs += wsum[k];
+      bb_ |= wbad[k];
+    }
+    const unsigned long long add =
+        (unsigned long long)(bs % PLK_GROUP_ORDER) | (1ull << 32) | ((unsigned long long)bb_ << 48);
+    const unsigned long long old = atomicAdd(&res->acc, add);
+    if (((old >> 32) & 0xFFFFull) == gridDim.x - 1) {
+      const unsigned long long tot = old + add;
+      const uint32_t lg = (uint32_t)(tot & 0xFFFFFFFFull) % PLK_GROUP_ORDER;
+      res->log = lg;
+      res->irregular = (uint32_t)(tot >> 48);
+      res->g1[0] = c_exp[4 * lg + 0];
+      res->g1[1] = c_exp[4 * lg + 1];
+      res->g1[2] = c_exp[4 * lg + 2];
+      res->g1[3] = 0;
+      atomicExch(&res->acc, 0ull);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Exact serial fold on raw bytes, for inputs the discrete-log path flagged as irregular.
+// Restates the reference arithmetic byte for byte (src/gf.h:87-162, src/g1.h:37-103):
+// uint16 sums with one conditional subtract, int16 differences with one conditional add,
+// products % 101, inverse a^99 (= INV[a mod 101] for a != 0 mod 101, 0 otherwise).
+// ---------------------------------------------------------------------------------------
+namespace {
+struct RawPt { uint32_t x, y, inf; };
+
+__device__ __forceinline__ uint32_t r_add(uint32_t a, uint32_t b) { uint32_t s = a + b; return (s >= 101 ? s - 101 : s) & 0xFF; }
+__device__ __forceinline__ uint32_t r_sub(uint32_t a, uint32_t b) { int d = (int)a - (int)b; if (d < 0) d += 101; return (uint32_t)d & 0xFF; }
+__device__ __forceinline__ uint32_t r_mul(uint32_t a, uint32_t b) { return (a * b) % 101; }
+__device__ __forceinline__ uint32_t r_inv(uint32_t a) { return c_inv101[a % 101]; }
+__device__ __forceinline__ uint32_t r_red(uint32_t v) { return v % 101; }  // f101(uint64 of a byte)
+
+__device__ RawPt r_double(RawPt a) {
+  if (a.inf || a.y == 0) return RawPt{0, 0, 1};
+  const uint32_t m = r_mul(r_mul(3, r_mul(a.x, a.x)), r_inv(r_mul(2, a.y)));
+  const uint32_t m2 = r_mul(m, m);
+  const uint32_t xr = r_sub(m2, r_mul(2, a.x));
+  const uint32_t yr = r_sub(r_mul(m, r_sub(r_mul(3, a.x), m2)), a.y);
+  return RawPt{r_red(xr), r_red(yr), 0};
+}
+
+__device__ RawPt r_addp(RawPt a, RawPt b) {
+  if (a.inf) return b;
+  if (b.inf) return a;
+  if (a.x == b.x) {
+    if (r_add(a.y, b.y) == 0) return RawPt{0, 0, 1};
+    return r_double(a);
+  }
+  const uint32_t m = r_mul(r_sub(b.y, a.y), r_inv(r_sub(b.x, a.x)));
+  const uint32_t xr = r_sub(r_sub(r_mul(m, m), a.x), b.x);
+  const uint32_t yr = r_sub(r_mul(m, r_sub(a.x, xr)), a.y);
+  return RawPt{r_red(xr), r_red(yr), 0};
+}
+}  // namespace
+
+__global__ void msm_serial_fold_kernel(const uint8_t* __restrict__ pts, const uint8_t* __restrict__ sc,
+                                       uint64_t n, PlkMsmResult* res) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  RawPt acc{0, 0, 1};
+  for (uint64_t i = 0; i < n; i++) {
+    RawPt run{pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
+    RawPt term{0, 0, 1};
+    for (uint32_t k = sc[i]; k; k >>= 1) {
+      if (k & 1) term = r_addp(term, run);
+      run = r_double(run);
+    }
+    acc = r_addp(acc, term);
+  }
+  res->g1[0] = (uint8_t)acc.x;
+  res->g1[1] = (uint8_t)acc.y;
+  res->g1[2] = (uint8_t)acc.inf;
+  res->g1[3] = 0;
+}
+
+// Combine per-shard partial logs (e.g. after an RCCL all-reduce SUM of int32 logs) into
+// the final point: out = EXP[sum mod 102].
+__global__ void msm_combine_kernel(const uint32_t* __restrict__ logs, int count, uint8_t* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t s = 0;
+  for (int i = 0; i < count; i++) s += logs[i];
+  const uint32_t lg = (uint32_t)(s % PLK_GROUP_ORDER);
+  out[0] = c_exp[4 * lg + 0];
+  out[1] = c_exp[4 * lg + 1];
+  out[2] = c_exp[4 * lg + 2];
+}
+
+// Batched finalisation: out[4 i .. 4 i + 3] = EXP[logs[i * stride] mod 102] for i < batch.
+// Used after a collective SUM of per-rank partial logs for a batch of MSMs.
+__global__ void msm_finalize_kernel(const uint32_t* __restrict__ logs, int batch, int stride, uint8_t* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= batch) return;
+  const uint32_t lg = logs[(int64_t)i * stride] % PLK_GROUP_ORDER;
+  out[4 * i + 0] = c_exp[4 * lg + 0];
+  out[4 * i + 1] = c_exp[4 * lg + 1];
+  out[4 * i + 2] = c_exp[4 * lg + 2];
+  out[4 * i + 3] = 0;
+}
+
+// ------------------------------------------------------------------------------ launchers
+int plk_msm_upload_tables(const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101) {
+  PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_ytab), ytab, sizeof(uint32_t) * 512));
+  PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_exp), exp4, PLK_GROUP_ORDER * 4));
+  PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_inv101), inv101, PLK_GF_P));
+  return PLK_OK;
+}
+
+// Launch geometry: one 16-point group per thread per pass.  Big MSMs use 1024-thread
+// blocks (one 32 KB table per CU, 16 waves, every load of the CU's share in flight at
+// once); small ones 256-thread blocks so they still spread over many CUs.  Overridable
+// for tuning with PLK_MSM_THREADS / PLK_MSM_MAX_BLOCKS.
+void plk_msm_geometry(uint64_t n, int* threads, int* blocks) {
+  static int env_threads = -1, env_blocks = -1;
+  if (env_threads < 0) {
+    const char* t = getenv("PLK_MSM_THREADS");
+    const char* b = getenv("PLK_MSM_MAX_BLOCKS");
+    env_threads = t ? atoi(t) : 0;
+    env_blocks = b ? atoi(b) : 0;
+  }
+  const uint64_t groups = n >> 4;
+  int th = groups >= 256ull * 1024 ? 1024 : 256;
+  if (env_threads == 256 || env_threads == 512 || env_threads == 1024) th = env_threads;
+  uint64_t b = (groups + th - 1) / th;
+  const uint64_t cap = env_blocks > 0 ? (uint64_t)env_blocks : (th == 1024 ? 512 : 2048);
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  *threads = th;
+  *blocks = (int)b;
+}
+
+int plk_msm_batch_launch(const uint8_t* d_pts, uint64_t pstride, const uint8_t* d_sc, uint64_t sstride, uint64_t n,
+                         int batch, PlkMsmResult* d_res, hipStream_t st) {
+  if (batch <= 0) return PLK_OK;
+  if (batch > 65535) {
+    plk_set_error("plk_msm batch %d too large", batch);
+    return PLK_ERR_RANGE;
+  }
+  int threads, blocks;
+  plk_msm_geometry(n, &threads, &blocks);
+  const bool aligned = ((uintptr_t)d_pts % 16 == 0) && ((uintptr_t)d_sc % 16 == 0) &&
+                       (batch == 1 || (pstride % 16 == 0 && sstride % 16 == 0));
+  if (aligned)
+    hipLaunchKernelGGL(msm_dlog_kernel<true>, dim3(blocks, batch), dim3(threads), 0, st, d_pts, pstride, d_sc,
+                       sstride, n, d_res);
+  else
+    hipLaunchKernelGGL(msm_dlog_kernel<false>, dim3(blocks, batch), dim3(threads), 0, st, d_pts, pstride, d_sc,
+                       sstride, n, d_res);
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
+int plk_msm_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsmResult* d_res, hipStream_t st) {
+  return plk_msm_batch_launch(d_pts, 0, d_sc, 0, n, 1, d_res, st);
+}
+
+int plk_msm_serial_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsmResult* d_res,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(msm_serial_fold_kernel, dim3(1), dim3(64), 0, st, d_pts, d_sc, n, d_res);
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
+int plk_msm_finalize_launch(const uint32_t* d_logs, int batch, int stride, uint8_t* d_out, hipStream_t st) {
+  if (batch <= 0) return PLK_OK;
+  hipLaunchKernelGGL(msm_finalize_kernel, dim3((batch + 255) / 256), dim3(256), 0, st, d_logs, batch, stride, d_out);
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
+int plk_msm_combine_launch(const uint32_t* d_logs, int count, uint8_t* d_out, hipStream_t st) {
+  hipLaunchKernelGGL(msm_combine_kernel, dim3(1), dim3(64), 0, st, d_logs, count, d_out);
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}

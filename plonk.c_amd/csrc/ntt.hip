@@ -1,0 +1,505 @@
+// Exact GF(17) polynomial multiplication (reference poly_mul, src/poly.h:106-122) on gfx950.
+//
+// GF(17)* has order 16, so GF(17) itself has no NTT beyond 16 points.  The product of two
+// coefficient vectors reduced into [0,17) is an integer convolution whose terms are all
+// < min(la, lb) * 256, which is < p = 2013265921 (BabyBear, 2-adicity 27) whenever
+// min(la, lb) < 7,864,320.  So the convolution is computed EXACTLY by an NTT over BabyBear
+// (Montgomery u32) and reduced mod 17 at the end: bit-identical to the schoolbook.
+//
+// Transform layout -- no bit-reversal pass anywhere:
+//   forward  DIF (Gentleman-Sande), natural order in  -> bit-reversed out
+//   pointwise product in bit-reversed order
+//   inverse  DIT (Cooley-Tukey),   bit-reversed in   -> natural order out, times N^-1
+// A size-2^k transform is cut into passes over disjoint bit ranges [lo, lo+M) of the index;
+// one pass = one launch whose workgroups each own a tile of 2^M rows (the butterfly bits)
+// x C columns (consecutive low-bit values when lo > 0, consecutive groups when lo = 0),
+// staged once through LDS and run through all M radix-2 stages there.
+// Twiddles factor into a universal per-stage table T[2^j + r] = w_{2^(j+1)}^r (independent
+// of N) times a per-column factor F[c][j] = w_{2^27}^(L * 2^(26-lo-j)) (1 when lo = 0).
+//
+// poly_mul plan at 2^k > 2^12 (3 launches for k <= 23):
+//   ntt_pass_kernel   forward passes over the high bits, reading the u8 inputs directly
+//   ntt_center_kernel last forward pass (lo = 0) of a AND b, pointwise product, first
+//                     inverse pass -- one tile, one LDS round trip
+//   ntt_pass_kernel   inverse passes over the high bits; the last one scales by N^-1,
+//                     leaves Montgomery form, reduces mod 17, stores bytes and records the
+//                     last non-zero index for the reference's trailing-zero trim
+// k <= 12: one workgroup does everything (polymul_small_kernel); min(la, lb) <= 32: direct
+// convolution (polymul_direct_kernel).
+#include "plk_device.h"
+#include "plk_internal.h"
+
+#include <vector>
+
+__constant__ uint32_t c_mont17[17];            // v * R mod p for v = 0..16
+
+namespace {
+
+constexpr int NTT_THREADS = 256;
+
+struct Tw {
+  const uint32_t* small;   // T[2^j + r] = w_{2^(j+1)}^r  (Montgomery), 2^PLK_NTT_SMALL_LOG
+  const uint32_t* lo;      // w_{2^27}^i,        i < 4096
+  const uint32_t* hi;      // w_{2^27}^(4096 i), i < 2^15
+};
+
+__device__ __forceinline__ uint32_t root27(const Tw& t, uint32_t e) {  // w_{2^27}^e, e < 2^27
+  return bb::mmul(t.lo[e & 4095u], t.hi[e >> 12]);
+}
+
+// Tile geometry of one pass
+struct Pass {
+  int k;       // log2 N
+  int lo;      // lowest bit of this pass
+  int M;       // bits in this pass (rows = 2^M)
+  int C;       // columns per tile
+};
+
+__device__ __forceinline__ uint64_t tile_index(const Pass& p, uint32_t t, int r, int c) {
+  if (p.lo == 0) return (((uint64_t)t * p.C + c) << p.M) | (uint64_t)r;
+  const uint32_t per_h = (1u << p.lo) / p.C;
+  const uint64_t H = t / per_h;
+  const uint32_t L = (t % per_h) * p.C + c;
+  return (H << (p.lo + p.M)) | ((uint64_t)r << p.lo) | L;
+}
+
+// element e of the tile in global-coalescing order -> (r, c)
+__device__ __forceinline__ void tile_rc(const Pass& p, int e, int& r, int& c) {
+  if (p.lo == 0) { r = e & ((1 << p.M) - 1); c = e >> p.M; }
+  else { c = e % p.C; r = e / p.C; }
+}
+
+// F[c][j] for the tile's columns (only when lo > 0)
+__device__ void column_factors(const Pass& p, uint32_t t, const Tw& tw, uint32_t* F) {
+  if (p.lo == 0) return;
+  const uint32_t per_h = (1u << p.lo) / p.C;
+  for (int c = threadIdx.x; c < p.C; c += blockDim.x) {
+    const uint32_t L = (t % per_h) * p.C + c;
+    uint32_t f = root27(tw, L << (27 - p.lo - p.M));      // stage j = M-1
+    for (int j = p.M - 1; j >= 0; j--) {
+      F[c * p.M + j] = f;
+      f = bb::mmul(f, f);
+    }
+  }
+}
+
+// All M radix-2 stages of one tile held in LDS as X[c * RS + r].
+// DIF: j = M-1 .. 0, (u, v) -> (u + v, (u - v) w).  DIT: j = 0 .. M-1, (u, v w) -> (u + v w, u - v w).
+template <bool INV>
+__device__ void tile_stages(uint32_t* X, int M, int C, int RS, const uint32_t* Tsm, const uint32_t* F,
+                            bool has_f) {
+  const int half = 1 << (M - 1);
+  const int nb = C * half;
+  for (int s = 0; s < M; s++) {
+    const int j = INV ? s : (M - 1 - s);
+    const int h = 1 << j;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+      const int c = b >> (M - 1);
+      const int q = b & (half - 1);
+      const int rr = q & (h - 1);
+      const int r = ((q >> j) << (j + 1)) | rr;
+      uint32_t w = Tsm[h + rr];
+      if (has_f) w = bb::mmul(w, F[c * M + j]);
+      uint32_t* pu = X + c * RS + r;
+      uint32_t* pv = pu + h;
+      const uint32_t u = *pu, v = *pv;
+      if (!INV) {
+        *pu = bb::madd(u, v);
+        *pv = bb::mmul(bb::msub(u, v), w);
+      } else {
+        const uint32_t vw = bb::mmul(v, w);
+        *pu = bb::madd(u, vw);
+        *pv = bb::msub(u, vw);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+// Input/output modes of a pass
+enum : int { IN_U32 = 0, IN_U8 = 1 };
+enum : int { OUT_U32 = 0, OUT_U8 = 1 };
+
+// One NTT pass over `batch` arrays (blockIdx.y).  IN_U8: arrays are byte vectors of length
+// len_in[y] (zero-padded, reduced mod 17, converted to Montgomery).  OUT_U8: the final
+// inverse pass: scale by N^-1 (normal form -> leaves Montgomery), mod 17, bytes to out8 for
+// idx < out_len, max non-zero idx + 1 -> *nz (atomicMax).
+template <bool INV, int IN, int OUT>
+__global__ __launch_bounds__(NTT_THREADS) void ntt_pass_kernel(
+    Pass p, uint32_t* d0, uint32_t* d1, const uint8_t* a8, const uint8_t* b8, uint64_t la, uint64_t lb,
+    Tw tw, uint8_t* out8, uint64_t out_len, uint32_t ninv, uint32_t* nz) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int rows = 1 << p.M;
+  const int RS = rows + 1;
+  uint32_t* X = smem;
+  uint32_t* Tsm = X + p.C * RS;
+  uint32_t* F = Tsm + rows;
+  uint32_t* d = blockIdx.y == 0 ? d0 : d1;
+  const uint8_t* s8 = blockIdx.y == 0 ? a8 : b8;
+  const uint64_t ls = blockIdx.y == 0 ? la : lb;
+  const uint32_t t = blockIdx.x;
+
+  for (int i = threadIdx.x; i < rows; i += blockDim.x) Tsm[i] = tw.small[i];
+  column_factors(p, t, tw, F);
+  const int E = rows * p.C;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    int r, c;
+    tile_rc(p, e, r, c);
+    const uint64_t idx = tile_index(p, t, r, c);
+    uint32_t v;
+    if (IN == IN_U8) v = idx < ls ? c_mont17[s8[idx] % 17] : 0u;
+    else v = d[idx];
+    X[c * RS + r] = v;
+  }
+  __syncthreads();
+  tile_stages<INV>(X, p.M, p.C, RS, Tsm, F, p.lo != 0);
+
+  uint32_t last = 0;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    int r, c;
+    tile_rc(p, e, r, c);
+    const uint64_t idx = tile_index(p, t, r, c);
+    const uint32_t v = X[c * RS + r];
+    if (OUT == OUT_U8) {
+      if (idx < out_len) {
+        const uint8_t byte = (uint8_t)(bb::mmul(v, ninv) % 17u);
+        out8[idx] = byte;
+        if (byte && (uint32_t)idx + 1 > last) last = (uint32_t)idx + 1;
+      }
+    } else {
+      d[idx] = v;
+    }
+  }
+  if (OUT == OUT_U8) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) last = max(last, (uint32_t)__shfl_xor(last, off, PLK_WAVE));
+    if ((threadIdx.x & (PLK_WAVE - 1)) == 0 && last) atomicMax(nz, last);
+  }
+}
+
+// Last forward pass of a and b (lo = 0), pointwise product, first inverse pass; writes the
+// product spectrum-turned-partial-inverse into d0.
+__global__ __launch_bounds__(NTT_THREADS) void ntt_center_kernel(Pass p, uint32_t* d0, const uint32_t* d1,
+                                                                 Tw twf, Tw twi) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int rows = 1 << p.M;
+  const int RS = rows + 1;
+  uint32_t* X = smem;
+  uint32_t* Y = X + p.C * RS;
+  uint32_t* Tf = Y + p.C * RS;
+  uint32_t* Ti = Tf + rows;
+  const uint32_t t = blockIdx.x;
+  for (int i = threadIdx.x; i < rows; i += blockDim.x) {
+    Tf[i] = twf.small[i];
+    Ti[i] = twi.small[i];
+  }
+  const int E = rows * p.C;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    int r, c;
+    tile_rc(p, e, r, c);
+    const uint64_t idx = tile_index(p, t, r, c);
+    X[c * RS + r] = d0[idx];
+    Y[c * RS + r] = d1[idx];
+  }
+  __syncthreads();
+  tile_stages<false>(X, p.M, p.C, RS, Tf, nullptr, false);
+  tile_stages<false>(Y, p.M, p.C, RS, Tf, nullptr, false);
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    const int c = e >> p.M, r = e & (rows - 1);
+    X[c * RS + r] = bb::mmul(X[c * RS + r], Y[c * RS + r]);
+  }
+  __syncthreads();
+  tile_stages<true>(X, p.M, p.C, RS, Ti, nullptr, false);
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    int r, c;
+    tile_rc(p, e, r, c);
+    d0[tile_index(p, t, r, c)] = X[c * RS + r];
+  }
+}
+
+// Whole poly_mul in one workgroup for N = 2^k <= 2^PLK_SMALL_LOG.
+__global__ __launch_bounds__(1024) void polymul_small_kernel(const uint8_t* a8, uint64_t la, const uint8_t* b8,
+                                                             uint64_t lb, int k, Tw twf, Tw twi,
+                                                             uint8_t* out8, uint32_t ninv, uint32_t* nz) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int N = 1 << k;
+  uint32_t* X = smem;
+  uint32_t* Y = X + N;
+  uint32_t* Tf = Y + N;
+  uint32_t* Ti = Tf + N;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    X[i] = i < (int64_t)la ? c_mont17[a8[i] % 17] : 0u;
+    Y[i] = i < (int64_t)lb ? c_mont17[b8[i] % 17] : 0u;
+    Tf[i] = twf.small[i];
+    Ti[i] = twi.small[i];
+  }
+  __syncthreads();
+  if (k > 0) {
+    tile_stages<false>(X, k, 1, N, Tf, nullptr, false);
+    tile_stages<false>(Y, k, 1, N, Tf, nullptr, false);
+  }
+  for (int i = threadIdx.x; i < N; i += blockDim.x) X[i] = bb::mmul(X[i], Y[i]);
+  __syncthreads();
+  if (k > 0) tile_stages<true>(X, k, 1, N, Ti, nullptr, false);
+  const uint64_t rl = la + lb - 1;
+  uint32_t last = 0;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    if ((uint64_t)i < rl) {
+      const uint8_t byte = (uint8_t)(bb::mmul(X[i], ninv) % 17u);
+      out8[i] = byte;
+      if (byte) last = max(last, (uint32_t)i + 1);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) last = max(last, (uint32_t)__shfl_xor(last, off, PLK_WAVE));
+  if ((threadIdx.x & (PLK_WAVE - 1)) == 0 && last) atomicMax(nz, last);
+}
+
+// Direct convolution when one operand is short: out[i] = sum_j a[j] b[i-j] mod 17 over the
+// short operand s (length ls <= 32, staged in LDS), the long one read coalesced.
+__global__ __launch_bounds__(256) void polymul_direct_kernel(const uint8_t* lg, uint64_t llg, const uint8_t* sh,
+                                                             int lsh, uint8_t* out8, uint32_t* nz) {
+  __shared__ uint32_t S[64];
+  if (threadIdx.x < lsh) S[threadIdx.x] = sh[threadIdx.x] % 17u;
+  __syncthreads();
+  const uint64_t rl = llg + lsh - 1;
+  uint32_t last = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rl; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t acc = 0;
+    for (int j = 0; j < lsh; j++) {
+      const int64_t o = (int64_t)i - j;
+      if (o >= 0 && (uint64_t)o < llg) acc += S[j] * (lg[o] % 17u);
+    }
+    const uint8_t byte = (uint8_t)(acc % 17u);
+    out8[i] = byte;
+    if (byte) last = max(last, (uint32_t)(i + 1));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) last = max(last, (uint32_t)__shfl_xor(last, off, PLK_WAVE));
+  if ((threadIdx.x & (PLK_WAVE - 1)) == 0 && last) atomicMax(nz, last);
+}
+
+// ------------------------------------------------------------------------------ host side
+namespace {
+
+struct TwHost {
+  uint32_t* d_small_f = nullptr;
+  uint32_t* d_small_i = nullptr;
+  uint32_t* d_lo_f = nullptr;
+  uint32_t* d_hi_f = nullptr;
+  uint32_t* d_lo_i = nullptr;
+  uint32_t* d_hi_i = nullptr;
+} g_tw;
+
+Tw tw_fwd() { return Tw{g_tw.d_small_f, g_tw.d_lo_f, g_tw.d_hi_f}; }
+Tw tw_inv() { return Tw{g_tw.d_small_i, g_tw.d_lo_i, g_tw.d_hi_i}; }
+
+// split k bits into passes (high bits first); every pass <= 11 bits except a lone center
+void make_plan(int k, int* Ms, int& npass) {
+  if (k <= 22) {
+    npass = 2;
+    const int center = k - k / 2;    // >= the high pass
+    Ms[0] = k - center;              // high bits
+    Ms[1] = center;                  // low bits (center kernel)
+  } else {
+    npass = 3;
+    const int a = (k + 2) / 3;
+    Ms[0] = k - 2 * a;
+    Ms[1] = a;
+    Ms[2] = a;
+  }
+}
+
+int cols_for(int M, bool center) {
+  int C = (1 << 12) >> M;
+  if (C < 1) C = 1;
+  if (!center && C < 4) C = 4;
+  return C;
+}
+
+}  // namespace
+
+int plk_ntt_init_tables(void) {
+  if (g_tw.d_small_f) return PLK_OK;
+  const uint32_t w27 = bb::hpow(bb::GENERATOR, (bb::P - 1) >> bb::TWO_ADICITY);   // order 2^27
+  const uint32_t w27i = bb::hpow(w27, bb::P - 2);
+  const int SM = 1 << PLK_NTT_SMALL_LOG;
+  std::vector<uint32_t> sf(SM), si(SM), lf(4096), hf(1 << 15), li(4096), hi_(1 << 15);
+  sf[0] = si[0] = bb::to_mont(1);
+  for (int j = 0; (1 << j) < SM; j++) {
+    const uint32_t wf = bb::hpow(w27, 1ull << (26 - j));   // order 2^(j+1)
+    const uint32_t wi = bb::hpow(w27i, 1ull << (26 - j));
+    uint64_t xf = 1, xi = 1;
+    for (int r = 0; r < (1 << j); r++) {
+      sf[(1 << j) + r] = bb::to_mont((uint32_t)xf);
+      si[(1 << j) + r] = bb::to_mont((uint32_t)xi);
+      xf = xf * wf % bb::P;
+      xi = xi * wi % bb::P;
+    }
+  }
+  {
+    uint64_t x = 1, y = 1;
+    for (int i = 0; i < 4096; i++) {
+      lf[i] = bb::to_mont((uint32_t)x);
+      li[i] = bb::to_mont((uint32_t)y);
+      x = x * w27 % bb::P;
+      y = y * w27i % bb::P;
+    }
+    const uint64_t s = bb::hpow(w27, 4096), si2 = bb::hpow(w27i, 4096);
+    x = 1, y = 1;
+    for (int i = 0; i < (1 << 15); i++) {
+      hf[i] = bb::to_mont((uint32_t)x);
+      hi_[i] = bb::to_mont((uint32_t)y);
+      x = x * s % bb::P;
+      y = y * si2 % bb::P;
+    }
+  }
+  uint32_t m17[17];
+  for (int v = 0; v < 17; v++) m17[v] = bb::to_mont((uint32_t)v);
+  PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_mont17), m17, sizeof m17));
+  auto up = [](uint32_t** d, const std::vector<uint32_t>& h) -> int {
+    PLK_HIP(hipMalloc((void**)d, h.size() * 4));
+    PLK_HIP(hipMemcpy(*d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    return PLK_OK;
+  };
+  int rc;
+  if ((rc = up(&g_tw.d_small_f, sf)) || (rc = up(&g_tw.d_small_i, si)) || (rc = up(&g_tw.d_lo_f, lf)) ||
+      (rc = up(&g_tw.d_hi_f, hf)) || (rc = up(&g_tw.d_lo_i, li)) || (rc = up(&g_tw.d_hi_i, hi_)))
+    return rc;
+  return PLK_OK;
+}
+
+void plk_ntt_free_tables(void) {
+  (void)hipFree(g_tw.d_small_f); (void)hipFree(g_tw.d_small_i); (void)hipFree(g_tw.d_lo_f);
+  (void)hipFree(g_tw.d_hi_f); (void)hipFree(g_tw.d_lo_i); (void)hipFree(g_tw.d_hi_i);
+  g_tw = TwHost{};
+}
+
+static int log2_ceil(uint64_t v) {
+  int k = 0;
+  while ((1ull << k) < v) k++;
+  return k;
+}
+
+size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb) {
+  if (la == 0 || lb == 0) return 0;
+  const uint64_t rl = la + lb - 1;
+  const int k = log2_ceil(rl);
+  if ((la < lb ? la : lb) <= PLK_DIRECT_MAX || k <= PLK_SMALL_LOG) return 0;
+  return (size_t)2 * 4 * (1ull << k);
+}
+
+static size_t pass_lds(int M, int C, bool center) {
+  const size_t rows = 1u << M;
+  return (center ? 2 : 1) * C * (rows + 1) * 4 + (center ? 2 : 1) * rows * 4 + (size_t)C * M * 4;
+}
+
+// d_out must hold la+lb-1 bytes; *d_nz is zeroed here and receives the trimmed length
+// (0 means "all zero" -> caller reports length 1).
+int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
+                        uint32_t* d_nz, void* d_work, hipStream_t st) {
+  if (la == 0 || lb == 0) return PLK_ERR_ARG;
+  const uint64_t rl = la + lb - 1;
+  const uint64_t mn = la < lb ? la : lb;
+  if (mn * 256 >= bb::P) return PLK_ERR_RANGE;
+  if (rl >= (1ull << 32)) return PLK_ERR_RANGE;
+  PLK_HIP(hipMemsetAsync(d_nz, 0, 4, st));
+  if (mn <= PLK_DIRECT_MAX) {
+    const uint8_t* lg = la >= lb ? d_a : d_b;
+    const uint8_t* sh = la >= lb ? d_b : d_a;
+    const uint64_t blocks64 = (rl + 255) / 256;
+    const int blocks = (int)(blocks64 > 8192 ? 8192 : blocks64);
+    hipLaunchKernelGGL(polymul_direct_kernel, dim3(blocks), dim3(256), 0, st, lg, la >= lb ? la : lb, sh, (int)mn,
+                       d_out, d_nz);
+    PLK_HIP(hipGetLastError());
+    return PLK_OK;
+  }
+  const int k = log2_ceil(rl);
+  if (k > bb::TWO_ADICITY) return PLK_ERR_RANGE;
+  const uint32_t ninv = bb::hpow(1ull << k, bb::P - 2);   // normal form on purpose
+  if (k <= PLK_SMALL_LOG) {
+    const size_t lds = (size_t)4 * 4 * (1u << k);
+    hipLaunchKernelGGL(polymul_small_kernel, dim3(1), dim3(1024), lds, st, d_a, la, d_b, lb, k, tw_fwd(), tw_inv(),
+                       d_out, ninv, d_nz);
+    PLK_HIP(hipGetLastError());
+    return PLK_OK;
+  }
+  if (!d_work) return PLK_ERR_ARG;
+  uint32_t* A = (uint32_t*)d_work;
+  uint32_t* B = A + (1ull << k);
+  int Ms[3], np;
+  make_plan(k, Ms, np);
+  // bit ranges: pass i covers [lo_i, lo_i + Ms[i]), lo decreasing
+  int lo[3];
+  {
+    int top = k;
+    for (int i = 0; i < np; i++) { lo[i] = top - Ms[i]; top = lo[i]; }
+  }
+  const Tw twf = tw_fwd(), twi = tw_inv();
+  // forward passes over the high bits (first one reads the u8 inputs)
+  for (int i = 0; i < np - 1; i++) {
+    Pass p{k, lo[i], Ms[i], cols_for(Ms[i], false)};
+    const uint32_t tiles = (uint32_t)((1ull << k) >> (p.M + log2_ceil(p.C)));
+    const size_t lds = pass_lds(p.M, p.C, false);
+    if (i == 0)
+      hipLaunchKernelGGL((ntt_pass_kernel<false, IN_U8, OUT_U32>), dim3(tiles, 2), dim3(NTT_THREADS), lds, st, p, A,
+                         B, d_a, d_b, la, lb, twf, nullptr, 0, 0u, nullptr);
+    else
+      hipLaunchKernelGGL((ntt_pass_kernel<false, IN_U32, OUT_U32>), dim3(tiles, 2), dim3(NTT_THREADS), lds, st, p, A,
+                         B, nullptr, nullptr, 0, 0, twf, nullptr, 0, 0u, nullptr);
+    PLK_HIP(hipGetLastError());
+  }
+  {
+    Pass p{k, 0, Ms[np - 1], cols_for(Ms[np - 1], true)};
+    const uint32_t tiles = (uint32_t)((1ull << k) >> (p.M + log2_ceil(p.C)));
+    const size_t lds = pass_lds(p.M, p.C, true);
+    hipLaunchKernelGGL(ntt_center_kernel, dim3(tiles), dim3(NTT_THREADS), lds, st, p, A, B, twf, twi);
+    PLK_HIP(hipGetLastError());
+  }
+  for (int i = np - 2; i >= 0; i--) {
+    Pass p{k, lo[i], Ms[i], cols_for(Ms[i], false)};
+    const uint32_t tiles = (uint32_t)((1ull << k) >> (p.M + log2_ceil(p.C)));
+    const size_t lds = pass_lds(p.M, p.C, false);
+    if (i == 0)
+      hipLaunchKernelGGL((ntt_pass_kernel<true, IN_U32, OUT_U8>), dim3(tiles, 1), dim3(NTT_THREADS), lds, st, p, A,
+                         A, nullptr, nullptr, 0, 0, twi, d_out, rl, ninv, d_nz);
+    else
+      hipLaunchKernelGGL((ntt_pass_kernel<true, IN_U32, OUT_U32>), dim3(tiles, 1), dim3(NTT_THREADS), lds, st, p, A,
+                         A, nullptr, nullptr, 0, 0, twi, nullptr, 0, 0u, nullptr);
+    PLK_HIP(hipGetLastError());
+  }
+  return PLK_OK;
+}
+
+// Standalone forward NTT (DIF, natural -> bit-reversed), in place on Montgomery-form u32,
+// or inverse (DIT, bit-reversed -> natural, NOT scaled by N^-1).  Same passes as poly_mul.
+int plk_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st) {
+  if (k < 1 || k > bb::TWO_ADICITY) return PLK_ERR_RANGE;
+  int Ms[3], np = 1;
+  if (k <= 12) { Ms[0] = k; np = 1; }
+  else make_plan(k, Ms, np);
+  int lo[3];
+  {
+    int top = k;
+    for (int i = 0; i < np; i++) { lo[i] = top - Ms[i]; top = lo[i]; }
+  }
+  const Tw tw = inverse ? tw_inv() : tw_fwd();
+  for (int s = 0; s < np; s++) {
+    const int i = inverse ? (np - 1 - s) : s;
+    Pass p{k, lo[i], Ms[i], cols_for(Ms[i], lo[i] == 0)};
+    if (lo[i] != 0 && (1 << lo[i]) < p.C) p.C = 1 << lo[i];
+    if ((1ull << k) < ((uint64_t)p.C << p.M)) p.C = 1;
+    const uint32_t tiles = (uint32_t)((1ull << k) >> (p.M + log2_ceil(p.C)));
+    const size_t lds = pass_lds(p.M, p.C, false);
+    if (inverse)
+      hipLaunchKernelGGL((ntt_pass_kernel<true, IN_U32, OUT_U32>), dim3(tiles, 1), dim3(NTT_THREADS), lds, st, p, d,
+                         d, nullptr, nullptr, 0, 0, tw, nullptr, 0, 0u, nullptr);
+    else
+      hipLaunchKernelGGL((ntt_pass_kernel<false, IN_U32, OUT_U32>), dim3(tiles, 1), dim3(NTT_THREADS), lds, st, p, d,
+                         d, nullptr, nullptr, 0, 0, tw, nullptr, 0, 0u, nullptr);
+    PLK_HIP(hipGetLastError());
+  }
+  return PLK_OK;
+}

@@ -1,0 +1,71 @@
+// Device-side building blocks shared by the gfx950 kernels of libplonkhip.
+//
+//   * GF(101) group tables for the discrete-log MSM (msm.hip)
+//   * BabyBear (p = 15*2^27 + 1) Montgomery arithmetic for the exact NTT poly_mul (ntt.hip)
+//
+// Everything here is integer work; no MFMA is involved anywhere in this library.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PLK_WAVE 64
+
+// ----------------------------------------------------------------------------------------
+// BabyBear Montgomery arithmetic, R = 2^32.  Values are kept fully reduced in [0, p).
+// ----------------------------------------------------------------------------------------
+namespace bb {
+constexpr uint32_t P = 2013265921u;          // 15 * 2^27 + 1
+constexpr int TWO_ADICITY = 27;
+
+constexpr uint32_t neg_inv_p() {             // p' = -p^{-1} mod 2^32 (Newton iteration)
+  uint32_t x = 1;
+  for (int i = 0; i < 5; i++) x *= 2u - P * x;
+  return 0u - x;
+}
+constexpr uint32_t PINV = neg_inv_p();
+static_assert(P * (0u - PINV) == 1u, "p * p^{-1} == 1 mod 2^32");
+
+__host__ __device__ __forceinline__ uint32_t mmul(uint32_t a, uint32_t b) {
+  uint64_t t = (uint64_t)a * b;
+  uint32_t m = (uint32_t)t * PINV;
+  uint64_t u = (t + (uint64_t)m * P) >> 32;
+  return u >= P ? (uint32_t)(u - P) : (uint32_t)u;
+}
+__host__ __device__ __forceinline__ uint32_t madd(uint32_t a, uint32_t b) {
+  uint32_t s = a + b;                        // a, b < 2^31: no wrap
+  return s >= P ? s - P : s;
+}
+__host__ __device__ __forceinline__ uint32_t msub(uint32_t a, uint32_t b) {
+  return a >= b ? a - b : a + P - b;
+}
+
+// host-side helpers (plain modular arithmetic, used to build tables)
+inline uint32_t hpow(uint64_t b, uint64_t e) {
+  uint64_t r = 1;
+  b %= P;
+  while (e) {
+    if (e & 1) r = r * b % P;
+    b = b * b % P;
+    e >>= 1;
+  }
+  return (uint32_t)r;
+}
+inline uint32_t to_mont(uint32_t x) { return (uint32_t)(((uint64_t)x << 32) % P); }
+inline uint32_t from_mont(uint32_t x) { return mmul(x, 1u); }
+constexpr uint32_t GENERATOR = 31;           // generates F_p^*
+}  // namespace bb
+
+// ----------------------------------------------------------------------------------------
+// E(F101): y^2 = x^3 + 3 has 102 points and is cyclic (102 = 2*3*17).  The MSM maps every
+// canonical point to its discrete log in Z/102 w.r.t. a fixed generator g0 of order 102,
+// so sum c_i * P_i becomes sum c_i * log(P_i) mod 102 -- an exact group isomorphism.
+//
+// Per x in [0,101): one dword  Y | L << 8 | Lneg << 16
+//   Y    = the smaller root y of y^2 = x^3 + 3  (0xFF: no point with this x)
+//   L    = log(x, Y),  Lneg = log(x, 101 - Y) = (102 - L) mod 102
+// The only point with y = 0 is the 2-torsion point (48, 0), log 51.
+// Exp table: 102 canonical encodings {x, y, infinite}, index 0 = identity {0, 0, 1}.
+// Both tables are built on the host at plk_init (capi.hip) from the group law itself.
+// ----------------------------------------------------------------------------------------
+#define PLK_GF_P 101
+#define PLK_GROUP_ORDER 102

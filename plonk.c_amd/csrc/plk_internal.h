@@ -1,0 +1,42 @@
+// Internal declarations shared by the .hip translation units of libplonkhip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/plonkhip.h"
+
+typedef plk_msm_result_t PlkMsmResult;
+
+#define PLK_NTT_SMALL_LOG 12   // universal small twiddle table covers tiles up to 2^12 rows
+#define PLK_SMALL_LOG 12       // poly_mul with N <= 2^12: one workgroup does everything
+#define PLK_DIRECT_MAX 32      // poly_mul with min(la, lb) <= 32: direct convolution
+
+void plk_set_error(const char* fmt, ...);
+
+#define PLK_HIP(call)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (call);                                                              \
+    if (e_ != hipSuccess) {                                                              \
+      plk_set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+      return PLK_ERR_HIP;                                                                \
+    }                                                                                    \
+  } while (0)
+
+// msm.hip
+int plk_msm_upload_tables(const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101);
+void plk_msm_geometry(uint64_t n, int* threads, int* blocks);
+int plk_msm_batch_launch(const uint8_t* d_pts, uint64_t pstride, const uint8_t* d_sc, uint64_t sstride, uint64_t n,
+                         int batch, PlkMsmResult* d_res, hipStream_t st);
+int plk_msm_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsmResult* d_res, hipStream_t st);
+int plk_msm_serial_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsmResult* d_res,
+                          hipStream_t st);
+int plk_msm_finalize_launch(const uint32_t* d_logs, int batch, int stride, uint8_t* d_out, hipStream_t st);
+int plk_msm_combine_launch(const uint32_t* d_logs, int count, uint8_t* d_out, hipStream_t st);
+
+// ntt.hip
+int plk_ntt_init_tables(void);
+void plk_ntt_free_tables(void);
+size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb);
+int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
+                        uint32_t* d_nz, void* d_work, hipStream_t st);
+int plk_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st);

@@ -1,0 +1,218 @@
+"""Python plumbing over libplonkhip.so -- the C ABI declared in include/plonkhip.h.
+
+The product boundary is the C ABI (and the drop-in C headers in include/ that the
+reference's plonk.h compiles against).  This module only loads that library with ctypes
+for the tests, bench.py and the multi-GPU driver; it never computes anything itself and
+there is no fallback: if libplonkhip.so is missing or no GPU is usable, every call raises.
+
+Host-buffer functions mirror the reference hot path (src/srs.h:53-68, src/poly.h:106-122):
+    msm_g1(points, scalars) -> 3 bytes {x, y, infinite}        (srs_eval_at_s)
+    poly_mul(a, b)          -> trimmed coefficient bytes         (poly_mul)
+    srs_eval_at_s(g1s, coeffs) -- with the reference's degree check
+Device functions take torch CUDA tensors (or raw ints) and an optional stream.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "libplonkhip.so")
+HEADER_PATH = os.path.join(REPO_DIR, "include", "plonkhip.h")
+
+PLK_OK, PLK_ERR_HIP, PLK_ERR_ARG, PLK_ERR_RANGE, PLK_ERR_NODEV, PLK_ERR_NOMEM = range(6)
+MSM_RESULT_BYTES = 32
+
+_u8p = C.POINTER(C.c_uint8)
+_vp = C.c_void_p
+_sz = C.c_size_t
+
+# every exported entry point with its ctypes signature (restype, argtypes)
+SIGNATURES = {
+    "plk_init": (C.c_int, [C.c_int]),
+    "plk_shutdown": (None, []),
+    "plk_last_error": (C.c_char_p, []),
+    "plk_device_count": (C.c_int, []),
+    "plk_version": (C.c_char_p, []),
+    "plk_msm_g1": (C.c_int, [_u8p, _u8p, _sz, _u8p]),
+    "plk_poly_mul": (C.c_int, [_u8p, _sz, _u8p, _sz, _u8p, C.POINTER(_sz)]),
+    "plk_msm_result_init": (C.c_int, [_vp, _vp]),
+    "plk_msm_g1_dev": (C.c_int, [_vp, _vp, _sz, _vp, _vp]),
+    "plk_msm_g1_batch_dev": (C.c_int, [_vp, _sz, _vp, _sz, _sz, C.c_int, _vp, _vp]),
+    "plk_msm_g1_serial_dev": (C.c_int, [_vp, _vp, _sz, _vp, _vp]),
+    "plk_msm_combine_dev": (C.c_int, [_vp, C.c_int, _vp, _vp]),
+    "plk_msm_finalize_dev": (C.c_int, [_vp, C.c_int, C.c_int, _vp, _vp]),
+    "plk_dlog_generator": (C.c_int, [_u8p]),
+    "plk_poly_mul_workspace": (_sz, [_sz, _sz]),
+    "plk_poly_mul_dev": (C.c_int, [_vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp]),
+    "plk_ntt_dev": (C.c_int, [_vp, C.c_int, C.c_int, _vp]),
+}
+
+
+class PlonkHipError(RuntimeError):
+    def __init__(self, fn, code, msg):
+        super().__init__("%s failed (code %d): %s" % (fn, code, msg))
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load libplonkhip.so (raises if it was never built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FileNotFoundError("libplonkhip.so not built (run `make -C plonk.c_amd` or "
+                                    "__graft_entry__.build()): %s" % LIB_PATH)
+        # torch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7) and asks for it by a
+        # different file name, so loading ours first would put TWO HIP runtimes in the
+        # process.  Load torch first: our NEEDED libamdhip64.so.7 then binds to torch's copy
+        # and the process has one runtime, one device context, shared streams.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error():
+    return lib().plk_last_error().decode(errors="replace")
+
+
+def _check(fn, rc):
+    if rc != PLK_OK:
+        raise PlonkHipError(fn, rc, last_error())
+
+
+def _u8(a):
+    return np.ascontiguousarray(np.frombuffer(a, np.uint8) if isinstance(a, (bytes, bytearray))
+                                else np.asarray(a, dtype=np.uint8))
+
+
+def _p(a):
+    return a.ctypes.data_as(_u8p)
+
+
+def init(device=-1):
+    _check("plk_init", lib().plk_init(int(device)))
+
+
+def device_count():
+    return int(lib().plk_device_count())
+
+
+def dlog_generator():
+    out = np.zeros(3, np.uint8)
+    _check("plk_dlog_generator", lib().plk_dlog_generator(_p(out)))
+    return bytes(out)
+
+
+# ---------------------------------------------------------------- host-buffer entry points
+def msm_g1(points, scalars):
+    """sum_i scalars[i] * points[i] as the reference's serial fold would return it."""
+    pts = _u8(points).reshape(-1)
+    sc = _u8(scalars).reshape(-1)
+    if pts.size != 3 * sc.size:
+        raise ValueError("points must be n x 3 bytes for n scalars")
+    out = np.zeros(3, np.uint8)
+    _check("plk_msm_g1", lib().plk_msm_g1(_p(pts), _p(sc), sc.size, _p(out)))
+    return bytes(out)
+
+
+def srs_eval_at_s(g1s, coeffs):
+    """srs_eval_at_s(srs, vs) (src/srs.h:53-68): the reference exits when the polynomial is
+    longer than the SRS; this mirror raises ValueError instead of exiting the interpreter."""
+    pts = _u8(g1s).reshape(-1)
+    sc = _u8(coeffs).reshape(-1)
+    if sc.size > pts.size // 3:
+        raise ValueError("Poynomial degree exceeds SRS size: POLY degree: %d, SRS supports up "
+                         "to degree: %d" % (sc.size, sc.size))
+    return msm_g1(pts[:3 * sc.size], sc)
+
+
+def poly_mul(a, b):
+    """GF(17) product, trimmed exactly like the reference's poly_new."""
+    a = _u8(a).reshape(-1)
+    b = _u8(b).reshape(-1)
+    rl = max(a.size + b.size - 1, 1)
+    out = np.zeros(rl, np.uint8)
+    n = _sz(0)
+    _check("plk_poly_mul", lib().plk_poly_mul(_p(a), a.size, _p(b), b.size, _p(out), C.byref(n)))
+    return bytes(out[:n.value])
+
+
+# ---------------------------------------------------------------- device entry points
+def _ptr(t):
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+def _stream(s):
+    if s is None:
+        return None
+    if isinstance(s, int):
+        return s
+    return s.cuda_stream
+
+
+def msm_result_init(res, stream=None):
+    _check("plk_msm_result_init", lib().plk_msm_result_init(_ptr(res), _stream(stream)))
+
+
+def msm_g1_dev(points, scalars, n, res, stream=None):
+    _check("plk_msm_g1_dev", lib().plk_msm_g1_dev(_ptr(points), _ptr(scalars), int(n), _ptr(res),
+                                                  _stream(stream)))
+
+
+def msm_g1_batch_dev(points, points_stride, scalars, scalars_stride, n, batch, res, stream=None):
+    _check("plk_msm_g1_batch_dev", lib().plk_msm_g1_batch_dev(
+        _ptr(points), int(points_stride), _ptr(scalars), int(scalars_stride), int(n), int(batch),
+        _ptr(res), _stream(stream)))
+
+
+def msm_g1_serial_dev(points, scalars, n, res, stream=None):
+    _check("plk_msm_g1_serial_dev", lib().plk_msm_g1_serial_dev(_ptr(points), _ptr(scalars), int(n),
+                                                                _ptr(res), _stream(stream)))
+
+
+def msm_combine_dev(logs, count, out3, stream=None):
+    _check("plk_msm_combine_dev", lib().plk_msm_combine_dev(_ptr(logs), int(count), _ptr(out3),
+                                                            _stream(stream)))
+
+
+def msm_finalize_dev(logs, batch, stride, out4, stream=None):
+    _check("plk_msm_finalize_dev", lib().plk_msm_finalize_dev(_ptr(logs), int(batch), int(stride),
+                                                              _ptr(out4), _stream(stream)))
+
+
+def poly_mul_workspace(la, lb):
+    return int(lib().plk_poly_mul_workspace(int(la), int(lb)))
+
+
+def poly_mul_dev(a, la, b, lb, out, nz, work, stream=None):
+    _check("plk_poly_mul_dev", lib().plk_poly_mul_dev(_ptr(a), int(la), _ptr(b), int(lb), _ptr(out),
+                                                      _ptr(nz), _ptr(work), _stream(stream)))
+
+
+def ntt_dev(data, log_n, inverse=False, stream=None):
+    _check("plk_ntt_dev", lib().plk_ntt_dev(_ptr(data), int(log_n), 1 if inverse else 0,
+                                            _stream(stream)))
+
+
+def parse_result(res_bytes):
+    """Decode a 32-byte plk_msm_result_t copied to the host."""
+    b = bytes(res_bytes)
+    return {"log": int.from_bytes(b[8:12], "little"),
+            "irregular": int.from_bytes(b[12:16], "little"),
+            "g1": b[16:19]}

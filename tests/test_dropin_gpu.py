@@ -1,0 +1,55 @@
+"""Drop-in proof: the reference's UNMODIFIED plonk.h prover compiled against include/
+(pre-included prelude) so poly_mul / srs_eval_at_s run in libplonkhip on the GPU.  The
+34-byte proofs must equal the golden proofs recorded from the all-CPU reference.
+
+The drop-in library (oracle/_ref/libplonkref_dropin.so) can only be BUILT where
+/root/reference exists; it travels to the GPU box with the snapshot.  Without it this module
+skips (the C-ABI parity tests still cover the hot path)."""
+import os
+
+import numpy as np
+import pytest
+
+import gen
+from conftest import ROOT, load_golden
+
+pytestmark = pytest.mark.gpu
+DROPIN = os.path.join(ROOT, "oracle", "_ref", "libplonkref_dropin.so")
+
+
+@pytest.fixture(scope="module")
+def dropin(hip):
+    if not os.path.exists(DROPIN):
+        pytest.skip("drop-in build absent (needs /root/reference at build time)")
+    from pyoracle import Reference
+    return Reference(DROPIN)
+
+
+def test_toy_proof_bytes(dropin):
+    g = load_golden("prove.json")
+    for p in g["proofs"]:
+        got = dropin.prove4(p["gates"], p["copies"], p["wires"], p["chal"], p["rand"],
+                            p["secret"], p["srs_n"], p["srs_mode"])
+        assert got.hex() == p["proof"], p.get("note", p["chal"])
+
+
+def test_interpolate_and_hot_ops(dropin):
+    g = load_golden("prove.json")
+    for c in g["interpolate_at_h"]:
+        assert dropin.interpolate4(c["values"]).hex() == c["out"]
+    for c in load_golden("msm.json")["cases"]:
+        pts = np.frombuffer(bytes.fromhex(c["points"]), np.uint8)
+        sc = np.frombuffer(bytes.fromhex(c["scalars"]), np.uint8)
+        assert dropin.msm(pts, sc).hex() == c["out"]
+    for c in load_golden("poly_mul.json")["cases"]:
+        assert dropin.poly_mul(bytes.fromhex(c["a"]), bytes.fromhex(c["b"])).hex() == c["out"]
+
+
+def test_large_through_headers(dropin):
+    c = load_golden("msm.json")["large"][5]
+    pts, sc = gen.msm_inputs(c["seed"], c["n"], c["kind"])
+    assert dropin.msm(pts, sc).hex() == c["out"]
+    c = load_golden("poly_mul.json")["large"][6]
+    a, b = gen.poly_inputs(c["seed"], c["la"], c["lb"])
+    out = dropin.poly_mul(a, b)
+    assert gen.digest(np.frombuffer(out, np.uint8)) == c["sha256"]

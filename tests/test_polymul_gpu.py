@@ -1,0 +1,81 @@
+"""GPU parity for poly_mul (reference src/poly.h:106-122 + trim src/poly.h:20-38) through
+the C ABI: bit-exact coefficient bytes and trimmed length."""
+import numpy as np
+import pytest
+
+import gen
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def test_golden_cases(hip):
+    g = load_golden("poly_mul.json")
+    for c in g["cases"]:
+        a, b = bytes.fromhex(c["a"]), bytes.fromhex(c["b"])
+        assert hip.poly_mul(a, b).hex() == c["out"], (len(a), len(b))
+
+
+@pytest.mark.parametrize("idx", range(9))
+def test_golden_large_digests(hip, idx):
+    c = load_golden("poly_mul.json")["large"][idx]
+    a, b = gen.poly_inputs(c["seed"], c["la"], c["lb"])
+    out = hip.poly_mul(a, b)
+    assert len(out) == c["len"]
+    assert gen.digest(np.frombuffer(out, np.uint8)) == c["sha256"]
+
+
+def test_survey_digests(hip, oracle):
+    for c in load_golden("poly_mul.json")["survey_xorshift"]:
+        a, b = oracle.gen_survey_poly(c["n"])
+        out = hip.poly_mul(a, b)
+        assert len(out) == c["len"]
+        assert "%08x" % oracle.digest31(np.frombuffer(out, np.uint8)) == c["digest31"]
+
+
+# shapes straddling every dispatch boundary: direct (min <= 32), one workgroup (N <= 2^12),
+# two passes (2^13..2^22), three passes (2^23+)
+SHAPES = [(1, 1), (33, 33), (32, 1000), (33, 1000), (2048, 2049), (2049, 2048), (4097, 4),
+          (4097, 33), (3000, 5000), (1 << 12, 1 << 12), ((1 << 13) + 1, 999),
+          (1 << 15, (1 << 15) + 1), (100000, 3), (70000, 90000), ((1 << 19), (1 << 19)),
+          ((1 << 20) + 3, (1 << 20) + 5), (3 * (1 << 20) + 4, (1 << 20) + 3)]
+
+
+@pytest.mark.parametrize("la,lb", SHAPES)
+def test_shapes_vs_oracle(hip, oracle, la, lb):
+    a, b = gen.poly_inputs(la * 31 + lb, la, lb)
+    want = oracle.poly_mul(a, b) if la * lb <= (1 << 24) else oracle.poly_mul_ntt(a, b)
+    assert hip.poly_mul(a, b) == want
+
+
+def test_trailing_cancellation_and_zero(hip, oracle):
+    # products whose top coefficients vanish: trimmed length < la + lb - 1
+    a = np.zeros(5000, np.uint8); a[0] = 1; a[4000] = 0   # untrimmed input a = 1
+    b = np.zeros(6000, np.uint8); b[10] = 3
+    assert hip.poly_mul(a, b) == oracle.poly_mul(a, b)
+    z = np.zeros(7000, np.uint8)
+    assert hip.poly_mul(z, z) == bytes([0])
+    # non-canonical coefficient bytes are reduced like hf_mul does
+    a, b = gen.poly_inputs(5, 3000, 3000, modulus=256)
+    assert hip.poly_mul(a, b) == oracle.poly_mul(a, b)
+
+
+def test_empty_operand_mirrors_reference(hip):
+    assert hip.poly_mul(b"", b"\x03\x04") == bytes([0])
+
+
+def test_device_api(hip, oracle):
+    import torch
+    dev = torch.device("cuda:0")
+    la, lb = 300000, 200001
+    a, b = gen.poly_inputs(8, la, lb)
+    da, db = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
+    out = torch.zeros(la + lb - 1, dtype=torch.uint8, device=dev)
+    nz = torch.zeros(4, dtype=torch.int32, device=dev)
+    work = torch.zeros(max(hip.poly_mul_workspace(la, lb), 4), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream()
+    for _ in range(2):
+        hip.poly_mul_dev(da, la, db, lb, out, nz, work, st)
+    torch.cuda.synchronize()
+    n = int(nz[0].item()) or 1
+    assert bytes(out[:n].cpu().numpy()) == oracle.poly_mul_ntt(a, b)
