@@ -1,0 +1,114 @@
+"""The C-ABI boundary without a GPU: libplonkhip.so loads, exports exactly what
+include/plonkhip.h declares, fails loudly (no CPU fallback) when no device is present, and
+the drop-in headers compile -- standalone and under the reference's own plonk.h."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+INCLUDE = os.path.join(ROOT, "include")
+PKG = os.path.join(ROOT, "plonk.c_amd")
+REF_SRC = "/root/reference/src"
+
+
+def declared_symbols():
+    txt = open(os.path.join(INCLUDE, "plonkhip.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(plk_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    import plonkhip
+    lib = plonkhip.lib()
+    decl = declared_symbols()
+    assert len(decl) >= 15
+    for s in decl:
+        assert hasattr(lib, s), s
+    out = subprocess.run(["nm", "-D", "--defined-only", plonkhip.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (plk_\w+)", out))
+    assert exported == set(decl)
+    assert set(plonkhip.SIGNATURES) == set(decl)
+
+
+def test_library_is_gfx950_code():
+    """The fat binary embedded in libplonkhip.so carries gfx950 code objects (and nothing
+    else: no other targets, no host fallback)."""
+    import plonkhip
+    data = open(plonkhip.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in data
+
+
+def test_no_cpu_fallback_without_gpu():
+    import plonkhip
+    if plonkhip.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(plonkhip.PlonkHipError) as e:
+        plonkhip.msm_g1([1, 2, 0], [1])
+    assert e.value.code == plonkhip.PLK_ERR_NODEV
+    with pytest.raises(plonkhip.PlonkHipError):
+        plonkhip.poly_mul([1, 2], [3, 4])
+
+
+def test_host_argument_checks():
+    import plonkhip
+    with pytest.raises(ValueError):
+        plonkhip.msm_g1([1, 2, 0, 1], [1])
+    with pytest.raises(ValueError):
+        plonkhip.srs_eval_at_s([1, 2, 0], [1, 1])
+
+
+def _gcc(args, **kw):
+    return subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Werror", "-I", INCLUDE] + args,
+                          capture_output=True, text=True, **kw)
+
+
+def test_dropin_headers_compile_and_link(tmp_path):
+    src = tmp_path / "use.c"
+    src.write_text('#include "prelude.h"\n'
+                   "int main(void) {\n"
+                   "  SRS srs = srs_create(f101(5), 5);\n"
+                   "  HF c[] = {{1}, {2}, {3}};\n"
+                   "  POLY p = poly_new(c, 3);\n"
+                   "  G1 e = srs_eval_at_s(&srs, &p);\n"
+                   "  POLY q = poly_mul(&p, &p);\n"
+                   "  poly_free(&q); poly_free(&p); srs_free(&srs);\n"
+                   "  return e.infinite ? 0 : 1;\n}\n")
+    r = _gcc([str(src), "-L", PKG, "-lplonkhip", "-o", str(tmp_path / "use")])
+    assert r.returncode == 0, r.stderr
+    # two translation units including the headers link together (static inline, unlike
+    # the reference's single-TU headers)
+    (tmp_path / "a.c").write_text('#include "srs.h"\nG1 fa(void){ return g1_generator(); }\n')
+    (tmp_path / "b.c").write_text('#include "srs.h"\nG1 fa(void);\nint main(void){ G1 g = fa(); '
+                                  'return g.x.value == 1 ? 0 : 1; }\n')
+    r = _gcc([str(tmp_path / "a.c"), str(tmp_path / "b.c"), "-L", PKG, "-lplonkhip",
+              "-o", str(tmp_path / "ab")])
+    assert r.returncode == 0, r.stderr
+
+
+def test_struct_layouts(tmp_path):
+    (tmp_path / "l.c").write_text('#include "prelude.h"\n#include <stdio.h>\n'
+                                  "int main(void){ printf(\"%zu %zu %zu %zu\", sizeof(G1), "
+                                  "sizeof(HF), sizeof(GF), sizeof(plk_msm_result_t)); return 0; }\n")
+    r = _gcc([str(tmp_path / "l.c"), "-o", str(tmp_path / "l")])
+    assert r.returncode == 0, r.stderr
+    out = subprocess.run([str(tmp_path / "l")], capture_output=True, text=True).stdout
+    assert out == "3 1 1 32"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_SRC), reason="reference sources not present")
+def test_reference_plonk_test_compiles_against_dropin(tmp_path):
+    """The reference's unmodified plonk-test.c + plonk.h build with our headers pre-included
+    (the drop-in mechanism); running it needs the GPU (tests/test_dropin_gpu.py)."""
+    r = subprocess.run(["gcc", "-std=gnu11", "-w", "-include", os.path.join(INCLUDE, "prelude.h"),
+                        "-I", INCLUDE, os.path.join(REF_SRC, "plonk-test.c"), "-L", PKG,
+                        "-lplonkhip", "-o", str(tmp_path / "plonk-test")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    nm = subprocess.run(["nm", str(tmp_path / "plonk-test")], capture_output=True, text=True).stdout
+    assert "U plk_poly_mul" in nm and "U plk_msm_g1" in nm

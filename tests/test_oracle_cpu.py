@@ -1,0 +1,144 @@
+"""The oracle (oracle/oracle.c) against golden vectors recorded from the compiled reference.
+
+This pins the checker before any GPU test trusts it: G1 group law tables (all 102 points,
+every pair, every scalar byte), the MSM fold incl. irregular encodings, poly_mul, and the
+independent fast checkers (discrete-log MSM, NTT poly_mul) against the reference."""
+import numpy as np
+import pytest
+
+import gen
+from conftest import load_golden
+
+
+def _b(h):
+    return np.frombuffer(bytes.fromhex(h), np.uint8)
+
+
+@pytest.fixture(scope="module")
+def g1():
+    return load_golden("g1.json")
+
+
+def test_points_are_the_group(g1, oracle):
+    pts = [bytes.fromhex(p) for p in g1["points"]]
+    assert len(pts) == 102 and pts[0] == bytes([0, 0, 1])
+    assert all(oracle.g1_is_on_curve(p) for p in pts)
+    # exactly one affine point per y (cubing is a bijection of GF(101))
+    ys = sorted(p[1] for p in pts[1:])
+    assert ys == list(range(101))
+
+
+def test_add_table(g1, oracle):
+    pts = [bytes.fromhex(p) for p in g1["points"]]
+    table = bytes.fromhex(g1["add_table"])
+    k = 0
+    for a in pts:
+        for b in pts:
+            assert oracle.g1_add(a, b) == table[k:k + 3]
+            k += 3
+
+
+def test_double_and_mul_tables(g1, oracle):
+    pts = [bytes.fromhex(p) for p in g1["points"]]
+    dbl = bytes.fromhex(g1["double_table"])
+    mul = bytes.fromhex(g1["mul_table_k0_255"])
+    for i, p in enumerate(pts):
+        assert oracle.g1_double(p) == dbl[3 * i:3 * i + 3]
+        for k in range(256):
+            o = 3 * (256 * i + k)
+            assert oracle.g1_mul(p, k) == mul[o:o + 3]
+    assert [oracle.g1_mul([1, 2, 0], k).hex() for k in range(18)] == g1["kG_k0_17"]
+    # src/g1-test.c known answers
+    kg = g1["kG_k0_17"]
+    assert kg[2] == "444a00" and kg[3] == "1a2d00" and kg[16] == "016300" and kg[17] == "000001"
+
+
+def test_irregular_group_ops(g1, oracle):
+    for c in g1["irregular"]:
+        a, b = bytes.fromhex(c["a"]), bytes.fromhex(c["b"])
+        assert oracle.g1_add(a, b).hex() == c["add"]
+        assert oracle.g1_double(a).hex() == c["double_a"]
+        assert oracle.g1_mul(a, 7).hex() == c["mul_a_7"]
+
+
+def test_msm_small_cases(oracle):
+    g = load_golden("msm.json")
+    for c in g["cases"] + g["irregular"]:
+        assert oracle.msm(_b(c["points"]), _b(c["scalars"])).hex() == c["out"], c["kind"]
+
+
+def test_msm_large_fold_and_dlog(oracle):
+    g = load_golden("msm.json")
+    for c in g["large"]:
+        pts, sc = gen.msm_inputs(c["seed"], c["n"], c["kind"])
+        lg, pt = oracle.msm_dlog(pts, sc)
+        assert pt.hex() == c["out"], (c["kind"], c["n"])
+        if c["n"] <= (1 << 20) + 3:
+            assert oracle.msm(pts, sc).hex() == c["out"]
+
+
+def test_msm_survey_known_answers(oracle):
+    for c in load_golden("msm.json")["survey_xorshift"]:
+        pts, sc = oracle.gen_survey_msm(c["n"])
+        assert oracle.msm_dlog(pts, sc)[1].hex() == c["out"]
+
+
+def test_dlog_is_a_group_isomorphism(oracle):
+    pts = gen.all_points()
+    gen_pt = oracle.dlog_generator()
+    assert oracle.dlog(gen_pt) == 1
+    logs = [oracle.dlog(p) for p in pts]
+    assert sorted(logs) == list(range(102))
+    rng = np.random.default_rng(0)
+    for _ in range(500):
+        i, j = rng.integers(0, 102, 2)
+        s = oracle.g1_add(pts[i], pts[j])
+        assert oracle.dlog(s) == (logs[i] + logs[j]) % 102
+    # irregular encodings have no log
+    for bad in ([5, 5, 0], [0, 0, 0], [200, 1, 0], [1, 2, 1], [0, 0, 2]):
+        assert oracle.dlog(bad) is None
+
+
+def test_poly_cases(oracle):
+    g = load_golden("poly_mul.json")
+    for c in g["cases"]:
+        a, b = bytes.fromhex(c["a"]), bytes.fromhex(c["b"])
+        assert oracle.poly_mul(a, b).hex() == c["out"]
+        if not c.get("edge"):
+            assert oracle.poly_mul_ntt(a, b).hex() == c["out"]
+
+
+def test_poly_large_digests(oracle):
+    for c in load_golden("poly_mul.json")["large"]:
+        a, b = gen.poly_inputs(c["seed"], c["la"], c["lb"])
+        out = oracle.poly_mul_ntt(a, b)
+        assert len(out) == c["len"]
+        assert gen.digest(np.frombuffer(out, np.uint8)) == c["sha256"]
+        if c["la"] * c["lb"] <= 1 << 24:
+            assert oracle.poly_mul(a, b) == out
+
+
+def test_poly_survey_digests(oracle):
+    for c in load_golden("poly_mul.json")["survey_xorshift"]:
+        a, b = oracle.gen_survey_poly(c["n"])
+        out = oracle.poly_mul_ntt(a, b)
+        assert len(out) == c["len"]
+        assert "%08x" % oracle.digest31(np.frombuffer(out, np.uint8)) == c["digest31"]
+
+
+def test_poly_next_rows(oracle):
+    g = load_golden("poly_next.json")
+    for c in g["divide"]:
+        q, r = oracle.poly_divide(bytes.fromhex(c["num"]), bytes.fromhex(c["den"]))
+        assert (q.hex(), r.hex()) == (c["q"], c["r"])
+    for c in g["eval"]:
+        assert oracle.poly_eval(bytes.fromhex(c["p"]), c["x"]) == c["y"]
+
+
+def test_toy_proof_fixture_shape():
+    g = load_golden("prove.json")
+    base = g["proofs"][0]
+    # src/plonk-test.c toy circuit: all commitments are the identity (srs_create's base is
+    # the identity, src/srs.h:27-36), evaluations a_z..z_omega_z = 15 13 5 1 12 15 15
+    assert base["proof"] == "000001" * 9 + "0f0d05010c0f0f"
+    assert all(len(bytes.fromhex(p["proof"])) == 34 for p in g["proofs"])
