@@ -33,6 +33,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--log2n", type=int, default=22)
+    ap.add_argument("--msm-batch", type=int, default=8,
+                    help="MSMs per kernel launch (plk_msm_g1_batch_dev); every MSM is one step")
     ap.add_argument("--rotate-mib", type=int, default=640)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -58,17 +60,21 @@ def make_msm_sets(torch, n, sets, dev, seed):
     return pts, sc
 
 
-def event_avg_ms(torch, st, fn, reps):
-    """Average device duration of fn() measured by an event pair around each call on st."""
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(reps)]
-    for i in range(reps):
-        evs[i][0].record(st)
-        fn(i)
-        evs[i][1].record(st)
-    torch.cuda.synchronize()
-    ts = sorted(a.elapsed_time(b) for a, b in evs)
-    return sum(ts) / len(ts), ts[len(ts) // 2]
+def event_avg_ms(torch, st, fn, reps, rounds=3):
+    """Device time per call of fn(i): one event pair around `reps` back-to-back calls on st
+    (includes launch gaps; a pair per call would add ~6 us of event overhead each).
+    Returns (best, median) over `rounds` rounds."""
+    per = []
+    for r in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for i in range(reps):
+            fn(r * reps + i)
+        e1.record(st)
+        torch.cuda.synchronize()
+        per.append(e0.elapsed_time(e1) / reps)
+    per.sort()
+    return per[0], per[len(per) // 2]
 
 
 def cpu_baseline(pts_np, sc_np, budget_s, gpu_g1):
@@ -100,17 +106,18 @@ def components(torch, hip, dev, st):
     # C2: 2^16-point MSM -- device-resident kernel time and host-buffer call (PCIe incl.)
     n = 1 << 16
     pts, sc = make_msm_sets(torch, n, 8, dev, 7)
-    res = torch.zeros((64, 32), dtype=torch.uint8, device=dev)
-    avg, med = event_avg_ms(torch, st, lambda i: hip.msm_g1_dev(pts[i % 8], sc[i % 8], n, res[i], st), 64)
+    res = torch.zeros((64, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
+    avg, med = event_avg_ms(torch, st, lambda i: hip.msm_g1_dev(pts[i % 8], sc[i % 8], n, res[i % 64], st), 64)
     ph, sh = pts[0].cpu().numpy(), sc[0].cpu().numpy()
     hip.msm_g1(ph, sh)
     t0 = time.perf_counter()
     for _ in range(20):
         hip.msm_g1(ph, sh)
     host_us = (time.perf_counter() - t0) / 20 * 1e6
-    out["msm_2^16"] = {"kernel_us": round(avg * 1e3, 2), "kernel_us_median": round(med * 1e3, 2),
-                       "Mpoint_s_kernel": round(n / (avg * 1e-3) / 1e6, 1),
-                       "host_call_us_incl_pcie": round(host_us, 1)}
+    out["msm_2^16"] = {"device_us_per_msm": round(avg * 1e3, 2), "median_us": round(med * 1e3, 2),
+                       "Mpoint_s": round(n / (avg * 1e-3) / 1e6, 1),
+                       "host_call_us_incl_pcie": round(host_us, 1),
+                       "note": "one launch per MSM, back-to-back on one stream"}
     # C3: forward NTT 2^20 over BabyBear (Montgomery u32, in place, 2 passes)
     k = 20
     bufs = [torch.randint(0, 2013265921, (1 << k,), dtype=torch.int64, device=dev).to(torch.int32)
@@ -156,26 +163,32 @@ def main():
     st = torch.cuda.current_stream()
 
     n = 1 << args.log2n
-    sets = max(2, -(-args.rotate_mib * (1 << 20) // (MSM_BYTES_PER_POINT * n)))
+    B = max(1, args.msm_batch)
+    sets = max(2 * B, -(-args.rotate_mib * (1 << 20) // (MSM_BYTES_PER_POINT * n)))
+    sets = -(-sets // B) * B                       # whole launches never wrap the rotation
     pts, sc = make_msm_sets(torch, n, sets, dev, 1234 + rank)
     K, W = args.steps, args.warmup
-    res = torch.zeros((W + K, 32), dtype=torch.uint8, device=dev)
+    res = torch.zeros((W + K, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
     outs = torch.zeros((K, 4), dtype=torch.uint8, device=dev)
 
-    def step(i):
-        s = i % sets
-        hip.msm_g1_dev(pts[s], sc[s], n, res[i], st)
+    def launch(first, count):
+        """MSMs first .. first+count-1 (one result record each), B per launch; MSM i reads
+        input set i mod sets."""
+        i = first
+        while i < first + count:
+            b = min(B, first + count - i, sets - i % sets)
+            s0 = i % sets
+            hip.msm_g1_batch_dev(pts[s0], 3 * n, sc[s0], n, n, b, res[i], st)
+            i += b
 
-    for i in range(W):
-        step(i)
+    launch(0, W)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(W, W + K):
-        step(i)
-    logs = res[W:].view(torch.int32)[:, 2].contiguous()
+    launch(W, K)
+    logs = res[W:].view(torch.int32)[:, hip.MSM_LOG_OFFSET // 4].contiguous()
     if world > 1:
         dist.all_reduce(logs, op=dist.ReduceOp.SUM)
     hip.msm_finalize_dev(logs, K, 1, outs, st)
@@ -188,19 +201,29 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    irregular = int(res[:, 12:16].view(torch.int32).sum().item())
+    irregular = int(res[:, hip.MSM_IRREGULAR_OFFSET:hip.MSM_IRREGULAR_OFFSET + 4].view(torch.int32).sum().item())
     if args.profile_only:
         if world > 1:
             dist.destroy_process_group()
         return
 
-    # kernel-level timing for the roofline: an event pair around every launch, same stream
-    reps = max(50, min(400, K))
-    off = W + K
-    res2 = torch.zeros((reps, 32), dtype=torch.uint8, device=dev)
-    avg_ms, med_ms = event_avg_ms(torch, st, lambda i: hip.msm_g1_dev(pts[(off + i) % sets], sc[(off + i) % sets],
-                                                                       n, res2[i], st), reps)
-    alg = MSM_BYTES_PER_POINT * n
+    # Kernel-level timing for the roofline, on the stream the kernel runs on: one event pair
+    # around L back-to-back launches of B MSMs (a pair around every launch would add its
+    # own ~6 us per pair); the average includes the launch gaps, so it is an upper bound on
+    # the kernel duration that rocprofv3 reports for the same command.
+    L = max(8, min(64, K // B))
+    res2 = torch.zeros((L * B, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    base = W + K
+    e0.record(st)
+    for j in range(L):
+        s0 = (base + j * B) % sets
+        s0 -= s0 % B
+        hip.msm_g1_batch_dev(pts[s0], 3 * n, sc[s0], n, n, B, res2[j * B], st)
+    e1.record(st)
+    torch.cuda.synchronize()
+    avg_ms = e0.elapsed_time(e1) / L
+    alg = MSM_BYTES_PER_POINT * n * B
     achieved = alg / (avg_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "msm_pmc_latest.json")
@@ -208,7 +231,7 @@ def main():
         try:
             with open(pmc) as f:
                 j = json.load(f)
-            if j.get("log2n") == args.log2n:
+            if j.get("log2n") == args.log2n and j.get("msm_batch") == B:
                 traffic = j.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
@@ -226,26 +249,36 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic: SRS points kG (k uniform 1..16), HF scalars uniform 0..16, %d input "
-                "sets (%d MiB) rotated per step, resident in HBM" % (sets, sets * alg >> 20),
-        "config": {"workload": "2^%d-point G1 MSM per GPU (srs_eval_at_s), point-range sharded"
-                               " over %d GPU(s), one RCCL all-reduce of partial logs per batch"
+        "data": "synthetic: SRS points kG (k uniform 1..16), HF scalars uniform 0..16, %d distinct "
+                "input sets (%d MiB) rotated so every step reads cold data, resident in HBM"
+                % (sets, sets * MSM_BYTES_PER_POINT * n >> 20),
+        "config": {"workload": "2^%d-point G1 MSM (srs_eval_at_s) per GPU per step, point-range "
+                               "sharded over %d GPU(s); one RCCL all-reduce of the K partial logs"
                                % (args.log2n, world),
-                   "points_per_gpu": n, "parallelism": "dp%d" % world},
+                   "points_per_gpu": n, "msms_per_launch": B, "parallelism": "dp%d" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": "msm_dlog_kernel<true>",
-                     "kernel_ms_avg": round(avg_ms, 5), "kernel_ms_median": round(med_ms, 5),
-                     "alg_bytes_per_launch": alg},
+                     "traffic": traffic, "kernel": "msm_dlog_kernel<true,1024,false>",
+                     "launch_ms_avg": round(avg_ms, 5), "alg_bytes_per_launch": alg,
+                     "timing": "hipEvent pair around %d back-to-back launches on the kernel's "
+                               "stream" % L},
         "irregular_inputs": irregular,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         torch.cuda.synchronize()
-        gpu_g1 = bytes(res[0, 16:19].cpu().numpy())
+        gpu_g1 = bytes(res[0, hip.MSM_G1_OFFSET:hip.MSM_G1_OFFSET + 3].cpu().numpy())
         line["cpu_baseline"] = cpu_baseline(pts[0].cpu().numpy(), sc[0].cpu().numpy(),
                                             args.cpu_seconds, gpu_g1)
     if rank == 0 and not args.no_components:
-        line["components"] = components(torch, hip, dev, st)
+        comp = components(torch, hip, dev, st)
+        r1 = torch.zeros((64, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
+        avg1, med1 = event_avg_ms(torch, st, lambda i: hip.msm_g1_dev(pts[i % sets], sc[i % sets], n,
+                                                                       r1[i % 64], st), 64)
+        comp["msm_2^%d_one_per_launch" % args.log2n] = {
+            "device_us_per_msm": round(avg1 * 1e3, 2), "median_us": round(med1 * 1e3, 2),
+            "GB_s": round(MSM_BYTES_PER_POINT * n / (avg1 * 1e-3) / 1e9, 1),
+            "note": "unbatched: one launch per MSM, back-to-back on one stream"}
+        line["components"] = comp
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -35,7 +35,6 @@ __constant__ uint8_t c_inv101[PLK_GF_P];       // a^-1 mod 101 (0 -> 0), for the
 
 namespace {
 
-constexpr int MSM_MAX_THREADS = 1024;
 constexpr int COPIES = 32;                     // one table copy per LDS bank
 constexpr int TAB_ENTRIES = 512;
 
@@ -63,13 +62,24 @@ __device__ __forceinline__ uint32_t point_term(uint32_t k, uint32_t c, const uin
   return (d & 0xFFu) * c;
 }
 
-__device__ __forceinline__ void fill_table(uint32_t* tab, uint32_t nthreads) {
-  uint4* t4 = reinterpret_cast<uint4*>(tab);
-  for (uint32_t q = threadIdx.x; q < TAB_ENTRIES * COPIES / 4; q += nthreads) {
-    const uint32_t v = c_ytab[q / (COPIES / 4)];
-    t4[q] = make_uint4(v, v, v, v);
+// Table fill in two halves so the caller can put the point loads between them: the table
+// source words are loaded FIRST, the group loads after, and the LDS writes then wait with a
+// counted vmcnt for the table words only (a fill loop that waits vmcnt(0) would also wait
+// for the whole first group to arrive from HBM -- ~2 us per launch).
+template <int NT>
+struct TableFill {
+  static constexpr int PER = TAB_ENTRIES * COPIES / 4 / NT;   // uint4 stores per thread
+  uint32_t v[PER];
+  __device__ __forceinline__ void load() {
+#pragma unroll
+    for (int j = 0; j < PER; j++) v[j] = c_ytab[(threadIdx.x + j * NT) / (COPIES / 4)];
   }
-}
+  __device__ __forceinline__ void store(uint32_t* tab) const {
+    uint4* t4 = reinterpret_cast<uint4*>(tab);
+#pragma unroll
+    for (int j = 0; j < PER; j++) t4[threadIdx.x + j * NT] = make_uint4(v[j], v[j], v[j], v[j]);
+  }
+};
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
@@ -115,48 +125,59 @@ __device__ __forceinline__ uint32_t group_sum(const Group& g, const uint32_t* ta
 }  // namespace
 
 // One launch = a batch of gridDim.y MSMs of n points each (points/scalars of MSM b at
-// pts + b * pstride, sc + b * sstride; result record res[b]).  Every block reduces its
-// points to a partial log (< 102) and adds
-//   partial | 1 << 32 | (irregular ? 1 << 48 : 0)
-// to res[b].acc with ONE 64-bit device-scope atomic.  The block whose ticket field comes back
-// as gridDim.x - 1 owns the complete sum (old + own add) -- no extra fence or re-read -- and
-// writes log / irregular / g1, then re-arms acc for the next launch on the stream.
-template <bool ALIGNED>
-__global__ __launch_bounds__(MSM_MAX_THREADS) void msm_dlog_kernel(const uint8_t* __restrict__ pts_base,
-                                                                   uint64_t pstride,
-                                                                   const uint8_t* __restrict__ sc_base,
-                                                                   uint64_t sstride, uint64_t n,
-                                                                   PlkMsmResult* res_base) {
+// pts + b * pstride, sc + b * sstride; result record res[b]); gridDim.x blocks per MSM,
+// each striding over its MSM's 16-point groups with the next group's loads in flight.
+//
+// Finish without a second launch: every block reduces its points to a partial log (< 102)
+// and adds   partial | 1 << 32 | (irregular ? 1 << 48 : 0)   with ONE 64-bit device-scope
+// atomic to the shard word res[b].shard[s], s = (linear block id) mod 8 -- blocks are dealt
+// round-robin over the 8 XCDs, so a shard is (for speed only) one XCD's blocks and no
+// word sees more than ~32 arrivals (one hot word for 256 arrivals costs ~3 us).  The block
+// whose ticket comes back as (shard size - 1) owns the shard's complete sum (old + own add,
+// no fence or re-read needed), re-arms the shard word and adds the shard total to
+// res[b].top the same way; the last shard's finisher writes log / irregular / g1 and
+// re-arms top.  Every word is zero again when the launch ends.
+template <bool ALIGNED, int NT, bool SHARDED>
+__global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* __restrict__ pts_base, uint64_t pstride,
+                                                      const uint8_t* __restrict__ sc_base, uint64_t sstride,
+                                                      uint64_t n, PlkMsmResult* res_base) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[TAB_ENTRIES * COPIES];
-  __shared__ uint32_t wsum[MSM_MAX_THREADS / PLK_WAVE];
-  __shared__ uint32_t wbad[MSM_MAX_THREADS / PLK_WAVE];
+  __shared__ uint32_t wsum[NT / PLK_WAVE];
+  __shared__ uint32_t wbad[NT / PLK_WAVE];
   const uint8_t* pts = pts_base + (uint64_t)blockIdx.y * pstride;
   const uint8_t* sc = sc_base + (uint64_t)blockIdx.y * sstride;
   PlkMsmResult* res = res_base + blockIdx.y;
 
-  const uint32_t nthreads = blockDim.x;
-  const uint64_t tid = (uint64_t)blockIdx.x * nthreads + threadIdx.x;
-  const uint64_t stride = (uint64_t)gridDim.x * nthreads;
+  const uint64_t tid = (uint64_t)blockIdx.x * NT + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * NT;
   const uint32_t lane4 = (threadIdx.x & 31u) << 2;
   uint32_t acc = 0;
   bool bad = false;
+  TableFill<NT> fill;
+  fill.load();                                  // table words first ...
 
-  if (ALIGNED) {
-    // 16 points per thread-step: 48 B of points (3 x dwordx4) + 16 B of scalars (1 x dwordx4);
-    // the first group's loads are in flight while the table is built.
-    const uint64_t ngroups = n >> 4;
+  const uint64_t ngroups = n >> 4;
+  if (ALIGNED && ngroups > 0) {
+    // 16 points per thread-step: 48 B of points (3 x dwordx4) + 16 B of scalars (1 x dwordx4)
     const uint4* p4 = reinterpret_cast<const uint4*>(pts);
     const uint4* s4 = reinterpret_cast<const uint4*>(sc);
     uint64_t g = tid;
-    Group cur;
-    if (g < ngroups) cur = load_group(p4, s4, g);
-    fill_table(tab, nthreads);
+    // ... then the first group, unconditionally: a clamped index (threads past the end
+    // re-read group 0 and drop its sum) so the loads cannot be sunk below the fill, and
+    // the compiler's vmcnt bookkeeping sees 4 table words older than 4 group loads ...
+    asm volatile("" ::: "memory");
+    Group cur = load_group(p4, s4, g < ngroups ? g : 0);
+    asm volatile("" ::: "memory");
+    fill.store(tab);                                  // ... LDS fill waits for the table words only
     __syncthreads();
-    while (g < ngroups) {
+    for (;;) {
       const uint64_t nx = g + stride;
+      const bool more = nx < ngroups;
       Group nxt;
-      if (nx < ngroups) nxt = load_group(p4, s4, nx);
-      acc += group_sum(cur, tab, lane4, bad) % PLK_GROUP_ORDER;
+      if (more) nxt = load_group(p4, s4, nx);
+      const uint32_t part = group_sum(cur, tab, lane4, bad) % PLK_GROUP_ORDER;
+      acc += g < ngroups ? part : 0u;
+      if (!more) break;
       cur = nxt;
       g = nx;
     }
@@ -167,7 +188,7 @@ __global__ __launch_bounds__(MSM_MAX_THREADS) void msm_dlog_kernel(const uint8_t
       acc += point_term(encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), sc[i], tab, lane4, bad);
     }
   } else {
-    fill_table(tab, nthreads);
+    fill.store(tab);
     __syncthreads();
     for (uint64_t i = tid; i < n; i += stride) {
       acc += point_term(encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), sc[i], tab, lane4, bad);
@@ -184,27 +205,42 @@ __global__ __launch_bounds__(MSM_MAX_THREADS) void msm_dlog_kernel(const uint8_t
     wbad[wave] = anybad != 0;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t bs = 0, bb_ = 0;
-    for (uint32_t k = 0; k < nthreads / PLK_WAVE; k++) {
-      bs += wsum[k];
-      bb_ |= wbad[k];
-    }
-    const unsigned long long add =
-        (unsigned long long)(bs % PLK_GROUP_ORDER) | (1ull << 32) | ((unsigned long long)bb_ << 48);
-    const unsigned long long old = atomicAdd(&res->acc, add);
-    if (((old >> 32) & 0xFFFFull) == gridDim.x - 1) {
-      const unsigned long long tot = old + add;
-      const uint32_t lg = (uint32_t)(tot & 0xFFFFFFFFull) % PLK_GROUP_ORDER;
-      res->log = lg;
-      res->irregular = (uint32_t)(tot >> 48);
-      res->g1[0] = c_exp[4 * lg + 0];
-      res->g1[1] = c_exp[4 * lg + 1];
-      res->g1[2] = c_exp[4 * lg + 2];
-      res->g1[3] = 0;
-      atomicExch(&res->acc, 0ull);
-    }
+  if (threadIdx.x != 0) return;
+  uint32_t bs = 0, bb_ = 0;
+#pragma unroll
+  for (int k = 0; k < NT / PLK_WAVE; k++) {
+    bs += wsum[k];
+    bb_ |= wbad[k];
   }
+  const uint32_t X = gridDim.x;
+  unsigned long long add =
+      (unsigned long long)(bs % PLK_GROUP_ORDER) | (1ull << 32) | ((unsigned long long)(bb_ != 0) << 48);
+  uint32_t arrivals = X;                       // expected arrivals on res->top
+  if (SHARDED) {
+    const uint32_t lin = blockIdx.y * X + blockIdx.x;
+    const uint32_t sh = lin % PLK_MSM_SHARDS;
+    // blocks of this MSM in shard sh: x in [0, X) with (y X + x) = sh (mod 8)
+    const uint32_t r = (sh + PLK_MSM_SHARDS - (blockIdx.y * X) % PLK_MSM_SHARDS) % PLK_MSM_SHARDS;
+    const uint32_t in_shard = r < X ? (X - r + PLK_MSM_SHARDS - 1) / PLK_MSM_SHARDS : 0u;
+    const unsigned long long old = atomicAdd(&res->shard[sh], add);
+    if (((old >> 32) & 0xFFFFull) != in_shard - 1) return;
+    const unsigned long long tot = old + add;
+    atomicExch(&res->shard[sh], 0ull);
+    add = (unsigned long long)((uint32_t)(tot & 0xFFFFFFFFull) % PLK_GROUP_ORDER) | (1ull << 32) |
+          ((unsigned long long)((tot >> 48) != 0) << 48);
+    arrivals = X < PLK_MSM_SHARDS ? X : PLK_MSM_SHARDS;
+  }
+  const unsigned long long old = atomicAdd(&res->top, add);
+  if (((old >> 32) & 0xFFFFull) != arrivals - 1) return;
+  const unsigned long long tot = old + add;
+  const uint32_t lg = (uint32_t)(tot & 0xFFFFFFFFull) % PLK_GROUP_ORDER;
+  res->log = lg;
+  res->irregular = (uint32_t)(tot >> 48);
+  res->g1[0] = c_exp[4 * lg + 0];
+  res->g1[1] = c_exp[4 * lg + 1];
+  res->g1[2] = c_exp[4 * lg + 2];
+  res->g1[3] = 0;
+  atomicExch(&res->top, 0ull);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -297,10 +333,12 @@ int plk_msm_upload_tables(const uint32_t* ytab, const uint8_t* exp4, const uint8
 }
 
 // Launch geometry: one 16-point group per thread per pass.  Big MSMs use 1024-thread
-// blocks (one 32 KB table per CU, 16 waves, every load of the CU's share in flight at
-// once); small ones 256-thread blocks so they still spread over many CUs.  Overridable
-// for tuning with PLK_MSM_THREADS / PLK_MSM_MAX_BLOCKS.
-void plk_msm_geometry(uint64_t n, int* threads, int* blocks) {
+// blocks (one 64 KB table per CU, 16 waves, the CU's share of loads in flight at once);
+// small ones 256-thread blocks so they still spread over many CUs.  A batch shares the
+// chip: ~256 blocks in total, so each block loops over its MSM's groups with the next
+// group's loads in flight instead of paying table fill + drain per 16 KB.
+// Overridable for tuning with PLK_MSM_THREADS / PLK_MSM_MAX_BLOCKS.
+void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks) {
   static int env_threads = -1, env_blocks = -1;
   if (env_threads < 0) {
     const char* t = getenv("PLK_MSM_THREADS");
@@ -312,7 +350,8 @@ void plk_msm_geometry(uint64_t n, int* threads, int* blocks) {
   int th = groups >= 256ull * 1024 ? 1024 : 256;
   if (env_threads == 256 || env_threads == 512 || env_threads == 1024) th = env_threads;
   uint64_t b = (groups + th - 1) / th;
-  const uint64_t cap = env_blocks > 0 ? (uint64_t)env_blocks : (th == 1024 ? 512 : 2048);
+  uint64_t cap = env_blocks > 0 ? (uint64_t)env_blocks : (th == 1024 ? 256 : 1024);
+  if (batch > 1) cap = cap / (uint64_t)batch > 1 ? cap / (uint64_t)batch : 1;
   if (b > cap) b = cap;
   if (b < 1) b = 1;
   *threads = th;
@@ -327,15 +366,28 @@ int plk_msm_batch_launch(const uint8_t* d_pts, uint64_t pstride, const uint8_t* 
     return PLK_ERR_RANGE;
   }
   int threads, blocks;
-  plk_msm_geometry(n, &threads, &blocks);
+  plk_msm_geometry(n, batch, &threads, &blocks);
+  static int sharded = -1;
+  if (sharded < 0) {
+    const char* e = getenv("PLK_MSM_SHARDED");
+    sharded = e ? atoi(e) != 0 : 0;
+  }
   const bool aligned = ((uintptr_t)d_pts % 16 == 0) && ((uintptr_t)d_sc % 16 == 0) &&
                        (batch == 1 || (pstride % 16 == 0 && sstride % 16 == 0));
-  if (aligned)
-    hipLaunchKernelGGL(msm_dlog_kernel<true>, dim3(blocks, batch), dim3(threads), 0, st, d_pts, pstride, d_sc,
-                       sstride, n, d_res);
-  else
-    hipLaunchKernelGGL(msm_dlog_kernel<false>, dim3(blocks, batch), dim3(threads), 0, st, d_pts, pstride, d_sc,
-                       sstride, n, d_res);
+  const dim3 grid(blocks, batch);
+#define PLK_MSM_GO(A, T, S) \
+  hipLaunchKernelGGL((msm_dlog_kernel<A, T, S>), grid, dim3(T), 0, st, d_pts, pstride, d_sc, sstride, n, d_res)
+  if (threads == 1024) {
+    if (aligned) { if (sharded) PLK_MSM_GO(true, 1024, true); else PLK_MSM_GO(true, 1024, false); }
+    else { if (sharded) PLK_MSM_GO(false, 1024, true); else PLK_MSM_GO(false, 1024, false); }
+  } else if (threads == 512) {
+    if (aligned) { if (sharded) PLK_MSM_GO(true, 512, true); else PLK_MSM_GO(true, 512, false); }
+    else { if (sharded) PLK_MSM_GO(false, 512, true); else PLK_MSM_GO(false, 512, false); }
+  } else {
+    if (aligned) { if (sharded) PLK_MSM_GO(true, 256, true); else PLK_MSM_GO(true, 256, false); }
+    else { if (sharded) PLK_MSM_GO(false, 256, true); else PLK_MSM_GO(false, 256, false); }
+  }
+#undef PLK_MSM_GO
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }

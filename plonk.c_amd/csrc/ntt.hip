@@ -35,7 +35,14 @@ __constant__ uint32_t c_mont17[17];            // v * R mod p for v = 0..16
 
 namespace {
 
-constexpr int NTT_THREADS = 256;
+constexpr int NTT_THREADS = 512;
+constexpr int PAD = 4;
+
+// LDS row padding: one spare word after every 32 rows, so the strided element accesses of
+// the low-stride rounds (lanes at base = 2^R g) hit distinct banks instead of 2^R-way
+// conflicts.  Column stride RS = phys(rows) + PAD.
+__device__ __forceinline__ int phys(int r) { return r + (r >> 5); }
+__host__ __device__ constexpr int col_stride(int rows) { return rows + (rows >> 5) + PAD; }
 
 struct Tw {
   const uint32_t* small;   // T[2^j + r] = w_{2^(j+1)}^r  (Montgomery), 2^PLK_NTT_SMALL_LOG
@@ -52,9 +59,10 @@ struct Pass {
   int k;       // log2 N
   int lo;      // lowest bit of this pass
   int M;       // bits in this pass (rows = 2^M)
-  int C;       // columns per tile
+  int C;       // columns per tile (power of two; >= 4 when lo > 0)
 };
 
+// global index of (row r, column c) of tile t
 __device__ __forceinline__ uint64_t tile_index(const Pass& p, uint32_t t, int r, int c) {
   if (p.lo == 0) return (((uint64_t)t * p.C + c) << p.M) | (uint64_t)r;
   const uint32_t per_h = (1u << p.lo) / p.C;
@@ -63,13 +71,7 @@ __device__ __forceinline__ uint64_t tile_index(const Pass& p, uint32_t t, int r,
   return (H << (p.lo + p.M)) | ((uint64_t)r << p.lo) | L;
 }
 
-// element e of the tile in global-coalescing order -> (r, c)
-__device__ __forceinline__ void tile_rc(const Pass& p, int e, int& r, int& c) {
-  if (p.lo == 0) { r = e & ((1 << p.M) - 1); c = e >> p.M; }
-  else { c = e % p.C; r = e / p.C; }
-}
-
-// F[c][j] for the tile's columns (only when lo > 0)
+// F[c][j] = w_{2^27}^(L * 2^(26-lo-j)) for the tile's columns (only when lo > 0)
 __device__ void column_factors(const Pass& p, uint32_t t, const Tw& tw, uint32_t* F) {
   if (p.lo == 0) return;
   const uint32_t per_h = (1u << p.lo) / p.C;
@@ -83,36 +85,135 @@ __device__ void column_factors(const Pass& p, uint32_t t, const Tw& tw, uint32_t
   }
 }
 
-// All M radix-2 stages of one tile held in LDS as X[c * RS + r].
-// DIF: j = M-1 .. 0, (u, v) -> (u + v, (u - v) w).  DIT: j = 0 .. M-1, (u, v w) -> (u + v w, u - v w).
+// ---- global <-> LDS tile movement, 4 elements per thread-step --------------------------
+// lo == 0: the tile is C contiguous runs of 2^M; 4 consecutive rows of one column.
+// lo  > 0: rows of C contiguous elements; 4 consecutive columns of one row.
+// LDS layout X[c * RS + phys(r)], RS = col_stride(2^M).
+template <bool U8>
+__device__ __forceinline__ void load_tile(const Pass& p, uint32_t t, uint32_t* X, int RS, const uint32_t* d,
+                                          const uint8_t* s8, uint64_t ls) {
+  const int rows = 1 << p.M;
+  if (p.lo == 0 && p.M < 2) {                  // tiny single-pass transforms
+    for (int e = threadIdx.x; e < rows * p.C; e += blockDim.x) {
+      const int r = e & (rows - 1), c = e >> p.M;
+      const uint64_t idx = tile_index(p, t, r, c);
+      X[c * RS + phys(r)] = U8 ? (idx < ls ? c_mont17[s8[idx] % 17u] : 0u) : d[idx];
+    }
+    return;
+  }
+  const int E4 = (rows * p.C) >> 2;
+  for (int e = threadIdx.x; e < E4; e += blockDim.x) {
+    int r, c;
+    bool colrun;
+    if (p.lo == 0) { c = (4 * e) >> p.M; r = (4 * e) & (rows - 1); colrun = true; }
+    else { r = (4 * e) / p.C; c = (4 * e) % p.C; colrun = false; }
+    const uint64_t idx = tile_index(p, t, r, c);
+    uint32_t v[4];
+    if (U8) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) v[i] = idx + i < ls ? c_mont17[s8[idx + i] % 17u] : 0u;
+    } else {
+      const uint4 q = *reinterpret_cast<const uint4*>(d + idx);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    }
+    if (colrun) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) X[c * RS + phys(r) + i] = v[i];   // r % 4 == 0: one 32-row block
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; i++) X[(c + i) * RS + phys(r)] = v[i];
+    }
+  }
+}
+
+__device__ __forceinline__ void store_tile(const Pass& p, uint32_t t, const uint32_t* X, int RS, uint32_t* d) {
+  const int rows = 1 << p.M;
+  if (p.lo == 0 && p.M < 2) {
+    for (int e = threadIdx.x; e < rows * p.C; e += blockDim.x) {
+      const int r = e & (rows - 1), c = e >> p.M;
+      d[tile_index(p, t, r, c)] = X[c * RS + phys(r)];
+    }
+    return;
+  }
+  const int E4 = (rows * p.C) >> 2;
+  for (int e = threadIdx.x; e < E4; e += blockDim.x) {
+    int r, c;
+    uint4 q;
+    if (p.lo == 0) {
+      c = (4 * e) >> p.M; r = (4 * e) & (rows - 1);
+      const uint32_t* x = X + c * RS + phys(r);
+      q = make_uint4(x[0], x[1], x[2], x[3]);
+    } else {
+      r = (4 * e) / p.C; c = (4 * e) % p.C;
+      const int pr = phys(r);
+      q = make_uint4(X[c * RS + pr], X[(c + 1) * RS + pr], X[(c + 2) * RS + pr], X[(c + 3) * RS + pr]);
+    }
+    *reinterpret_cast<uint4*>(d + tile_index(p, t, r, c)) = q;
+  }
+}
+
+// ---- radix-2^R rounds in registers -------------------------------------------------------
+// DIF stages j, j-1, .., j-R+1 on the 2^R elements {base + k 2^(j-R+1)} of one column:
+// (u, v) -> (u + v, (u - v) w), w = T[2^s + (row mod 2^s)] (* F[c][s] when lo > 0).
+template <int R, bool INV>
+__device__ __forceinline__ void round_r(uint32_t* X, int M, int C, int RS, int top, const uint32_t* Tsm,
+                                       const uint32_t* F, bool has_f) {
+  constexpr int NE = 1 << R;
+  const int lowbit = INV ? top : top - R + 1;      // lowest stage bit of this round
+  const int hstride = 1 << lowbit;
+  const int ng = C << (M - R);
+  for (int gi = threadIdx.x; gi < ng; gi += blockDim.x) {
+    const int c = gi >> (M - R);
+    const int g = gi & ((1 << (M - R)) - 1);
+    const int base = (g & (hstride - 1)) | ((g >> lowbit) << (lowbit + R));
+    uint32_t* col = X + c * RS;
+    uint32_t v[NE];
+#pragma unroll
+    for (int k = 0; k < NE; k++) v[k] = col[phys(base + k * hstride)];
+#pragma unroll
+    for (int t = 0; t < R; t++) {
+      const int kb = INV ? t : (R - 1 - t);          // k-bit of this stage
+      const int s = lowbit + kb;                     // stage = row bit
+      const int hk = 1 << kb;
+#pragma unroll
+      for (int k = 0; k < NE; k++) {
+        if (k & hk) continue;
+        const int rr = (base + k * hstride) & ((1 << s) - 1);
+        uint32_t w = Tsm[(1 << s) + rr];
+        if (has_f) w = bb::mmul(w, F[c * M + s]);
+        const uint32_t u = v[k], x = v[k + hk];
+        if (!INV) {
+          v[k] = bb::madd(u, x);
+          v[k + hk] = bb::mmul(bb::msub(u, x), w);
+        } else {
+          const uint32_t xw = bb::mmul(x, w);
+          v[k] = bb::madd(u, xw);
+          v[k + hk] = bb::msub(u, xw);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NE; k++) col[phys(base + k * hstride)] = v[k];
+  }
+  __syncthreads();
+}
+
+// All M stages of a tile: DIF top-down / DIT bottom-up, in rounds of up to 4 stages.
 template <bool INV>
 __device__ void tile_stages(uint32_t* X, int M, int C, int RS, const uint32_t* Tsm, const uint32_t* F,
                             bool has_f) {
-  const int half = 1 << (M - 1);
-  const int nb = C * half;
-  for (int s = 0; s < M; s++) {
-    const int j = INV ? s : (M - 1 - s);
-    const int h = 1 << j;
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-      const int c = b >> (M - 1);
-      const int q = b & (half - 1);
-      const int rr = q & (h - 1);
-      const int r = ((q >> j) << (j + 1)) | rr;
-      uint32_t w = Tsm[h + rr];
-      if (has_f) w = bb::mmul(w, F[c * M + j]);
-      uint32_t* pu = X + c * RS + r;
-      uint32_t* pv = pu + h;
-      const uint32_t u = *pu, v = *pv;
-      if (!INV) {
-        *pu = bb::madd(u, v);
-        *pv = bb::mmul(bb::msub(u, v), w);
-      } else {
-        const uint32_t vw = bb::mmul(v, w);
-        *pu = bb::madd(u, vw);
-        *pv = bb::msub(u, vw);
-      }
+  int done = 0;
+  while (done < M) {
+    const int left = M - done;
+    const int R = left >= 4 ? 4 : left;
+    const int top = INV ? done : (M - 1 - done);
+    switch (R) {
+      case 4: round_r<4, INV>(X, M, C, RS, top, Tsm, F, has_f); break;
+      case 3: round_r<3, INV>(X, M, C, RS, top, Tsm, F, has_f); break;
+      case 2: round_r<2, INV>(X, M, C, RS, top, Tsm, F, has_f); break;
+      default: round_r<1, INV>(X, M, C, RS, top, Tsm, F, has_f); break;
     }
-    __syncthreads();
+    done += R;
   }
 }
 
@@ -122,70 +223,59 @@ __device__ void tile_stages(uint32_t* X, int M, int C, int RS, const uint32_t* T
 enum : int { IN_U32 = 0, IN_U8 = 1 };
 enum : int { OUT_U32 = 0, OUT_U8 = 1 };
 
-// One NTT pass over `batch` arrays (blockIdx.y).  IN_U8: arrays are byte vectors of length
-// len_in[y] (zero-padded, reduced mod 17, converted to Montgomery).  OUT_U8: the final
-// inverse pass: scale by N^-1 (normal form -> leaves Montgomery), mod 17, bytes to out8 for
-// idx < out_len, max non-zero idx + 1 -> *nz (atomicMax).
+// One NTT pass over 1 or 2 arrays (blockIdx.y).  IN_U8: arrays are byte vectors of length
+// la / lb (zero-padded, reduced mod 17, converted to Montgomery).  OUT_U8: the final inverse
+// pass: scale by N^-1 given in normal form (which also leaves Montgomery form), mod 17,
+// bytes to out8 for idx < out_len; max non-zero idx + 1 -> *nz (atomicMax).
 template <bool INV, int IN, int OUT>
 __global__ __launch_bounds__(NTT_THREADS) void ntt_pass_kernel(
     Pass p, uint32_t* d0, uint32_t* d1, const uint8_t* a8, const uint8_t* b8, uint64_t la, uint64_t lb,
     Tw tw, uint8_t* out8, uint64_t out_len, uint32_t ninv, uint32_t* nz) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int rows = 1 << p.M;
-  const int RS = rows + 1;
+  const int RS = col_stride(rows);
   uint32_t* X = smem;
   uint32_t* Tsm = X + p.C * RS;
   uint32_t* F = Tsm + rows;
   uint32_t* d = blockIdx.y == 0 ? d0 : d1;
-  const uint8_t* s8 = blockIdx.y == 0 ? a8 : b8;
-  const uint64_t ls = blockIdx.y == 0 ? la : lb;
   const uint32_t t = blockIdx.x;
 
   for (int i = threadIdx.x; i < rows; i += blockDim.x) Tsm[i] = tw.small[i];
   column_factors(p, t, tw, F);
-  const int E = rows * p.C;
-  for (int e = threadIdx.x; e < E; e += blockDim.x) {
-    int r, c;
-    tile_rc(p, e, r, c);
-    const uint64_t idx = tile_index(p, t, r, c);
-    uint32_t v;
-    if (IN == IN_U8) v = idx < ls ? c_mont17[s8[idx] % 17] : 0u;
-    else v = d[idx];
-    X[c * RS + r] = v;
-  }
+  if (IN == IN_U8) load_tile<true>(p, t, X, RS, nullptr, blockIdx.y == 0 ? a8 : b8, blockIdx.y == 0 ? la : lb);
+  else load_tile<false>(p, t, X, RS, d, nullptr, 0);
   __syncthreads();
   tile_stages<INV>(X, p.M, p.C, RS, Tsm, F, p.lo != 0);
 
+  if (OUT == OUT_U32) {
+    store_tile(p, t, X, RS, d);
+    return;
+  }
   uint32_t last = 0;
+  const int E = rows * p.C;
   for (int e = threadIdx.x; e < E; e += blockDim.x) {
     int r, c;
-    tile_rc(p, e, r, c);
+    if (p.lo == 0) { r = e & (rows - 1); c = e >> p.M; }
+    else { c = e % p.C; r = e / p.C; }
     const uint64_t idx = tile_index(p, t, r, c);
-    const uint32_t v = X[c * RS + r];
-    if (OUT == OUT_U8) {
-      if (idx < out_len) {
-        const uint8_t byte = (uint8_t)(bb::mmul(v, ninv) % 17u);
-        out8[idx] = byte;
-        if (byte && (uint32_t)idx + 1 > last) last = (uint32_t)idx + 1;
-      }
-    } else {
-      d[idx] = v;
+    if (idx < out_len) {
+      const uint8_t byte = (uint8_t)(bb::mmul(X[c * RS + phys(r)], ninv) % 17u);
+      out8[idx] = byte;
+      if (byte && (uint32_t)idx + 1 > last) last = (uint32_t)idx + 1;
     }
   }
-  if (OUT == OUT_U8) {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) last = max(last, (uint32_t)__shfl_xor(last, off, PLK_WAVE));
-    if ((threadIdx.x & (PLK_WAVE - 1)) == 0 && last) atomicMax(nz, last);
-  }
+  for (int off = 32; off > 0; off >>= 1) last = max(last, (uint32_t)__shfl_xor(last, off, PLK_WAVE));
+  if ((threadIdx.x & (PLK_WAVE - 1)) == 0 && last) atomicMax(nz, last);
 }
 
 // Last forward pass of a and b (lo = 0), pointwise product, first inverse pass; writes the
-// product spectrum-turned-partial-inverse into d0.
+// result into d0.  One tile of each array, one LDS round trip.
 __global__ __launch_bounds__(NTT_THREADS) void ntt_center_kernel(Pass p, uint32_t* d0, const uint32_t* d1,
                                                                  Tw twf, Tw twi) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int rows = 1 << p.M;
-  const int RS = rows + 1;
+  const int RS = col_stride(rows);
   uint32_t* X = smem;
   uint32_t* Y = X + p.C * RS;
   uint32_t* Tf = Y + p.C * RS;
@@ -195,28 +285,20 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_center_kernel(Pass p, uint32_
     Tf[i] = twf.small[i];
     Ti[i] = twi.small[i];
   }
-  const int E = rows * p.C;
-  for (int e = threadIdx.x; e < E; e += blockDim.x) {
-    int r, c;
-    tile_rc(p, e, r, c);
-    const uint64_t idx = tile_index(p, t, r, c);
-    X[c * RS + r] = d0[idx];
-    Y[c * RS + r] = d1[idx];
-  }
+  load_tile<false>(p, t, X, RS, d0, nullptr, 0);
+  load_tile<false>(p, t, Y, RS, d1, nullptr, 0);
   __syncthreads();
   tile_stages<false>(X, p.M, p.C, RS, Tf, nullptr, false);
   tile_stages<false>(Y, p.M, p.C, RS, Tf, nullptr, false);
+  const int E = rows * p.C;
   for (int e = threadIdx.x; e < E; e += blockDim.x) {
     const int c = e >> p.M, r = e & (rows - 1);
-    X[c * RS + r] = bb::mmul(X[c * RS + r], Y[c * RS + r]);
+    const int o = c * RS + phys(r);
+    X[o] = bb::mmul(X[o], Y[o]);
   }
   __syncthreads();
   tile_stages<true>(X, p.M, p.C, RS, Ti, nullptr, false);
-  for (int e = threadIdx.x; e < E; e += blockDim.x) {
-    int r, c;
-    tile_rc(p, e, r, c);
-    d0[tile_index(p, t, r, c)] = X[c * RS + r];
-  }
+  store_tile(p, t, X, RS, d0);
 }
 
 // Whole poly_mul in one workgroup for N = 2^k <= 2^PLK_SMALL_LOG.
@@ -225,29 +307,30 @@ __global__ __launch_bounds__(1024) void polymul_small_kernel(const uint8_t* a8, 
                                                              uint8_t* out8, uint32_t ninv, uint32_t* nz) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int N = 1 << k;
+  const int RS = col_stride(N);
   uint32_t* X = smem;
-  uint32_t* Y = X + N;
-  uint32_t* Tf = Y + N;
+  uint32_t* Y = X + RS;
+  uint32_t* Tf = Y + RS;
   uint32_t* Ti = Tf + N;
   for (int i = threadIdx.x; i < N; i += blockDim.x) {
-    X[i] = i < (int64_t)la ? c_mont17[a8[i] % 17] : 0u;
-    Y[i] = i < (int64_t)lb ? c_mont17[b8[i] % 17] : 0u;
+    X[phys(i)] = i < (int64_t)la ? c_mont17[a8[i] % 17] : 0u;
+    Y[phys(i)] = i < (int64_t)lb ? c_mont17[b8[i] % 17] : 0u;
     Tf[i] = twf.small[i];
     Ti[i] = twi.small[i];
   }
   __syncthreads();
   if (k > 0) {
-    tile_stages<false>(X, k, 1, N, Tf, nullptr, false);
-    tile_stages<false>(Y, k, 1, N, Tf, nullptr, false);
+    tile_stages<false>(X, k, 1, RS, Tf, nullptr, false);
+    tile_stages<false>(Y, k, 1, RS, Tf, nullptr, false);
   }
-  for (int i = threadIdx.x; i < N; i += blockDim.x) X[i] = bb::mmul(X[i], Y[i]);
+  for (int i = threadIdx.x; i < N; i += blockDim.x) X[phys(i)] = bb::mmul(X[phys(i)], Y[phys(i)]);
   __syncthreads();
-  if (k > 0) tile_stages<true>(X, k, 1, N, Ti, nullptr, false);
+  if (k > 0) tile_stages<true>(X, k, 1, RS, Ti, nullptr, false);
   const uint64_t rl = la + lb - 1;
   uint32_t last = 0;
   for (int i = threadIdx.x; i < N; i += blockDim.x) {
     if ((uint64_t)i < rl) {
-      const uint8_t byte = (uint8_t)(bb::mmul(X[i], ninv) % 17u);
+      const uint8_t byte = (uint8_t)(bb::mmul(X[phys(i)], ninv) % 17u);
       out8[i] = byte;
       if (byte) last = max(last, (uint32_t)i + 1);
     }
@@ -323,6 +406,18 @@ int cols_for(int M, bool center) {
 
 int plk_ntt_init_tables(void) {
   if (g_tw.d_small_f) return PLK_OK;
+  // tiles of 2^12 rows with two arrays exceed the default 64 KB dynamic-LDS limit
+  const int lds_max = 160 * 1024;
+  PLK_HIP(hipFuncSetAttribute((const void*)polymul_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+  PLK_HIP(hipFuncSetAttribute((const void*)ntt_center_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+  PLK_HIP(hipFuncSetAttribute((const void*)ntt_pass_kernel<false, IN_U8, OUT_U32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+  PLK_HIP(hipFuncSetAttribute((const void*)ntt_pass_kernel<false, IN_U32, OUT_U32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+  PLK_HIP(hipFuncSetAttribute((const void*)ntt_pass_kernel<true, IN_U32, OUT_U32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+  PLK_HIP(hipFuncSetAttribute((const void*)ntt_pass_kernel<true, IN_U32, OUT_U8>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
   const uint32_t w27 = bb::hpow(bb::GENERATOR, (bb::P - 1) >> bb::TWO_ADICITY);   // order 2^27
   const uint32_t w27i = bb::hpow(w27, bb::P - 2);
   const int SM = 1 << PLK_NTT_SMALL_LOG;
@@ -393,7 +488,7 @@ size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb) {
 
 static size_t pass_lds(int M, int C, bool center) {
   const size_t rows = 1u << M;
-  return (center ? 2 : 1) * C * (rows + 1) * 4 + (center ? 2 : 1) * rows * 4 + (size_t)C * M * 4;
+  return (center ? 2 : 1) * C * (size_t)col_stride((int)rows) * 4 + (center ? 2 : 1) * rows * 4 + (size_t)C * M * 4;
 }
 
 // d_out must hold la+lb-1 bytes; *d_nz is zeroed here and receives the trimmed length
@@ -420,7 +515,7 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
   if (k > bb::TWO_ADICITY) return PLK_ERR_RANGE;
   const uint32_t ninv = bb::hpow(1ull << k, bb::P - 2);   // normal form on purpose
   if (k <= PLK_SMALL_LOG) {
-    const size_t lds = (size_t)4 * 4 * (1u << k);
+    const size_t lds = (size_t)4 * (2 * col_stride(1 << k) + 2 * (1 << k));
     hipLaunchKernelGGL(polymul_small_kernel, dim3(1), dim3(1024), lds, st, d_a, la, d_b, lb, k, tw_fwd(), tw_inv(),
                        d_out, ninv, d_nz);
     PLK_HIP(hipGetLastError());

@@ -98,7 +98,7 @@ def test_struct_layouts(tmp_path):
     r = _gcc([str(tmp_path / "l.c"), "-o", str(tmp_path / "l")])
     assert r.returncode == 0, r.stderr
     out = subprocess.run([str(tmp_path / "l")], capture_output=True, text=True).stdout
-    assert out == "3 1 1 32"
+    assert out == "3 1 1 128"
 
 
 @pytest.mark.skipif(not os.path.isdir(REF_SRC), reason="reference sources not present")

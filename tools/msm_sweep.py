@@ -31,7 +31,7 @@ def main():
     sets = 40 if log2n >= 22 else 64
     pts, sc = make_msm_sets(torch, n, sets, dev, 5)
     K = 200
-    res = torch.zeros((K, 32), dtype=torch.uint8, device=dev)
+    res = torch.zeros((K, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
     out = {"log2n": log2n, "threads_env": os.environ.get("PLK_MSM_THREADS")}
 
     def timed(fn, reps=3):
@@ -88,13 +88,13 @@ def main():
                               "GBs_dev": round(4 * n * B / (avg * 1e-3) / 1e9, 1)}
     # correctness spot check: every record agrees with a fresh single launch
     torch.cuda.synchronize()
-    bad = int(res[:, 12:16].view(torch.int32).sum().item())
-    r1 = torch.zeros((1, 32), dtype=torch.uint8, device=dev)
+    bad = int(res[:, 76:80].view(torch.int32).sum().item())
+    r1 = torch.zeros((1, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
     hip.msm_g1_dev(pts[0], sc[0], n, r1[0], st)
     torch.cuda.synchronize()
     out["irregular"] = bad
-    out["set0_g1"] = bytes(r1[0, 16:19].cpu().numpy()).hex()
-    out["set0_batch_g1"] = bytes(res[0, 16:19].cpu().numpy()).hex()
+    out["set0_g1"] = bytes(r1[0, 80:83].cpu().numpy()).hex()
+    out["set0_batch_g1"] = bytes(res[0, 80:83].cpu().numpy()).hex()
     print(json.dumps(out), flush=True)
 
 

@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Quick device-time check of the NTT / poly_mul kernels (tuning aid)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "plonk.c_amd"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import plonkhip as hip  # noqa: E402
+from bench import event_avg_ms  # noqa: E402
+
+hip.init(0)
+dev = torch.device("cuda", 0)
+st = torch.cuda.current_stream()
+out = {}
+for k in (16, 20, 22, 23):
+    bufs = [torch.randint(0, 2013265921, (1 << k,), dtype=torch.int64, device=dev).to(torch.int32) for _ in range(4)]
+    avg, med = event_avg_ms(torch, st, lambda i: hip.ntt_dev(bufs[i % 4], k, False, st), 40)
+    out["ntt_fwd_2^%d_us" % k] = round(avg * 1e3, 2)
+    out["ntt_fwd_2^%d_Gelem_s" % k] = round((1 << k) / (avg * 1e-3) / 1e9, 1)
+for la, lb in ((1 << 12, 1 << 12), (1 << 16, 1 << 16), (1 << 19, 1 << 19), (3 * (1 << 20) + 4, (1 << 20) + 3)):
+    a = torch.randint(0, 17, (la,), dtype=torch.int16, device=dev).to(torch.uint8)
+    b = torch.randint(0, 17, (lb,), dtype=torch.int16, device=dev).to(torch.uint8)
+    o = torch.zeros(la + lb - 1, dtype=torch.uint8, device=dev)
+    nz = torch.zeros(4, dtype=torch.int32, device=dev)
+    work = torch.zeros(max(4, hip.poly_mul_workspace(la, lb)), dtype=torch.uint8, device=dev)
+    avg, med = event_avg_ms(torch, st, lambda i: hip.poly_mul_dev(a, la, b, lb, o, nz, work, st), 20)
+    out["poly_mul_%dx%d_us" % (la, lb)] = round(avg * 1e3, 2)
+print(json.dumps(out))
