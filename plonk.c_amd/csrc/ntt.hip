@@ -269,38 +269,6 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_pass_kernel(
   if ((threadIdx.x & (PLK_WAVE - 1)) == 0 && last) atomicMax(nz, last);
 }
 
-// Last forward pass of a and b (lo = 0), pointwise product, first inverse pass; writes the
-// result into d0.  One tile of each array, one LDS round trip.
-__global__ __launch_bounds__(NTT_THREADS) void ntt_center_kernel(Pass p, uint32_t* d0, const uint32_t* d1,
-                                                                 Tw twf, Tw twi) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const int rows = 1 << p.M;
-  const int RS = col_stride(rows);
-  uint32_t* X = smem;
-  uint32_t* Y = X + p.C * RS;
-  uint32_t* Tf = Y + p.C * RS;
-  uint32_t* Ti = Tf + rows;
-  const uint32_t t = blockIdx.x;
-  for (int i = threadIdx.x; i < rows; i += blockDim.x) {
-    Tf[i] = twf.small[i];
-    Ti[i] = twi.small[i];
-  }
-  load_tile<false>(p, t, X, RS, d0, nullptr, 0);
-  load_tile<false>(p, t, Y, RS, d1, nullptr, 0);
-  __syncthreads();
-  tile_stages<false>(X, p.M, p.C, RS, Tf, nullptr, false);
-  tile_stages<false>(Y, p.M, p.C, RS, Tf, nullptr, false);
-  const int E = rows * p.C;
-  for (int e = threadIdx.x; e < E; e += blockDim.x) {
-    const int c = e >> p.M, r = e & (rows - 1);
-    const int o = c * RS + phys(r);
-    X[o] = bb::mmul(X[o], Y[o]);
-  }
-  __syncthreads();
-  tile_stages<true>(X, p.M, p.C, RS, Ti, nullptr, false);
-  store_tile(p, t, X, RS, d0);
-}
-
 // Whole poly_mul in one workgroup for N = 2^k <= 2^PLK_SMALL_LOG.
 __global__ __launch_bounds__(1024) void polymul_small_kernel(const uint8_t* a8, uint64_t la, const uint8_t* b8,
                                                              uint64_t lb, int k, Tw twf, Tw twi,
@@ -379,44 +347,20 @@ struct TwHost {
 Tw tw_fwd() { return Tw{g_tw.d_small_f, g_tw.d_lo_f, g_tw.d_hi_f}; }
 Tw tw_inv() { return Tw{g_tw.d_small_i, g_tw.d_lo_i, g_tw.d_hi_i}; }
 
-// split k bits into passes (high bits first); every pass <= 11 bits except a lone center
-void make_plan(int k, int* Ms, int& npass) {
-  if (k <= 22) {
-    npass = 2;
-    const int center = k - k / 2;    // >= the high pass
-    Ms[0] = k - center;              // high bits
-    Ms[1] = center;                  // low bits (center kernel)
-  } else {
-    npass = 3;
-    const int a = (k + 2) / 3;
-    Ms[0] = k - 2 * a;
-    Ms[1] = a;
-    Ms[2] = a;
-  }
-}
-
-int cols_for(int M, bool center) {
-  int C = (1 << 12) >> M;
-  if (C < 1) C = 1;
-  if (!center && C < 4) C = 4;
-  return C;
-}
-
 }  // namespace
+
+PlkTwTables plk_ntt_tables(void) {
+  return PlkTwTables{g_tw.d_small_f, g_tw.d_small_i, g_tw.d_lo_f, g_tw.d_hi_f, g_tw.d_lo_i, g_tw.d_hi_i};
+}
 
 int plk_ntt_init_tables(void) {
   if (g_tw.d_small_f) return PLK_OK;
   // tiles of 2^12 rows with two arrays exceed the default 64 KB dynamic-LDS limit
   const int lds_max = 160 * 1024;
   PLK_HIP(hipFuncSetAttribute((const void*)polymul_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
-  PLK_HIP(hipFuncSetAttribute((const void*)ntt_center_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
-  PLK_HIP(hipFuncSetAttribute((const void*)ntt_pass_kernel<false, IN_U8, OUT_U32>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
   PLK_HIP(hipFuncSetAttribute((const void*)ntt_pass_kernel<false, IN_U32, OUT_U32>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
   PLK_HIP(hipFuncSetAttribute((const void*)ntt_pass_kernel<true, IN_U32, OUT_U32>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
-  PLK_HIP(hipFuncSetAttribute((const void*)ntt_pass_kernel<true, IN_U32, OUT_U8>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
   const uint32_t w27 = bb::hpow(bb::GENERATOR, (bb::P - 1) >> bb::TWO_ADICITY);   // order 2^27
   const uint32_t w27i = bb::hpow(w27, bb::P - 2);
@@ -524,77 +468,24 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
   if (!d_work) return PLK_ERR_ARG;
   uint32_t* A = (uint32_t*)d_work;
   uint32_t* B = A + (1ull << k);
-  int Ms[3], np;
-  make_plan(k, Ms, np);
-  // bit ranges: pass i covers [lo_i, lo_i + Ms[i]), lo decreasing
-  int lo[3];
-  {
-    int top = k;
-    for (int i = 0; i < np; i++) { lo[i] = top - Ms[i]; top = lo[i]; }
-  }
-  const Tw twf = tw_fwd(), twi = tw_inv();
-  // forward passes over the high bits (first one reads the u8 inputs)
-  for (int i = 0; i < np - 1; i++) {
-    Pass p{k, lo[i], Ms[i], cols_for(Ms[i], false)};
-    const uint32_t tiles = (uint32_t)((1ull << k) >> (p.M + log2_ceil(p.C)));
-    const size_t lds = pass_lds(p.M, p.C, false);
-    if (i == 0)
-      hipLaunchKernelGGL((ntt_pass_kernel<false, IN_U8, OUT_U32>), dim3(tiles, 2), dim3(NTT_THREADS), lds, st, p, A,
-                         B, d_a, d_b, la, lb, twf, nullptr, 0, 0u, nullptr);
-    else
-      hipLaunchKernelGGL((ntt_pass_kernel<false, IN_U32, OUT_U32>), dim3(tiles, 2), dim3(NTT_THREADS), lds, st, p, A,
-                         B, nullptr, nullptr, 0, 0, twf, nullptr, 0, 0u, nullptr);
-    PLK_HIP(hipGetLastError());
-  }
-  {
-    Pass p{k, 0, Ms[np - 1], cols_for(Ms[np - 1], true)};
-    const uint32_t tiles = (uint32_t)((1ull << k) >> (p.M + log2_ceil(p.C)));
-    const size_t lds = pass_lds(p.M, p.C, true);
-    hipLaunchKernelGGL(ntt_center_kernel, dim3(tiles), dim3(NTT_THREADS), lds, st, p, A, B, twf, twi);
-    PLK_HIP(hipGetLastError());
-  }
-  for (int i = np - 2; i >= 0; i--) {
-    Pass p{k, lo[i], Ms[i], cols_for(Ms[i], false)};
-    const uint32_t tiles = (uint32_t)((1ull << k) >> (p.M + log2_ceil(p.C)));
-    const size_t lds = pass_lds(p.M, p.C, false);
-    if (i == 0)
-      hipLaunchKernelGGL((ntt_pass_kernel<true, IN_U32, OUT_U8>), dim3(tiles, 1), dim3(NTT_THREADS), lds, st, p, A,
-                         A, nullptr, nullptr, 0, 0, twi, d_out, rl, ninv, d_nz);
-    else
-      hipLaunchKernelGGL((ntt_pass_kernel<true, IN_U32, OUT_U32>), dim3(tiles, 1), dim3(NTT_THREADS), lds, st, p, A,
-                         A, nullptr, nullptr, 0, 0, twi, nullptr, 0, 0u, nullptr);
-    PLK_HIP(hipGetLastError());
-  }
-  return PLK_OK;
+  return plk_wave_poly_mul_launch(d_a, la, d_b, lb, k, d_out, d_nz, A, B, ninv, st);
 }
 
 // Standalone forward NTT (DIF, natural -> bit-reversed), in place on Montgomery-form u32,
 // or inverse (DIT, bit-reversed -> natural, NOT scaled by N^-1).  Same passes as poly_mul.
 int plk_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st) {
   if (k < 1 || k > bb::TWO_ADICITY) return PLK_ERR_RANGE;
-  int Ms[3], np = 1;
-  if (k <= 12) { Ms[0] = k; np = 1; }
-  else make_plan(k, Ms, np);
-  int lo[3];
-  {
-    int top = k;
-    for (int i = 0; i < np; i++) { lo[i] = top - Ms[i]; top = lo[i]; }
-  }
+  if (plk_wave_ntt_supported(k)) return plk_wave_ntt_launch(d, k, inverse, st);
+  // k <= 12: one workgroup-tile pass (lo = 0, a single tile holds the whole array)
   const Tw tw = inverse ? tw_inv() : tw_fwd();
-  for (int s = 0; s < np; s++) {
-    const int i = inverse ? (np - 1 - s) : s;
-    Pass p{k, lo[i], Ms[i], cols_for(Ms[i], lo[i] == 0)};
-    if (lo[i] != 0 && (1 << lo[i]) < p.C) p.C = 1 << lo[i];
-    if ((1ull << k) < ((uint64_t)p.C << p.M)) p.C = 1;
-    const uint32_t tiles = (uint32_t)((1ull << k) >> (p.M + log2_ceil(p.C)));
-    const size_t lds = pass_lds(p.M, p.C, false);
-    if (inverse)
-      hipLaunchKernelGGL((ntt_pass_kernel<true, IN_U32, OUT_U32>), dim3(tiles, 1), dim3(NTT_THREADS), lds, st, p, d,
-                         d, nullptr, nullptr, 0, 0, tw, nullptr, 0, 0u, nullptr);
-    else
-      hipLaunchKernelGGL((ntt_pass_kernel<false, IN_U32, OUT_U32>), dim3(tiles, 1), dim3(NTT_THREADS), lds, st, p, d,
-                         d, nullptr, nullptr, 0, 0, tw, nullptr, 0, 0u, nullptr);
-    PLK_HIP(hipGetLastError());
-  }
+  const Pass p{k, 0, k, 1};
+  const size_t lds = pass_lds(p.M, p.C, false);
+  if (inverse)
+    hipLaunchKernelGGL((ntt_pass_kernel<true, IN_U32, OUT_U32>), dim3(1, 1), dim3(NTT_THREADS), lds, st, p, d, d,
+                       nullptr, nullptr, 0, 0, tw, nullptr, 0, 0u, nullptr);
+  else
+    hipLaunchKernelGGL((ntt_pass_kernel<false, IN_U32, OUT_U32>), dim3(1, 1), dim3(NTT_THREADS), lds, st, p, d, d,
+                       nullptr, nullptr, 0, 0, tw, nullptr, 0, 0u, nullptr);
+  PLK_HIP(hipGetLastError());
   return PLK_OK;
 }

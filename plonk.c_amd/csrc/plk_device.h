@@ -24,6 +24,7 @@ constexpr uint32_t neg_inv_p() {             // p' = -p^{-1} mod 2^32 (Newton it
 }
 constexpr uint32_t PINV = neg_inv_p();
 static_assert(P * (0u - PINV) == 1u, "p * p^{-1} == 1 mod 2^32");
+constexpr uint32_t R2 = (uint32_t)((((unsigned __int128)1) << 64) % P);   // R^2 mod p: mmul(x, R2) = x R
 
 __host__ __device__ __forceinline__ uint32_t mmul(uint32_t a, uint32_t b) {
   uint64_t t = (uint64_t)a * b;

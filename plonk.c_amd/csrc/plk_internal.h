@@ -38,9 +38,21 @@ int plk_msm_finalize_launch(const uint32_t* d_logs, int batch, int stride, uint8
 int plk_msm_combine_launch(const uint32_t* d_logs, int count, uint8_t* d_out, hipStream_t st);
 
 // ntt.hip
+struct PlkTwTables {
+  const uint32_t *small_f, *small_i;   // T[2^j + r] = w_{2^(j+1)}^(+-r), 2^PLK_NTT_SMALL_LOG entries
+  const uint32_t *lo_f, *hi_f;         // w_{2^27}^i = lo[i & 4095] * hi[i >> 12]
+  const uint32_t *lo_i, *hi_i;         // same for the inverse root
+};
+PlkTwTables plk_ntt_tables(void);
 int plk_ntt_init_tables(void);
 void plk_ntt_free_tables(void);
 size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb);
 int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
                         uint32_t* d_nz, void* d_work, hipStream_t st);
 int plk_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st);
+
+// ntt_wave.hip (transforms of 2^13 .. 2^27 points)
+bool plk_wave_ntt_supported(int k);
+int plk_wave_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, int k,
+                             uint8_t* d_out, uint32_t* d_nz, uint32_t* A, uint32_t* B, uint32_t ninv, hipStream_t st);
+int plk_wave_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st);
