@@ -219,6 +219,19 @@ __device__ void tile_stages(uint32_t* X, int M, int C, int RS, const uint32_t* T
 
 }  // namespace
 
+// max over the block (blockDim a multiple of 64, <= 1024); every thread gets the result
+__device__ __forceinline__ uint32_t block_max(uint32_t v) {
+  __shared__ uint32_t red[16];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off, PLK_WAVE));
+  __syncthreads();
+  if ((threadIdx.x & (PLK_WAVE - 1)) == 0) red[threadIdx.x / PLK_WAVE] = v;
+  __syncthreads();
+  uint32_t m = 0;
+  for (int w = 0; w < (int)(blockDim.x / PLK_WAVE); w++) m = max(m, red[w]);
+  return m;
+}
+
 // Input/output modes of a pass
 enum : int { IN_U32 = 0, IN_U8 = 1 };
 enum : int { OUT_U32 = 0, OUT_U8 = 1 };
@@ -303,9 +316,28 @@ __global__ __launch_bounds__(1024) void polymul_small_kernel(const uint8_t* a8, 
       if (byte) last = max(last, (uint32_t)i + 1);
     }
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) last = max(last, (uint32_t)__shfl_xor(last, off, PLK_WAVE));
-  if ((threadIdx.x & (PLK_WAVE - 1)) == 0 && last) atomicMax(nz, last);
+  last = block_max(last);
+  if (threadIdx.x == 0) *nz = last;
+}
+
+// Trimmed length of out8[0, rl): index + 1 of the last non-zero byte, 0 if none (the
+// reference's poly_new trim, src/poly.h:21-24).  One block scans backwards in 16 KiB chunks and
+// stops at the first chunk holding a non-zero byte -- almost always the last one -- instead
+// of every tile of the product racing on one atomic word.
+__global__ __launch_bounds__(1024) void trim_kernel(const uint8_t* __restrict__ out8, uint64_t rl, uint32_t* nz) {
+  constexpr int64_t CH = 16384;
+  for (int64_t end = (int64_t)rl; end > 0; end -= CH) {
+    const int64_t start = end > CH ? end - CH : 0;
+    uint32_t last = 0;
+    for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x)
+      if (out8[i]) last = max(last, (uint32_t)(i + 1));
+    last = block_max(last);
+    if (last) {
+      if (threadIdx.x == 0) *nz = last;
+      return;
+    }
+  }
+  if (threadIdx.x == 0) *nz = 0;
 }
 
 // Direct convolution when one operand is short: out[i] = sum_j a[j] b[i-j] mod 17 over the
@@ -316,20 +348,15 @@ __global__ __launch_bounds__(256) void polymul_direct_kernel(const uint8_t* lg, 
   if (threadIdx.x < lsh) S[threadIdx.x] = sh[threadIdx.x] % 17u;
   __syncthreads();
   const uint64_t rl = llg + lsh - 1;
-  uint32_t last = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rl; i += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t acc = 0;
     for (int j = 0; j < lsh; j++) {
       const int64_t o = (int64_t)i - j;
       if (o >= 0 && (uint64_t)o < llg) acc += S[j] * (lg[o] % 17u);
     }
-    const uint8_t byte = (uint8_t)(acc % 17u);
-    out8[i] = byte;
-    if (byte) last = max(last, (uint32_t)(i + 1));
+    out8[i] = (uint8_t)(acc % 17u);
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) last = max(last, (uint32_t)__shfl_xor(last, off, PLK_WAVE));
-  if ((threadIdx.x & (PLK_WAVE - 1)) == 0 && last) atomicMax(nz, last);
+  (void)nz;   // trimmed length: trim_kernel
 }
 
 // ------------------------------------------------------------------------------ host side
@@ -356,7 +383,7 @@ PlkTwTables plk_ntt_tables(void) {
 int plk_ntt_init_tables(void) {
   if (g_tw.d_small_f) return PLK_OK;
   // tiles of 2^12 rows with two arrays exceed the default 64 KB dynamic-LDS limit
-  const int lds_max = 160 * 1024;
+  const int lds_max = 150 * 1024;   // leaves room for the kernels' static LDS
   PLK_HIP(hipFuncSetAttribute((const void*)polymul_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
   PLK_HIP(hipFuncSetAttribute((const void*)ntt_pass_kernel<false, IN_U32, OUT_U32>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
@@ -435,8 +462,8 @@ static size_t pass_lds(int M, int C, bool center) {
   return (center ? 2 : 1) * C * (size_t)col_stride((int)rows) * 4 + (center ? 2 : 1) * rows * 4 + (size_t)C * M * 4;
 }
 
-// d_out must hold la+lb-1 bytes; *d_nz is zeroed here and receives the trimmed length
-// (0 means "all zero" -> caller reports length 1).
+// d_out must hold la+lb-1 bytes; *d_nz receives the trimmed length (0 means "all zero" ->
+// the caller reports length 1).
 int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
                         uint32_t* d_nz, void* d_work, hipStream_t st) {
   if (la == 0 || lb == 0) return PLK_ERR_ARG;
@@ -444,7 +471,6 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
   const uint64_t mn = la < lb ? la : lb;
   if (mn * 256 >= bb::P) return PLK_ERR_RANGE;
   if (rl >= (1ull << 32)) return PLK_ERR_RANGE;
-  PLK_HIP(hipMemsetAsync(d_nz, 0, 4, st));
   if (mn <= PLK_DIRECT_MAX) {
     const uint8_t* lg = la >= lb ? d_a : d_b;
     const uint8_t* sh = la >= lb ? d_b : d_a;
@@ -452,6 +478,8 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
     const int blocks = (int)(blocks64 > 8192 ? 8192 : blocks64);
     hipLaunchKernelGGL(polymul_direct_kernel, dim3(blocks), dim3(256), 0, st, lg, la >= lb ? la : lb, sh, (int)mn,
                        d_out, d_nz);
+    PLK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d_out, rl, d_nz);
     PLK_HIP(hipGetLastError());
     return PLK_OK;
   }
@@ -468,7 +496,11 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
   if (!d_work) return PLK_ERR_ARG;
   uint32_t* A = (uint32_t*)d_work;
   uint32_t* B = A + (1ull << k);
-  return plk_wave_poly_mul_launch(d_a, la, d_b, lb, k, d_out, d_nz, A, B, ninv, st);
+  int rc = plk_wave_poly_mul_launch(d_a, la, d_b, lb, k, d_out, A, B, ninv, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d_out, rl, d_nz);
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
 }
 
 // Standalone forward NTT (DIF, natural -> bit-reversed), in place on Montgomery-form u32,

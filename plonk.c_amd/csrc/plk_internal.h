@@ -54,5 +54,5 @@ int plk_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st);
 // ntt_wave.hip (transforms of 2^13 .. 2^27 points)
 bool plk_wave_ntt_supported(int k);
 int plk_wave_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, int k,
-                             uint8_t* d_out, uint32_t* d_nz, uint32_t* A, uint32_t* B, uint32_t ninv, hipStream_t st);
+                             uint8_t* d_out, uint32_t* A, uint32_t* B, uint32_t ninv, hipStream_t st);
 int plk_wave_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st);
