@@ -108,6 +108,43 @@ int plk_poly_mul_dev(const uint8_t *d_a, size_t la, const uint8_t *d_b, size_t l
  * forward = DIF natural -> bit-reversed; inverse = DIT bit-reversed -> natural, unscaled. */
 int plk_ntt_dev(uint32_t *d_data, int log_n, int inverse, void *stream);
 
+/* ---- device-resident prover (replaces plonk_new / plonk_prove / plonk_free,
+ * src/plonk.h:53-139, 223-656, 120-139) ---------------------------------------------------
+ * plk_prover_create uploads the SRS and Z_H once (the PLONK struct of plonk_new); the
+ * circuit tables h, k1_h, k2_h, h_pows_inv are optional (needed only by plk_prover_prove).
+ * h_pows_inv is the inverse Vandermonde matrix row-major, [r * n + c] = matrix_get(r, c). */
+typedef struct plk_prover plk_prover_t;
+typedef struct {
+  size_t n;                                  /* gates = |H| */
+  const uint8_t *h, *k1_h, *k2_h;            /* n each (HF values), or NULL */
+  const uint8_t *h_pows_inv;                 /* n * n, or NULL */
+  const uint8_t *z_h;                        /* Z_H(x) coefficients (plonk.z_h_x) */
+  size_t z_h_len;
+  const uint8_t *srs_g1;                     /* srs.g1s, 3 bytes per G1 */
+  size_t srs_len;
+} plk_plonk_desc_t;
+/* CONSTRAINTS + ASSIGNMENTS (src/constraints.h:11-60); copies are (type, index) byte pairs,
+ * type 0 = COPYOF_A, 1 = COPYOF_B, 2 = COPYOF_C, index 1-based (n <= 16 in GF(17)) */
+typedef struct {
+  const uint8_t *q_m, *q_l, *q_r, *q_o, *q_c;
+  const uint8_t *copy_a, *copy_b, *copy_c;   /* 2n bytes each */
+  const uint8_t *a, *b, *c;
+} plk_circuit_t;
+#define PLK_PROVE_STRICT 1                   /* enforce the zero-remainder asserts */
+int plk_prover_create(const plk_plonk_desc_t *desc, plk_prover_t **out);
+void plk_prover_destroy(plk_prover_t *p);
+size_t plk_prover_device_bytes(const plk_prover_t *p);
+/* plonk_prove: chal = {alpha, beta, gamma, z, v}; proof = the 34-byte PROOF struct.  Errors
+ * where the reference exits or asserts (unsatisfied gate, bad copy, SRS too short, non-zero
+ * remainder, t(x) too short to slice) return PLK_ERR_ARG / PLK_ERR_RANGE. */
+int plk_prover_prove(plk_prover_t *p, const plk_circuit_t *circuit, const uint8_t chal[5],
+                     const uint8_t rand9[9], uint8_t proof[34]);
+/* rounds 1-5 of plonk_prove from device-resident interpolated polynomials (each zero padded
+ * to n bytes): f_a f_b f_c q_o q_m q_l q_r q_c s_sigma_1 s_sigma_2 s_sigma_3 acc_x l_1_x.
+ * Without PLK_PROVE_STRICT non-zero remainders are tolerated (synthetic inputs). */
+int plk_prover_rounds_dev(plk_prover_t *p, const uint8_t *const d_polys[13], const uint8_t chal[5],
+                          const uint8_t rand9[9], int flags, uint8_t proof[34]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -177,6 +177,19 @@ class Reference(_Lib):
         L.ref_interpolate4.argtypes = [_u8p, _u8p]
         L.ref_poly_divide.argtypes = [_u8p, C.c_size_t, _u8p, C.c_size_t, _u8p,
                                       C.POINTER(C.c_size_t), _u8p, C.POINTER(C.c_size_t)]
+        L.ref_plonk4_data.restype = C.c_size_t
+        L.ref_plonk4_data.argtypes = [C.c_uint8, C.c_size_t, C.c_int] + [_u8p] * 6
+
+    def plonk4_data(self, secret=2, srs_n=6, srs_mode=0):
+        """srs_create + plonk_new(srs, 4): h, k1_h, k2_h, h_pows_inv (row-major), z_h_x, g1s."""
+        h, k1, k2 = (np.zeros(4, np.uint8) for _ in range(3))
+        hinv = np.zeros(16, np.uint8)
+        zh = np.zeros(16, np.uint8)
+        g1s = np.zeros(3 * (srs_n + 1), np.uint8)
+        zl = self.lib.ref_plonk4_data(secret, srs_n, srs_mode, _ptr(h), _ptr(k1), _ptr(k2),
+                                      _ptr(hinv), _ptr(zh), _ptr(g1s))
+        return {"h": bytes(h), "k1_h": bytes(k1), "k2_h": bytes(k2), "h_pows_inv": bytes(hinv),
+                "z_h": bytes(zh[:zl]), "g1s": bytes(g1s)}
 
     @staticmethod
     def available(path=os.path.join(HERE, "_ref", "libplonkref.so")):

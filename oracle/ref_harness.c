@@ -17,6 +17,7 @@
  *   ref_poly_eval     -> poly_eval                                      src/poly.h:265-272
  *   ref_interpolate4  -> plonk_new + interpolate_at_h                   src/plonk.h:53,162
  *   ref_prove4        -> srs_create + plonk_new + plonk_prove           src/srs.h:18, src/plonk.h:53,223
+ *   ref_plonk4_data   -> srs_create + plonk_new: h, k1_h, k2_h, h_pows_inv, z_h_x, g1s
  *
  * The same file compiled with `-include include/prelude.h -DPLK_NO_FORK` (target
  * _ref/libplonkref_dropin.so) is the DROP-IN demonstration: the reference's unmodified
@@ -106,6 +107,39 @@ size_t ref_interpolate4(const uint8_t *values, uint8_t *out) {
   return len;
 }
 
+/* The setup plonk_prove consumes (PLONK of plonk_new, SRS of srs_create; srs_mode as in
+ * ref_prove4): h, k1_h, k2_h (4 each), h_pows_inv row-major (16), z_h_x (returns its len),
+ * g1s (3 * (srs_n + 1) bytes). */
+static SRS make_srs(uint8_t secret, size_t srs_n, int srs_mode) {
+  SRS srs = srs_create(f101(secret), srs_n);
+  if (srs_mode == 1) {
+    G1 g = g1_generator();
+    GF s = f101(secret), sp = s;
+    for (size_t i = 0; i < srs.len; i++) {
+      srs.g1s[i] = g1_mul(&g, sp.value);
+      sp = gf_mul(sp, s);
+    }
+  }
+  return srs;
+}
+
+size_t ref_plonk4_data(uint8_t secret, size_t srs_n, int srs_mode, uint8_t *h, uint8_t *k1,
+                       uint8_t *k2, uint8_t *hinv, uint8_t *zh, uint8_t *g1s) {
+  SRS srs = make_srs(secret, srs_n, srs_mode);
+  memcpy(g1s, srs.g1s, 3 * srs.len);
+  PLONK plonk = plonk_new(srs, 4);
+  for (int i = 0; i < 4; i++) {
+    h[i] = plonk.h[i].value;
+    k1[i] = plonk.k1_h[i].value;
+    k2[i] = plonk.k2_h[i].value;
+    for (int c = 0; c < 4; c++) hinv[4 * i + c] = matrix_get(&plonk.h_pows_inv, i, c).value;
+  }
+  size_t zl = plonk.z_h_x.len;
+  memcpy(zh, plonk.z_h_x.coeffs, zl);
+  plonk_free(&plonk);
+  return zl;
+}
+
 /*
  * One 4-gate prove through the reference plonk_prove, inside a forked child so that the
  * reference's assert()/exit() on an unsatisfiable instance cannot take the caller down.
@@ -123,15 +157,7 @@ static void prove4_body(const uint8_t *gates, const uint8_t *copies, const uint8
                         const uint8_t *chal, const uint8_t *rnd, uint8_t secret, size_t srs_n,
                         int srs_mode, uint8_t *buf) {
     {
-    SRS srs = srs_create(f101(secret), srs_n);
-    if (srs_mode == 1) {
-      G1 g = g1_generator();
-      GF s = f101(secret), sp = s;
-      for (size_t i = 0; i < srs.len; i++) {
-        srs.g1s[i] = g1_mul(&g, sp.value);
-        sp = gf_mul(sp, s);
-      }
-    }
+    SRS srs = make_srs(secret, srs_n, srs_mode);
     PLONK plonk = plonk_new(srs, 4);
     CONSTRAINTS c;
     memset(&c, 0, sizeof c);

@@ -317,7 +317,7 @@ __global__ __launch_bounds__(1024) void polymul_small_kernel(const uint8_t* a8, 
     }
   }
   last = block_max(last);
-  if (threadIdx.x == 0) *nz = last;
+  if (threadIdx.x == 0 && nz) *nz = last;
 }
 
 // Trimmed length of out8[0, rl): index + 1 of the last non-zero byte, 0 if none (the
@@ -462,7 +462,7 @@ static size_t pass_lds(int M, int C, bool center) {
   return (center ? 2 : 1) * C * (size_t)col_stride((int)rows) * 4 + (center ? 2 : 1) * rows * 4 + (size_t)C * M * 4;
 }
 
-// d_out must hold la+lb-1 bytes; *d_nz receives the trimmed length (0 means "all zero" ->
+// d_out must hold la+lb-1 bytes; *d_nz (if not NULL) receives the trimmed length (0 means "all zero" ->
 // the caller reports length 1).
 int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
                         uint32_t* d_nz, void* d_work, hipStream_t st) {
@@ -479,7 +479,7 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
     hipLaunchKernelGGL(polymul_direct_kernel, dim3(blocks), dim3(256), 0, st, lg, la >= lb ? la : lb, sh, (int)mn,
                        d_out, d_nz);
     PLK_HIP(hipGetLastError());
-    hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d_out, rl, d_nz);
+    if (d_nz) hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d_out, rl, d_nz);
     PLK_HIP(hipGetLastError());
     return PLK_OK;
   }
@@ -498,7 +498,7 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
   uint32_t* B = A + (1ull << k);
   int rc = plk_wave_poly_mul_launch(d_a, la, d_b, lb, k, d_out, A, B, ninv, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d_out, rl, d_nz);
+  if (d_nz) hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d_out, rl, d_nz);
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }

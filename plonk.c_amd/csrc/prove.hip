@@ -1,0 +1,1028 @@
+// Device-resident PLONK prover (reference plonk_prove, src/plonk.h:223-656) on gfx950.
+//
+// Everything between the circuit upload and the 34 proof bytes runs on one stream with no
+// host round trip: the 17 poly_mul of the prover go through the NTT path (ntt.hip /
+// ntt_wave.hip), the poly_add / poly_sub / poly_scale / poly_add_hf chains are fused into
+// one "lincomb" kernel each, poly_eval is a batched reduction, poly_divide by Z_H = x^m + c
+// is a strided chain walk and by a linear factor a suffix scan, and the 9 KZG commitments
+// (srs_eval_at_s) are ONE batched discrete-log MSM launch over a [9][stride] scalar arena.
+// Scalars derived from evaluations (a_z, b_z, ... and the r(x) / w(x) coefficients) live in
+// a small device "scalar file" written by single-thread kernels, so no kernel waits on
+// the host.
+//
+// Polynomials are carried at upper-bound lengths (untrimmed).  Every reference operation
+// used here is value-identical under zero extension (poly_add/sub/scale/mul, poly_eval,
+// poly_divide by a trimmed divisor, poly_slice of the quotient), so the commitments and
+// evaluations -- hence the proof bytes -- equal the reference's; the trimmed lengths that
+// decide the reference's error exits (SRS too short, t(x) too short to slice, non-zero
+// remainders, failed asserts) are computed on the device and checked once at the end.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <initializer_list>
+#include <tuple>
+#include <utility>
+#include <vector>
+
+#include "plk_device.h"
+#include "plk_internal.h"
+
+namespace {
+
+constexpr uint32_t HFP = 17;
+
+// ------------------------------------------------------------------ scalar file layout
+enum Slot : int {
+  S_ZERO = 0, S_ONE, S_NEG1,
+  S_ALPHA, S_BETA, S_GAMMA, S_Z, S_V,
+  S_OMEGA, S_K1, S_K2,
+  S_BK1, S_BK2, S_ALPHA2, S_ZN2, S_Z2N4, S_V2, S_V3, S_V4, S_V5, S_V6, S_NEGZ, S_ZOMEGA,
+  // evaluations (round 4)
+  S_AZ = 32, S_BZ, S_CZ, S_S1Z, S_S2Z, S_TZ, S_ZWZ, S_L1Z, S_RZ, S_ACCW,
+  // derived from evaluations
+  S_AB = 48, S_R24, S_BZW, S_R3, S_W0, S_NEGZWZ,
+  // small constant polynomials (blinding factors), 4-byte aligned
+  P_BLA = 64, P_BLB = 68, P_BLC = 72, P_BLZ = 76,
+  NSLOT = 128
+};
+
+// status words (device -> host once per proof)
+enum Stat : int {
+  ST_LEN0 = 0,          // trimmed lengths of the 9 committed polynomials
+  ST_TXLEN = 9,         // trimmed length of t(x)
+  ST_REM_T = 10,        // t(x) numerator mod Z_H != 0
+  ST_REM_W1 = 11,       // w_z remainder != 0
+  ST_REM_W2 = 12,       // w_z_omega remainder != 0
+  ST_GATE = 13,         // 1 + first unsatisfied gate
+  ST_COPY = 14,         // 1 + first invalid copy constraint
+  ST_ACC = 15,          // acc_x(omega^n) (must be 1)
+  NSTAT = 16
+};
+
+__device__ __forceinline__ uint32_t hneg(uint32_t a) { return a ? HFP - a : 0; }
+__device__ __forceinline__ uint32_t hpow_d(uint32_t b, uint64_t e) {
+  uint32_t r = 1;
+  b %= HFP;
+  while (e) {
+    if (e & 1) r = r * b % HFP;
+    b = b * b % HFP;
+    e >>= 1;
+  }
+  return r;
+}
+__device__ __forceinline__ uint32_t hinv(uint32_t a) { return hpow_d(a, HFP - 2); }   // inv(0) = 0 (hf.h LUT)
+
+// ------------------------------------------------------------------ lincomb
+// out[i] = S[scale] * (sum_t S[slot_t] * p_t[i] + [i==0] S[c0] + [i==1] S[c1]) mod 17,
+// optionally times S[twist]^i.  Covers poly_add/sub/scale/add_hf chains (src/poly.h:67-104,
+// :179-197) and the z(omega x) twist (src/plonk.h:459-463).
+constexpr int LC_MAX = 10;
+struct LcArgs {
+  const uint8_t* p[LC_MAX];
+  uint64_t len[LC_MAX];
+  int slot[LC_MAX];
+  int nt;
+  int c0, c1;       // constant slots added at coefficients 0 / 1 (-1: none)
+  int scale;        // slot of the outer factor
+  int twist;        // slot x: multiply coefficient i by x^i (-1: none)
+  uint8_t* out;
+  uint64_t out_len;
+};
+
+__global__ __launch_bounds__(256) void lincomb_kernel(LcArgs a, const uint8_t* __restrict__ S) {
+  uint32_t cf[LC_MAX];
+#pragma unroll
+  for (int t = 0; t < LC_MAX; t++) cf[t] = t < a.nt ? S[a.slot[t]] : 0u;
+  const uint32_t sc = S[a.scale];
+  const uint32_t c0 = a.c0 >= 0 ? S[a.c0] : 0u, c1 = a.c1 >= 0 ? S[a.c1] : 0u;
+  uint32_t tw[16];
+  const uint32_t x = a.twist >= 0 ? S[a.twist] : 1u;
+  tw[0] = 1;
+#pragma unroll
+  for (int j = 1; j < 16; j++) tw[j] = tw[j - 1] * x % HFP;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.out_len; i += stride) {
+    uint32_t acc = i == 0 ? c0 : (i == 1 ? c1 : 0u);
+#pragma unroll
+    for (int t = 0; t < LC_MAX; t++)
+      if (t < a.nt && i < a.len[t]) acc += cf[t] * a.p[t][i];
+    uint32_t v = acc % HFP * sc % HFP;
+    if (a.twist >= 0) v = v * (i == 0 ? 1u : (x == 0 ? 0u : tw[i & 15])) % HFP;
+    a.out[i] = (uint8_t)v;
+  }
+}
+
+// ------------------------------------------------------------------ poly_eval (batched)
+// Horner of src/poly.h:265-272 == sum c_i x^i mod 17; x^i = x^(i mod 16) for x != 0.
+constexpr int EV_MAX = 12;
+constexpr int EV_BLOCKS = 64;
+struct EvArgs {
+  const uint8_t* p[EV_MAX];
+  uint64_t len[EV_MAX];
+  int xslot[EV_MAX];
+  int out[EV_MAX];
+  int ne;
+};
+
+__global__ __launch_bounds__(256) void eval_partial_kernel(EvArgs a, const uint8_t* __restrict__ S,
+                                                           uint32_t* __restrict__ part) {
+  const int e = blockIdx.y;
+  const uint32_t x = S[a.xslot[e]];
+  uint32_t pw[16];
+  pw[0] = 1;
+#pragma unroll
+  for (int j = 1; j < 16; j++) pw[j] = pw[j - 1] * x % HFP;
+  const uint8_t* p = a.p[e];
+  const uint64_t n = a.len[e];
+  uint32_t acc = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t w = i == 0 ? 1u : (x == 0 ? 0u : pw[i & 15]);
+    acc += w * p[i];
+    if ((i & 0xFFFF) == 0) acc %= HFP;   // never overflows: < 2^16 terms of <= 256 between folds
+  }
+  acc %= HFP;
+  __shared__ uint32_t red[256];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[e * EV_BLOCKS + blockIdx.x] = red[0] % HFP;
+}
+
+__global__ void eval_final_kernel(EvArgs a, const uint32_t* __restrict__ part, uint8_t* __restrict__ S) {
+  const int e = threadIdx.x;
+  if (e >= a.ne) return;
+  uint32_t s = 0;
+  for (int b = 0; b < EV_BLOCKS; b++) s += part[e * EV_BLOCKS + b];
+  S[a.out[e]] = (uint8_t)(s % HFP);
+}
+
+// ------------------------------------------------------------------ poly_divide
+// (a) divisor L x^m + c (Z_H of a multiplicative subgroup is x^n - 1): the long division
+// of src/poly.h:124-177 gives q[j] = L^-1 (num[j+m] - c q[j+m]) and rem[r] = num[r] - c q[r]
+// (r < m) -- independent chains per residue r mod m, walked top-down by one thread each.
+__global__ __launch_bounds__(256) void divide_binomial_kernel(const uint8_t* __restrict__ num, uint64_t nl,
+                                                              uint64_t m, uint32_t lead, uint32_t c,
+                                                              uint8_t* __restrict__ q, uint64_t ql,
+                                                              uint32_t* __restrict__ rem_flag) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= m) return;
+  const uint32_t li = hinv(lead);
+  const uint32_t nc = hneg(c);
+  uint32_t prev = 0;   // q[j + m]
+  if (nl > m && r < ql) {
+    uint64_t j = r + ((ql - 1 - r) / m) * m;   // top of the chain
+    for (;;) {
+      const uint32_t v = (num[j + m] + nc * prev) % HFP * li % HFP;
+      q[j] = (uint8_t)v;
+      prev = v;
+      if (j < m) break;
+      j -= m;
+    }
+  }
+  if (r < nl) {
+    const uint32_t rv = (num[r] + nc * prev) % HFP;   // prev = q[r] (0 if none)
+    if (rv) atomicOr(rem_flag, 1u);
+  }
+}
+
+// (b) divisor d1 x + d0: the long division gives q[j] = b num[j+1] + a q[j+1] with
+// a = -d0/d1, b = 1/d1, i.e. q[j] = b a^-(j+1) sum_{i>j} num[i] a^i  (a != 0; a^i = a^(i mod 16)).
+// The prover only divides by x - z and x - z omega (d1 = 1).  Three-phase suffix scan over
+// 4096-element blocks.
+constexpr int SCAN_T = 256, SCAN_E = 16, SCAN_B = SCAN_T * SCAN_E;
+
+__global__ __launch_bounds__(SCAN_T) void lin_scan_sums_kernel(const uint8_t* __restrict__ num, uint64_t nl,
+                                                                const uint8_t* __restrict__ S, int aslot,
+                                                                uint32_t* __restrict__ bsum) {
+  const uint32_t a = S[aslot];
+  uint32_t pw[16];
+  pw[0] = 1;
+#pragma unroll
+  for (int j = 1; j < 16; j++) pw[j] = pw[j - 1] * a % HFP;
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_B + threadIdx.x;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_E; k++) {
+    const uint64_t i = base + (uint64_t)k * SCAN_T;
+    if (i < nl && i > 0) acc += num[i] * pw[i & 15];
+  }
+  __shared__ uint32_t red[SCAN_T];
+  red[threadIdx.x] = acc % HFP;
+  __syncthreads();
+  for (int s = SCAN_T / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bsum[blockIdx.x] = red[0] % HFP;
+}
+
+// exclusive suffix sums of the block sums (one block)
+__global__ __launch_bounds__(1024) void lin_scan_carry_kernel(uint32_t* __restrict__ bsum, int nb) {
+  __shared__ uint32_t t[1024];
+  uint32_t carry = 0;
+  for (int hi = nb; hi > 0; hi -= 1024) {
+    const int lo = hi - 1024 > 0 ? hi - 1024 : 0;
+    const int i = lo + (int)threadIdx.x;
+    const uint32_t v = i < hi ? bsum[i] : 0u;
+    t[threadIdx.x] = v;
+    __syncthreads();
+    // inclusive suffix scan (Hillis-Steele)
+    for (int s = 1; s < 1024; s <<= 1) {
+      const uint32_t add = (int)threadIdx.x + s < 1024 ? t[threadIdx.x + s] : 0u;
+      __syncthreads();
+      t[threadIdx.x] = (t[threadIdx.x] + add) % HFP;
+      __syncthreads();
+    }
+    if (i < hi) bsum[i] = (t[threadIdx.x] + HFP - v + carry) % HFP;   // exclusive + carry
+    const uint32_t tot = t[0];
+    __syncthreads();
+    carry = (carry + tot) % HFP;
+  }
+}
+
+// divisor x - a (d1 = 1, d0 = -a): q[j] = a^-(j+1) sum_{i>j} num[i] a^i, rem = num[0] + a q[0]
+__global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(const uint8_t* __restrict__ num, uint64_t nl,
+                                                                 const uint8_t* __restrict__ S, int aslot,
+                                                                 const uint32_t* __restrict__ carry,
+                                                                 uint8_t* __restrict__ q, uint32_t* rem_flag) {
+  const uint32_t a = S[aslot];
+  uint32_t pw[16], ipw[16];
+  pw[0] = ipw[0] = 1;
+  const uint32_t ai = hinv(a);
+#pragma unroll
+  for (int j = 1; j < 16; j++) { pw[j] = pw[j - 1] * a % HFP; ipw[j] = ipw[j - 1] * ai % HFP; }
+  // thread owns SCAN_E consecutive elements [base, base + SCAN_E)
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_B + (uint64_t)threadIdx.x * SCAN_E;
+  uint32_t w[SCAN_E];
+  uint32_t tot = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_E; k++) {
+    const uint64_t i = base + k;
+    w[k] = (i < nl && i > 0) ? num[i] * pw[i & 15] % HFP : 0u;
+    tot += w[k];
+  }
+  __shared__ uint32_t t[SCAN_T];
+  t[threadIdx.x] = tot % HFP;
+  __syncthreads();
+  for (int s = 1; s < SCAN_T; s <<= 1) {
+    const uint32_t add = (int)threadIdx.x + s < SCAN_T ? t[threadIdx.x + s] : 0u;
+    __syncthreads();
+    t[threadIdx.x] = (t[threadIdx.x] + add) % HFP;
+    __syncthreads();
+  }
+  // sum of w over elements after this thread's chunk
+  uint32_t run = ((int)threadIdx.x + 1 < SCAN_T ? t[threadIdx.x + 1] : 0u) + carry[blockIdx.x];
+  const uint64_t ql = nl - 1;
+#pragma unroll
+  for (int k = SCAN_E - 1; k >= 0; k--) {
+    const uint64_t j = base + k;   // run = sum_{i > j} w_i
+    if (j < ql) {
+      uint32_t v;
+      if (a == 0) v = num[j + 1];
+      else v = run % HFP * ipw[(j + 1) & 15] % HFP;
+      q[j] = (uint8_t)v;
+      if (j == 0) {
+        const uint32_t r0 = (num[0] + a * v) % HFP;
+        if (r0) atomicOr(rem_flag, 1u);
+      }
+    }
+    run += w[k];
+  }
+}
+
+// (c) any other divisor: the reference's long division in one workgroup (only reached for
+// tiny non-subgroup H, e.g. n = 3).
+__global__ __launch_bounds__(256) void divide_general_kernel(const uint8_t* __restrict__ num, uint64_t nl,
+                                                             const uint8_t* __restrict__ den, uint64_t dl,
+                                                             uint8_t* __restrict__ rem, uint8_t* __restrict__ q,
+                                                             uint32_t* rem_flag) {
+  for (uint64_t i = threadIdx.x; i < nl; i += blockDim.x) rem[i] = num[i];
+  __syncthreads();
+  const uint32_t li = hinv(den[dl - 1]);
+  for (int64_t i = (int64_t)nl - 1; i >= (int64_t)dl - 1; i--) {
+    const uint32_t coeff = rem[i] * li % HFP;
+    __syncthreads();
+    if (threadIdx.x == 0) q[i - (dl - 1)] = (uint8_t)coeff;
+    for (uint64_t j = threadIdx.x; j < dl; j += blockDim.x)
+      rem[i - j] = (uint8_t)((rem[i - j] + HFP - coeff * den[dl - 1 - j] % HFP) % HFP);
+    __syncthreads();
+  }
+  const uint64_t rl = dl - 1 < nl ? dl - 1 : nl;
+  for (uint64_t i = threadIdx.x; i < rl; i += blockDim.x)
+    if (rem[i]) atomicOr(rem_flag, 1u);
+}
+
+// ------------------------------------------------------------------ trimmed lengths
+// one block per buffer: index + 1 of the last non-zero byte, at least 1 (src/poly.h:20-24)
+struct TrimArgs {
+  const uint8_t* p[10];
+  uint64_t len[10];
+  int dst[10];
+};
+__global__ __launch_bounds__(256) void trim_many_kernel(TrimArgs a, uint32_t* __restrict__ stat) {
+  const uint8_t* p = a.p[blockIdx.x];
+  const uint64_t n = a.len[blockIdx.x];
+  __shared__ uint32_t best;
+  if (threadIdx.x == 0) best = 0;
+  __syncthreads();
+  for (uint64_t hi = n; hi > 0;) {
+    const uint64_t lo = hi > 4096 ? hi - 4096 : 0;
+    uint32_t last = 0;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
+      if (p[i]) last = max(last, (uint32_t)(i + 1));
+    if (last) atomicMax(&best, last);
+    __syncthreads();
+    const uint32_t b = best;
+    __syncthreads();
+    if (b) break;
+    hi = lo;
+  }
+  if (threadIdx.x == 0) stat[a.dst[blockIdx.x]] = best ? best : 1u;
+}
+
+// ------------------------------------------------------------------ scalar programs
+__global__ void scalars_r4_kernel(uint8_t* S) {
+  const uint32_t al = S[S_ALPHA], be = S[S_BETA], ga = S[S_GAMMA], z = S[S_Z];
+  const uint32_t az = S[S_AZ], bz = S[S_BZ], cz = S[S_CZ], s1 = S[S_S1Z], s2 = S[S_S2Z];
+  const uint32_t zw = S[S_ZWZ], l1 = S[S_L1Z];
+  S[S_AB] = (uint8_t)(az * bz % HFP);
+  // src/plonk.h:547-556: r_2 scale
+  const uint32_t x1 = (az + be * z + ga) % HFP;
+  const uint32_t x2 = (bz + be * S[S_K1] % HFP * z + ga) % HFP;
+  const uint32_t x3 = (cz + be * S[S_K2] % HFP * z + ga) % HFP;
+  const uint32_t r2 = x1 * x2 % HFP * x3 % HFP * al % HFP;
+  // src/plonk.h:569: r_4 scale
+  const uint32_t r4 = l1 * S[S_ALPHA2] % HFP;
+  S[S_R24] = (uint8_t)((r2 + r4) % HFP);
+  // src/plonk.h:559-566: r_3
+  S[S_BZW] = (uint8_t)(be * zw % HFP);
+  const uint32_t y1 = (az + be * s1 + ga) % HFP, y2 = (bz + be * s2 + ga) % HFP;
+  S[S_R3] = (uint8_t)(y1 * y2 % HFP * al % HFP);
+  S[S_NEGZWZ] = (uint8_t)hneg(zw);
+}
+
+__global__ void scalars_r5_kernel(uint8_t* S) {
+  // constant term of w_z(x), src/plonk.h:584-603
+  uint32_t c = hneg(S[S_TZ]);
+  c += S[S_V] * hneg(S[S_RZ]);
+  c += S[S_V2] * hneg(S[S_AZ]);
+  c += S[S_V3] * hneg(S[S_BZ]);
+  c += S[S_V4] * hneg(S[S_CZ]);
+  c += S[S_V5] * hneg(S[S_S1Z]);
+  c += S[S_V6] * hneg(S[S_S2Z]);
+  S[S_W0] = (uint8_t)(c % HFP);
+}
+
+// 9 commitments (4-byte records from msm_finalize_kernel) + 7 evaluations -> PROOF
+// (src/plonk.h:24-41: 9 x G1 {x, y, infinite}, then a_z b_z c_z s1_z s2_z r_z z_omega_z)
+__global__ void proof_pack_kernel(const uint8_t* __restrict__ g4, const uint8_t* __restrict__ S,
+                                  uint8_t* __restrict__ proof) {
+  const int t = threadIdx.x;
+  if (t < 27) proof[t] = g4[4 * (t / 3) + t % 3];
+  const int ev[7] = {S_AZ, S_BZ, S_CZ, S_S1Z, S_S2Z, S_RZ, S_ZWZ};
+  if (t >= 27 && t < 34) proof[t] = S[ev[t - 27]];
+}
+
+// ------------------------------------------------------------------ stage A (circuit)
+// constraints_satisfy (src/constraints.h:145-171) and copy_constraints_to_roots
+// (src/plonk.h:141-160): one thread per gate.
+__global__ void circuit_check_kernel(const uint8_t* __restrict__ cir, uint64_t n, const uint8_t* __restrict__ h3,
+                                     uint8_t* __restrict__ vals, uint32_t* __restrict__ stat) {
+  // cir: q_m q_l q_r q_o q_c | copies a,b,c as (type, index) pairs | a b c   (n each / 2n each)
+  // vals (11 x n): a b c q_o q_m q_l q_r q_c sigma1 sigma2 sigma3
+  const uint8_t *qm = cir, *ql = cir + n, *qr = cir + 2 * n, *qo = cir + 3 * n, *qc = cir + 4 * n;
+  const uint8_t* cp = cir + 5 * n;
+  const uint8_t *wa = cir + 11 * n, *wb = cir + 12 * n, *wc = cir + 13 * n;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t a = wa[i], b = wb[i], c = wc[i];
+    const uint32_t lhs = (ql[i] * a + qr[i] * b + qo[i] * c + qm[i] * (a * b % HFP) + qc[i]) % HFP;
+    if (lhs) atomicMin(&stat[ST_GATE], (uint32_t)i + 1);
+    vals[0 * n + i] = (uint8_t)a;
+    vals[1 * n + i] = (uint8_t)b;
+    vals[2 * n + i] = (uint8_t)c;
+    vals[3 * n + i] = qo[i];
+    vals[4 * n + i] = qm[i];
+    vals[5 * n + i] = ql[i];
+    vals[6 * n + i] = qr[i];
+    vals[7 * n + i] = qc[i];
+    for (int k = 0; k < 3; k++) {
+      const uint32_t type = cp[2 * (k * n + i)], idx = cp[2 * (k * n + i) + 1];
+      uint8_t s = 0;
+      if (type > 2 || idx == 0 || idx > n) atomicMin(&stat[ST_COPY], (uint32_t)(k * n + i) + 1);
+      else s = h3[type * n + (idx - 1)];   // h | k1_h | k2_h
+      vals[(8 + k) * n + i] = s;
+    }
+  }
+}
+
+// interpolate_at_h (src/plonk.h:162-195): out[v][r] = sum_c Hinv[r][c] vals[v][c] (matrix_mul,
+// src/matrix.h:81), batched over nv vectors; one thread per (vector, row).
+__global__ void interpolate_kernel(const uint8_t* __restrict__ hinvm, uint64_t n, const uint8_t* __restrict__ vals,
+                                   int nv, uint8_t* const* __restrict__ outs) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (uint64_t)nv * n) return;
+  const uint64_t v = t / n, r = t % n;
+  uint32_t acc = 0;
+  for (uint64_t c = 0; c < n; c++) {
+    acc += hinvm[r * n + c] * vals[v * n + c];
+    if ((c & 0xFFFF) == 0xFFFF) acc %= HFP;
+  }
+  outs[v][r] = (uint8_t)(acc % HFP);
+}
+
+// Round 2 grand product (src/plonk.h:326-359).  The s_sigma evaluations at omega^(i-1) take
+// at most 16 distinct points, evaluated by all threads first; the prefix product is serial
+// (n is the size of a subgroup of GF(17)*: <= 16).
+__global__ void grand_product_kernel(const uint8_t* __restrict__ vals, uint64_t n, const uint8_t* const* polys,
+                                     const uint8_t* __restrict__ S, uint8_t* __restrict__ acc) {
+  __shared__ uint32_t ev[3][16];
+  const uint32_t om = S[S_OMEGA];
+  for (int t = threadIdx.x; t < 48; t += blockDim.x) {
+    const int k = t / 16, j = t % 16;
+    const uint32_t x = hpow_d(om, j);
+    const uint8_t* p = polys[8 + k];   // s_sigma_1..3
+    uint32_t y = 0;
+    for (int64_t i = (int64_t)n - 1; i >= 0; i--) y = (y * x + p[i]) % HFP;
+    ev[k][j] = y;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const uint32_t be = S[S_BETA], ga = S[S_GAMMA], k1 = S[S_K1], k2 = S[S_K2];
+  uint32_t a = 1;
+  acc[0] = 1;
+  for (uint64_t i = 1; i < n; i++) {
+    const uint32_t wa = vals[i - 1], wb = vals[n + i - 1], wc = vals[2 * n + i - 1];
+    // hf_pow(omega, i-1) = omega^((i-1) mod 16): OMEGA = 4 is a unit
+    const uint32_t j = (uint32_t)((i - 1) & 15);
+    const uint32_t op = hpow_d(om, j);
+    const uint32_t den = (wa + be * op + ga) % HFP * ((wb + be * (k1 * op % HFP) + ga) % HFP) % HFP *
+                         ((wc + be * (k2 * op % HFP) + ga) % HFP) % HFP;
+    const uint32_t e1 = ev[0][j], e2 = ev[1][j], e3 = ev[2][j];
+    const uint32_t num = (wa + be * e1 + ga) % HFP * ((wb + be * e2 + ga) % HFP) % HFP * ((wc + be * e3 + ga) % HFP) % HFP;
+    a = a * (den * hinv(num) % HFP) % HFP;
+    acc[i] = (uint8_t)a;
+  }
+}
+
+__global__ void unit_vector_kernel(uint8_t* v, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    v[i] = i == 0 ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ host side
+uint8_t h_pow(uint32_t b, uint64_t e) {
+  uint32_t r = 1;
+  b %= HFP;
+  while (e) {
+    if (e & 1) r = r * b % HFP;
+    b = b * b % HFP;
+    e >>= 1;
+  }
+  return (uint8_t)r;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ prover object
+struct plk_prover {
+  size_t n = 0;
+  size_t srs_len = 0;
+  bool srs_irregular = false;
+  // Z_H shape (host analysis of the trimmed divisor)
+  size_t zh_len = 0;
+  int zh_kind = 0;   // 0 binomial L x^m + c, 1 general
+  uint32_t zh_lead = 1, zh_c = 0;
+  bool have_circuit_tables = false;
+  // device memory (one allocation, carved)
+  uint8_t* mem = nullptr;
+  size_t mem_bytes = 0;
+  uint8_t *d_srs = nullptr, *d_zh = nullptr, *d_h3 = nullptr, *d_hinv = nullptr;
+  uint8_t* d_S = nullptr;          // scalar file
+  uint32_t* d_stat = nullptr;      // status words
+  uint32_t* d_part = nullptr;      // eval partials
+  uint32_t* d_bsum = nullptr;      // scan block sums
+  PlkMsmResult* d_res = nullptr;   // 9 MSM records
+  uint8_t* d_g4 = nullptr;         // 9 x 4 bytes
+  uint8_t* d_proof = nullptr;
+  uint8_t* arena = nullptr;        // [9][cstride] committed polynomials
+  size_t cstride = 0, cmax = 0;
+  uint8_t* d_polys[13] = {};       // stage-A outputs (circuit path)
+  uint8_t* d_cir = nullptr;        // circuit upload
+  uint8_t* d_vals = nullptr;       // 11 x n values to interpolate
+  uint8_t** d_outs = nullptr;      // device array of the 13 poly pointers
+  // intermediates
+  uint8_t *blA, *blB, *blC, *zB, *AB, *ABQM, *AQL, *BQR, *CQO, *A2, *B2, *C2, *T2a, *T2b, *T2, *A3, *B3, *C3, *ZW,
+      *T3a, *T3b, *T3, *Z1, *T4, *NUM, *TX, *RX, *S3S, *P3, *W, *ZZ, *REMT, *ACCV, *E0;
+  void* work = nullptr;
+  size_t work_bytes = 0;
+  hipStream_t st = nullptr;
+  // host staging of async uploads (alive until the call's final stream synchronize)
+  uint8_t hS[NSLOT];
+  uint8_t hS0[NSLOT];
+  uint8_t h_om;
+};
+
+namespace {
+
+// upper-bound lengths of every polynomial of rounds 1-5 for n gates and |Z_H| = lz
+struct Lens {
+  uint64_t n, lz, la, lzx, lab, labqm, lq1, lt1, l2a, l2b, l2, lzw, l3, lz1, lt4, lnum, lq, ltx, lr3, lrx, lw, lwq,
+      lzz, lwo;
+};
+Lens lens_for(uint64_t n, uint64_t lz) {
+  Lens L{};
+  L.n = n;
+  L.lz = lz;
+  L.la = std::max<uint64_t>(lz + 1, n);          // a_x, b_x, c_x
+  L.lzx = std::max<uint64_t>(lz + 2, n);         // z_x
+  L.lab = 2 * L.la - 1;                          // a_x b_x
+  L.labqm = L.lab + n - 1;                       // (a_x b_x) q_m
+  L.lq1 = L.la + n - 1;                          // a_x q_l, ...
+  L.lt1 = std::max(L.labqm, L.lq1);
+  L.l2a = 2 * L.la - 1;                          // A2 B2
+  L.l2b = L.l2a + L.la - 1;                      // (A2 B2) C2
+  L.l2 = L.l2b + L.lzx - 1;                      // ... z_x
+  L.lzw = L.lzx;
+  L.l3 = L.l2b + L.lzw - 1;
+  L.lz1 = L.lzx;
+  L.lt4 = L.lz1 + n - 1;
+  L.lnum = std::max(std::max(L.lt1, L.l2), std::max(L.l3, L.lt4));
+  // quotient by Z_H (len lz)
+  L.ltx = L.lnum >= lz ? L.lnum - lz + 1 : 1;
+  L.lr3 = L.lzx + n - 1;                         // z_x * (s_sigma_3 scaled)
+  L.lrx = std::max(std::max<uint64_t>(n, L.lzx), L.lr3);
+  const uint64_t p = n + 2;
+  const uint64_t lhi = L.ltx > 2 * p ? L.ltx - 2 * p : 1;
+  L.lw = std::max(std::max<uint64_t>(p, lhi), std::max(L.lrx, std::max<uint64_t>(L.la, n)));
+  L.lwq = L.lw >= 2 ? L.lw - 1 : 1;
+  L.lzz = L.lzx;
+  L.lwo = L.lzz >= 2 ? L.lzz - 1 : 1;
+  return L;
+}
+
+struct Bump {
+  size_t off = 0;
+  size_t take(size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  }
+};
+
+int lincomb(plk_prover* P, std::initializer_list<std::pair<const uint8_t*, uint64_t>> terms,
+            std::initializer_list<int> slots, int c0, int c1, int scale, int twist, uint8_t* out, uint64_t out_len) {
+  LcArgs a{};
+  int t = 0;
+  for (const auto& pr : terms) { a.p[t] = pr.first; a.len[t] = pr.second; t++; }
+  int s = 0;
+  for (int sl : slots) a.slot[s++] = sl;
+  if (t != s || t > LC_MAX) { plk_set_error("lincomb: %d terms / %d slots", t, s); return PLK_ERR_ARG; }
+  a.nt = t;
+  a.c0 = c0;
+  a.c1 = c1;
+  a.scale = scale;
+  a.twist = twist;
+  a.out = out;
+  a.out_len = out_len;
+  const uint64_t blocks = std::min<uint64_t>((out_len + 255) / 256, 2048);
+  hipLaunchKernelGGL(lincomb_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, a, P->d_S);
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
+int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64_t, int, int>> ev) {
+  EvArgs a{};
+  int e = 0;
+  for (const auto& t : ev) {
+    a.p[e] = std::get<0>(t);
+    a.len[e] = std::get<1>(t);
+    a.xslot[e] = std::get<2>(t);
+    a.out[e] = std::get<3>(t);
+    e++;
+  }
+  a.ne = e;
+  hipLaunchKernelGGL(eval_partial_kernel, dim3(EV_BLOCKS, e), dim3(256), 0, P->st, a, P->d_S, P->d_part);
+  PLK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(eval_final_kernel, dim3(1), dim3(64), 0, P->st, a, P->d_part, P->d_S);
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
+int pmul(plk_prover* P, const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb, uint8_t* out) {
+  return plk_poly_mul_launch(a, la, b, lb, out, nullptr, P->work, P->st);
+}
+
+// divide num (upper-bound length nl) by Z_H; q gets ltx bytes
+int divide_zh(plk_prover* P, const uint8_t* num, uint64_t nl, uint8_t* q, uint64_t ql, uint32_t* flag) {
+  PLK_HIP(hipMemsetAsync(q, 0, ql, P->st));
+  if (P->zh_kind == 0) {
+    const uint64_t m = P->zh_len - 1;
+    hipLaunchKernelGGL(divide_binomial_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, P->st, num, nl, m,
+                       P->zh_lead, P->zh_c, q, ql, flag);
+  } else {
+    if (nl > (1u << 20)) { plk_set_error("poly_divide: non-binomial Z_H with %llu coefficients", (unsigned long long)nl); return PLK_ERR_RANGE; }
+    hipLaunchKernelGGL(divide_general_kernel, dim3(1), dim3(256), 0, P->st, num, nl, P->d_zh, (uint64_t)P->zh_len,
+                       P->REMT, q, flag);
+  }
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
+// divide num by x - S[aslot]; q gets nl - 1 bytes
+int divide_linear(plk_prover* P, const uint8_t* num, uint64_t nl, int aslot, uint8_t* q, uint32_t* flag) {
+  if (nl < 2) {   // quotient [0]; remainder = num (checked by trim)
+    PLK_HIP(hipMemsetAsync(q, 0, 1, P->st));
+    return PLK_OK;
+  }
+  const uint64_t nb = (nl + SCAN_B - 1) / SCAN_B;
+  hipLaunchKernelGGL(lin_scan_sums_kernel, dim3((unsigned)nb), dim3(SCAN_T), 0, P->st, num, nl, P->d_S, aslot,
+                     P->d_bsum);
+  PLK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(lin_scan_carry_kernel, dim3(1), dim3(1024), 0, P->st, P->d_bsum, (int)nb);
+  PLK_HIP(hipGetLastError());
+  // denominators poly_new({-z, 1}) and ({-z omega, 1}), src/plonk.h:604-613
+  hipLaunchKernelGGL(lin_scan_apply_kernel, dim3((unsigned)nb), dim3(SCAN_T), 0, P->st, num, nl, P->d_S, aslot,
+                     P->d_bsum, q, flag);
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
+  if (!d || !out) { plk_set_error("plk_prover_create: NULL argument"); return PLK_ERR_ARG; }
+  *out = nullptr;
+  if (d->n == 0 || !d->z_h || d->z_h_len == 0 || !d->srs_g1 || d->srs_len == 0) {
+    plk_set_error("plk_prover_create: n, z_h and srs are required");
+    return PLK_ERR_ARG;
+  }
+  int rc = plk_init(-1);
+  if (rc) return rc;
+  plk_prover* P = new plk_prover();
+  P->n = d->n;
+  P->srs_len = d->srs_len;
+  // Z_H: trimmed as poly_z returns it; classify
+  size_t zl = d->z_h_len;
+  while (zl > 1 && d->z_h[zl - 1] == 0) zl--;
+  if (zl == 1 && d->z_h[0] == 0) { delete P; plk_set_error("Division by zero polynomial in poly_divide"); return PLK_ERR_ARG; }
+  P->zh_len = zl;
+  P->zh_lead = d->z_h[zl - 1] % HFP;
+  P->zh_c = d->z_h[0] % HFP;
+  P->zh_kind = 0;
+  if (zl < 2) P->zh_kind = 1;
+  for (size_t i = 1; i + 1 < zl; i++)
+    if (d->z_h[i] % HFP) P->zh_kind = 1;
+  P->have_circuit_tables = d->h && d->k1_h && d->k2_h && d->h_pows_inv;
+
+  const Lens L = lens_for(P->n, P->zh_len);
+  const uint64_t n = P->n;
+  // commitments: a b c z t_lo t_mid t_hi w_z w_zw
+  P->cmax = std::max(std::max(L.la, L.lzx), std::max(std::max(n + 2, L.ltx), std::max(L.lwq, L.lwo)));
+  P->cstride = (P->cmax + 15) & ~(size_t)15;
+  // poly_mul workspace: the largest product shape
+  size_t ws = 0;
+  const uint64_t shapes[][2] = {{2, L.lz},       {3, L.lz},       {L.la, L.la},   {L.lab, n},    {L.la, n},
+                                {L.la, L.la},    {L.l2a, L.la},   {L.l2b, L.lzx}, {L.l2b, L.lzw}, {L.lz1, n},
+                                {L.lzx, n}};
+  for (const auto& s : shapes) ws = std::max(ws, plk_poly_mul_workspace_bytes(s[0], s[1]));
+  Bump B;
+  const size_t o_srs = B.take(3 * P->srs_len + 16), o_zh = B.take(zl + 16), o_h3 = B.take(3 * n + 16),
+               o_hinv = B.take(P->have_circuit_tables ? n * n + 16 : 16), o_S = B.take(NSLOT),
+               o_stat = B.take(4 * NSTAT), o_part = B.take(4 * EV_MAX * EV_BLOCKS),
+               o_bsum = B.take(4 * ((L.lw + SCAN_B - 1) / SCAN_B + 2) + 4 * ((L.lzz + SCAN_B) / SCAN_B + 2)),
+               o_res = B.take(9 * sizeof(PlkMsmResult)), o_g4 = B.take(64), o_proof = B.take(64),
+               o_arena = B.take(9 * P->cstride);
+  size_t o_polys[13];
+  for (int i = 0; i < 13; i++) o_polys[i] = B.take(n + 16);
+  const size_t o_cir = B.take(14 * n + 16), o_vals = B.take(11 * n + 16), o_outs = B.take(13 * sizeof(void*));
+  struct { uint8_t** p; uint64_t len; } iv[] = {
+      {&P->blA, L.lz + 1}, {&P->blB, L.lz + 1}, {&P->blC, L.lz + 1}, {&P->zB, L.lz + 2}, {&P->AB, L.lab},
+      {&P->ABQM, L.labqm}, {&P->AQL, L.lq1}, {&P->BQR, L.lq1}, {&P->CQO, L.lq1}, {&P->A2, L.la}, {&P->B2, L.la},
+      {&P->C2, L.la}, {&P->T2a, L.l2a}, {&P->T2b, L.l2b}, {&P->T2, L.l2}, {&P->A3, L.la}, {&P->B3, L.la},
+      {&P->C3, L.la}, {&P->ZW, L.lzw}, {&P->T3a, L.l2a}, {&P->T3b, L.l2b}, {&P->T3, L.l3}, {&P->Z1, L.lz1},
+      {&P->T4, L.lt4}, {&P->NUM, L.lnum}, {&P->TX, L.ltx}, {&P->RX, L.lrx}, {&P->S3S, n}, {&P->P3, L.lr3},
+      {&P->W, L.lw}, {&P->ZZ, L.lzz}, {&P->REMT, L.lnum}, {&P->ACCV, n}, {&P->E0, n}};
+  size_t o_iv[sizeof(iv) / sizeof(iv[0])];
+  for (size_t i = 0; i < sizeof(iv) / sizeof(iv[0]); i++) o_iv[i] = B.take(iv[i].len + 16);
+  const size_t o_work = B.take(ws + 16);
+  P->mem_bytes = B.off;
+  if (hipMalloc((void**)&P->mem, P->mem_bytes) != hipSuccess) {
+    plk_set_error("plk_prover_create: hipMalloc(%zu) failed", P->mem_bytes);
+    delete P;
+    return PLK_ERR_NOMEM;
+  }
+  uint8_t* m = P->mem;
+  P->d_srs = m + o_srs; P->d_zh = m + o_zh; P->d_h3 = m + o_h3; P->d_hinv = m + o_hinv; P->d_S = m + o_S;
+  P->d_stat = (uint32_t*)(m + o_stat); P->d_part = (uint32_t*)(m + o_part); P->d_bsum = (uint32_t*)(m + o_bsum);
+  P->d_res = (PlkMsmResult*)(m + o_res); P->d_g4 = m + o_g4; P->d_proof = m + o_proof; P->arena = m + o_arena;
+  for (int i = 0; i < 13; i++) P->d_polys[i] = m + o_polys[i];
+  P->d_cir = m + o_cir; P->d_vals = m + o_vals; P->d_outs = (uint8_t**)(m + o_outs);
+  for (size_t i = 0; i < sizeof(iv) / sizeof(iv[0]); i++) *iv[i].p = m + o_iv[i];
+  P->work = m + o_work;
+  P->work_bytes = ws;
+  P->st = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&P->st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMemsetAsync(P->mem, 0, P->mem_bytes, P->st);
+  if (e == hipSuccess) e = hipMemcpyAsync(P->d_srs, d->srs_g1, 3 * P->srs_len, hipMemcpyHostToDevice, P->st);
+  if (e == hipSuccess) e = hipMemcpyAsync(P->d_zh, d->z_h, zl, hipMemcpyHostToDevice, P->st);
+  if (e == hipSuccess && P->have_circuit_tables) {
+    e = hipMemcpyAsync(P->d_h3, d->h, n, hipMemcpyHostToDevice, P->st);
+    if (e == hipSuccess) e = hipMemcpyAsync(P->d_h3 + n, d->k1_h, n, hipMemcpyHostToDevice, P->st);
+    if (e == hipSuccess) e = hipMemcpyAsync(P->d_h3 + 2 * n, d->k2_h, n, hipMemcpyHostToDevice, P->st);
+    if (e == hipSuccess) e = hipMemcpyAsync(P->d_hinv, d->h_pows_inv, n * n, hipMemcpyHostToDevice, P->st);
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(P->d_outs, P->d_polys, 13 * sizeof(void*), hipMemcpyHostToDevice, P->st);
+  if (e != hipSuccess) {
+    plk_set_error("plk_prover_create: %s", hipGetErrorString(e));
+    plk_prover_destroy(P);
+    return PLK_ERR_HIP;
+  }
+  {  // SRS encodings: one probe MSM decides whether every point is canonical (fast path)
+    uint8_t* d_ones = nullptr;
+    if (hipMalloc((void**)&d_ones, P->srs_len + 16) != hipSuccess) { plk_prover_destroy(P); plk_set_error("hipMalloc"); return PLK_ERR_NOMEM; }
+    (void)hipMemsetAsync(d_ones, 1, P->srs_len, P->st);
+    (void)hipMemsetAsync(P->d_res, 0, sizeof(PlkMsmResult), P->st);
+    rc = plk_msm_launch(P->d_srs, d_ones, P->srs_len, P->d_res, P->st);
+    PlkMsmResult h{};
+    if (!rc && hipMemcpyAsync(&h, P->d_res, sizeof h, hipMemcpyDeviceToHost, P->st) == hipSuccess &&
+        hipStreamSynchronize(P->st) == hipSuccess) {
+      P->srs_irregular = h.irregular != 0;
+    } else if (!rc) {
+      rc = PLK_ERR_HIP;
+    }
+    (void)hipFree(d_ones);
+    if (rc) { plk_prover_destroy(P); return rc; }
+  }
+  *out = P;
+  return PLK_OK;
+}
+
+void plk_prover_destroy(plk_prover_t* P) {
+  if (!P) return;
+  if (P->st) (void)hipStreamSynchronize(P->st);
+  (void)hipFree(P->mem);
+  if (P->st) (void)hipStreamDestroy(P->st);
+  delete P;
+}
+
+size_t plk_prover_device_bytes(const plk_prover_t* P) { return P ? P->mem_bytes : 0; }
+
+}  // extern "C"
+
+namespace {
+
+// rounds 1-5 (src/plonk.h:277-655) on polys[13] = f_a f_b f_c q_o q_m q_l q_r q_c s1 s2 s3 acc_x l_1_x
+// (each of length <= n, zero padded to n).  Enqueued on P->st; status words in P->d_stat.
+int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const uint8_t rnd[9]) {
+  const uint64_t n = P->n;
+  const Lens L = lens_for(n, P->zh_len);
+  const uint8_t *FA = pl[0], *FB = pl[1], *FC = pl[2], *QO = pl[3], *QM = pl[4], *QL = pl[5], *QR = pl[6],
+                *QC = pl[7], *S1 = pl[8], *S2 = pl[9], *S3 = pl[10], *ACC = pl[11], *L1 = pl[12];
+  // scalar file: challenges, constants and host-derivable powers (src/plonk.h:237-247)
+  uint8_t* S = P->hS;
+  memset(S, 0, NSLOT);
+  const uint32_t al = chal[0] % HFP, be = chal[1] % HFP, ga = chal[2] % HFP, z = chal[3] % HFP, v = chal[4] % HFP;
+  S[S_ZERO] = 0; S[S_ONE] = 1; S[S_NEG1] = 16;
+  S[S_ALPHA] = al; S[S_BETA] = be; S[S_GAMMA] = ga; S[S_Z] = z; S[S_V] = v;
+  S[S_OMEGA] = 4; S[S_K1] = 2; S[S_K2] = 3;   // OMEGA_VALUE, K1_VALUE, K2_VALUE (src/plonk.h:12-14)
+  S[S_BK1] = be * 2 % HFP; S[S_BK2] = be * 3 % HFP;
+  S[S_ALPHA2] = h_pow(al, 2);
+  S[S_ZN2] = h_pow(z, n + 2); S[S_Z2N4] = h_pow(z, 2 * n + 4);
+  S[S_V2] = h_pow(v, 2); S[S_V3] = h_pow(v, 3); S[S_V4] = h_pow(v, 4); S[S_V5] = h_pow(v, 5); S[S_V6] = h_pow(v, 6);
+  S[S_NEGZ] = (uint8_t)((HFP - z) % HFP);
+  S[S_ZOMEGA] = (uint8_t)(z * 4 % HFP);
+  // blinding polynomials {b2, b1}, {b4, b3}, {b6, b5}, {b9, b8, b7} (src/plonk.h:280-320)
+  S[P_BLA] = rnd[1] % HFP; S[P_BLA + 1] = rnd[0] % HFP;
+  S[P_BLB] = rnd[3] % HFP; S[P_BLB + 1] = rnd[2] % HFP;
+  S[P_BLC] = rnd[5] % HFP; S[P_BLC + 1] = rnd[4] % HFP;
+  S[P_BLZ] = rnd[8] % HFP; S[P_BLZ + 1] = rnd[7] % HFP; S[P_BLZ + 2] = rnd[6] % HFP;
+  PLK_HIP(hipMemcpyAsync(P->d_S, S, NSLOT, hipMemcpyHostToDevice, P->st));
+  // status: stage-A words (gate/copy/acc) are owned by the circuit path; reset the rest
+  PLK_HIP(hipMemsetAsync(P->d_stat, 0, 4 * ST_GATE, P->st));
+  PLK_HIP(hipMemsetAsync(P->arena, 0, 9 * P->cstride, P->st));
+  uint8_t* const cA = P->arena;
+  uint8_t* const cB = cA + P->cstride;
+  uint8_t* const cC = cB + P->cstride;
+  uint8_t* const cZ = cC + P->cstride;
+  uint8_t* const cTlo = cZ + P->cstride;
+  uint8_t* const cTmid = cTlo + P->cstride;
+  uint8_t* const cThi = cTmid + P->cstride;
+  uint8_t* const cWz = cThi + P->cstride;
+  uint8_t* const cWzw = cWz + P->cstride;
+  const uint8_t* dS = P->d_S;
+  int rc;
+#define RC(x) do { if ((rc = (x))) return rc; } while (0)
+  // ---- round 1: a_x = (b2 + b1 x) Z_H + f_a, ...  (3 poly_mul)
+  RC(pmul(P, dS + P_BLA, 2, P->d_zh, L.lz, P->blA));
+  RC(pmul(P, dS + P_BLB, 2, P->d_zh, L.lz, P->blB));
+  RC(pmul(P, dS + P_BLC, 2, P->d_zh, L.lz, P->blC));
+  RC(lincomb(P, {{P->blA, L.lz + 1}, {FA, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cA, L.la));
+  RC(lincomb(P, {{P->blB, L.lz + 1}, {FB, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cB, L.la));
+  RC(lincomb(P, {{P->blC, L.lz + 1}, {FC, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cC, L.la));
+  // ---- round 2: z_x = (b9 + b8 x + b7 x^2) Z_H + acc_x  (1 poly_mul)
+  RC(pmul(P, dS + P_BLZ, 3, P->d_zh, L.lz, P->zB));
+  RC(lincomb(P, {{P->zB, L.lz + 2}, {ACC, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cZ, L.lzx));
+  // ---- round 3: t(x) numerator (12 poly_mul), src/plonk.h:386-503
+  RC(pmul(P, cA, L.la, cB, L.la, P->AB));
+  RC(pmul(P, P->AB, L.lab, QM, n, P->ABQM));
+  RC(pmul(P, cA, L.la, QL, n, P->AQL));
+  RC(pmul(P, cB, L.la, QR, n, P->BQR));
+  RC(pmul(P, cC, L.la, QO, n, P->CQO));
+  RC(lincomb(P, {{cA, L.la}}, {S_ONE}, S_GAMMA, S_BETA, S_ALPHA, -1, P->A2, L.la));   // alpha (a + gamma + beta x)
+  RC(lincomb(P, {{cB, L.la}}, {S_ONE}, S_GAMMA, S_BK1, S_ONE, -1, P->B2, L.la));      // b + gamma + beta k1 x
+  RC(lincomb(P, {{cC, L.la}}, {S_ONE}, S_GAMMA, S_BK2, S_ONE, -1, P->C2, L.la));      // c + gamma + beta k2 x
+  RC(pmul(P, P->A2, L.la, P->B2, L.la, P->T2a));
+  RC(pmul(P, P->T2a, L.l2a, P->C2, L.la, P->T2b));
+  RC(pmul(P, P->T2b, L.l2b, cZ, L.lzx, P->T2));
+  RC(lincomb(P, {{cA, L.la}, {S1, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ALPHA, -1, P->A3, L.la));
+  RC(lincomb(P, {{cB, L.la}, {S2, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ONE, -1, P->B3, L.la));
+  RC(lincomb(P, {{cC, L.la}, {S3, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ONE, -1, P->C3, L.la));
+  RC(lincomb(P, {{cZ, L.lzx}}, {S_ONE}, -1, -1, S_ONE, S_OMEGA, P->ZW, L.lzw));       // z(omega x)
+  RC(pmul(P, P->A3, L.la, P->B3, L.la, P->T3a));
+  RC(pmul(P, P->T3a, L.l2a, P->C3, L.la, P->T3b));
+  RC(pmul(P, P->T3b, L.l2b, P->ZW, L.lzw, P->T3));
+  RC(lincomb(P, {{cZ, L.lzx}}, {S_ONE}, S_NEG1, -1, S_ALPHA2, -1, P->Z1, L.lz1));     // alpha^2 (z - 1)
+  RC(pmul(P, P->Z1, L.lz1, L1, n, P->T4));
+  RC(lincomb(P,
+             {{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {P->BQR, L.lq1}, {P->CQO, L.lq1}, {QC, n}, {P->T2, L.l2},
+              {P->T3, L.l3}, {P->T4, L.lt4}},
+             {S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_NEG1, S_ONE}, -1, -1, S_ONE, -1, P->NUM, L.lnum));
+  RC(divide_zh(P, P->NUM, L.lnum, P->TX, L.ltx, P->d_stat + ST_REM_T));
+  // t_lo / t_mid / t_hi = poly_slice(t_x, ...) with part n + 2 (src/plonk.h:513-519)
+  const uint64_t part = n + 2;
+  const uint64_t lmid = L.ltx > part ? std::min<uint64_t>(part, L.ltx - part) : 0;
+  const uint64_t lhi = L.ltx > 2 * part ? L.ltx - 2 * part : 0;
+  PLK_HIP(hipMemcpyAsync(cTlo, P->TX, std::min<uint64_t>(part, L.ltx), hipMemcpyDeviceToDevice, P->st));
+  if (lmid) PLK_HIP(hipMemcpyAsync(cTmid, P->TX + part, lmid, hipMemcpyDeviceToDevice, P->st));
+  if (lhi) PLK_HIP(hipMemcpyAsync(cThi, P->TX + 2 * part, lhi, hipMemcpyDeviceToDevice, P->st));
+  // ---- round 4: evaluations at z (src/plonk.h:527-533) and r(x)
+  RC(evals(P, {{cA, L.la, S_Z, S_AZ}, {cB, L.la, S_Z, S_BZ}, {cC, L.la, S_Z, S_CZ}, {S1, n, S_Z, S_S1Z},
+               {S2, n, S_Z, S_S2Z}, {P->TX, L.ltx, S_Z, S_TZ}, {P->ZW, L.lzw, S_Z, S_ZWZ}, {L1, n, S_Z, S_L1Z}}));
+  hipLaunchKernelGGL(scalars_r4_kernel, dim3(1), dim3(1), 0, P->st, P->d_S);
+  PLK_HIP(hipGetLastError());
+  RC(lincomb(P, {{S3, n}}, {S_BZW}, -1, -1, S_ONE, -1, P->S3S, n));   // s_sigma_3 * beta z_omega_z
+  RC(pmul(P, cZ, L.lzx, P->S3S, n, P->P3));                          // the 17th poly_mul
+  RC(lincomb(P, {{QM, n}, {QL, n}, {QR, n}, {QO, n}, {cZ, L.lzx}, {P->P3, L.lr3}},
+             {S_AB, S_AZ, S_BZ, S_CZ, S_R24, S_R3}, -1, -1, S_ONE, -1, P->RX, L.lrx));
+  RC(evals(P, {{P->RX, L.lrx, S_Z, S_RZ}}));
+  // ---- round 5: opening polynomials (src/plonk.h:580-621)
+  hipLaunchKernelGGL(scalars_r5_kernel, dim3(1), dim3(1), 0, P->st, P->d_S);
+  PLK_HIP(hipGetLastError());
+  RC(lincomb(P,
+             {{cTlo, std::min<uint64_t>(part, L.ltx)}, {cTmid, lmid}, {cThi, lhi}, {P->RX, L.lrx}, {cA, L.la},
+              {cB, L.la}, {cC, L.la}, {S1, n}, {S2, n}},
+             {S_ONE, S_ZN2, S_Z2N4, S_V, S_V2, S_V3, S_V4, S_V5, S_V6}, S_W0, -1, S_ONE, -1, P->W, L.lw));
+  RC(divide_linear(P, P->W, L.lw, S_Z, cWz, P->d_stat + ST_REM_W1));
+  RC(lincomb(P, {{cZ, L.lzx}}, {S_ONE}, S_NEGZWZ, -1, S_ONE, -1, P->ZZ, L.lzz));
+  RC(divide_linear(P, P->ZZ, L.lzz, S_ZOMEGA, cWzw, P->d_stat + ST_REM_W2));
+  // ---- trimmed lengths for the reference's exits
+  {
+    TrimArgs t{};
+    const uint8_t* cps[9] = {cA, cB, cC, cZ, cTlo, cTmid, cThi, cWz, cWzw};
+    for (int i = 0; i < 9; i++) { t.p[i] = cps[i]; t.len[i] = P->cmax; t.dst[i] = ST_LEN0 + i; }
+    t.p[9] = P->TX; t.len[9] = L.ltx; t.dst[9] = ST_TXLEN;
+    hipLaunchKernelGGL(trim_many_kernel, dim3(10), dim3(256), 0, P->st, t, P->d_stat);
+    PLK_HIP(hipGetLastError());
+  }
+  // ---- the 9 commitments: one batched MSM over the arena (srs_eval_at_s, src/srs.h:53-68)
+  const uint64_t nm = std::min<uint64_t>(P->cmax, P->srs_len);
+  PLK_HIP(hipMemsetAsync(P->d_res, 0, 9 * sizeof(PlkMsmResult), P->st));
+  if (!P->srs_irregular) {
+    RC(plk_msm_batch_launch(P->d_srs, 0, P->arena, P->cstride, nm, 9, P->d_res, P->st));
+  } else {
+    for (int i = 0; i < 9; i++) RC(plk_msm_serial_launch(P->d_srs, P->arena + i * P->cstride, nm, P->d_res + i, P->st));
+  }
+  RC(plk_msm_finalize_launch((const uint32_t*)((const uint8_t*)P->d_res + offsetof(PlkMsmResult, log)), 9,
+                             (int)(sizeof(PlkMsmResult) / 4), P->d_g4, P->st));
+  hipLaunchKernelGGL(proof_pack_kernel, dim3(1), dim3(64), 0, P->st, P->d_g4, P->d_S, P->d_proof);
+  PLK_HIP(hipGetLastError());
+#undef RC
+  return PLK_OK;
+}
+
+// the reference's exits, in the order plonk_prove would hit them
+int check_status(const plk_prover* P, const uint32_t* st, int strict, int circuit) {
+  const uint64_t part = P->n + 2;
+  if (circuit && st[ST_GATE]) { plk_set_error("Constraint %u not satisfied.", st[ST_GATE] - 1); return PLK_ERR_ARG; }
+  if (circuit && st[ST_COPY]) { plk_set_error("Invalid copy_of type"); return PLK_ERR_ARG; }
+  for (int i = 0; i < 3; i++)
+    if (st[ST_LEN0 + i] > P->srs_len) { plk_set_error("SRS length is less than polynomial length"); return PLK_ERR_RANGE; }
+  if (circuit && strict && st[ST_ACC] != 1) { plk_set_error("assertion acc_x(omega^n) == 1 failed"); return PLK_ERR_ARG; }
+  if (st[ST_LEN0 + 3] > P->srs_len) { plk_set_error("SRS length is less than polynomial length"); return PLK_ERR_RANGE; }
+  if (strict && st[ST_REM_T]) { plk_set_error("Non-zero remainder in t(x) division"); return PLK_ERR_ARG; }
+  if (st[ST_TXLEN] <= 2 * part) { plk_set_error("Invalid slice indices in poly_slice"); return PLK_ERR_RANGE; }
+  for (int i = 4; i < 7; i++)
+    if (st[ST_LEN0 + i] > P->srs_len) { plk_set_error("SRS length is less than polynomial length"); return PLK_ERR_RANGE; }
+  if (strict && st[ST_REM_W1]) { plk_set_error("assertion poly_is_zero(&rem1) failed"); return PLK_ERR_ARG; }
+  if (strict && st[ST_REM_W2]) { plk_set_error("assertion poly_is_zero(&rem2) failed"); return PLK_ERR_ARG; }
+  for (int i = 7; i < 9; i++)
+    if (st[ST_LEN0 + i] > P->srs_len) { plk_set_error("SRS length is less than polynomial length"); return PLK_ERR_RANGE; }
+  return PLK_OK;
+}
+
+int finish(plk_prover* P, int strict, int circuit, uint8_t proof[34]) {
+  uint8_t hp[64];
+  uint32_t hs[NSTAT];
+  PLK_HIP(hipMemcpyAsync(hp, P->d_proof, 64, hipMemcpyDeviceToHost, P->st));
+  PLK_HIP(hipMemcpyAsync(hs, P->d_stat, sizeof hs, hipMemcpyDeviceToHost, P->st));
+  PLK_HIP(hipStreamSynchronize(P->st));
+  const int rc = check_status(P, hs, strict, circuit);
+  if (rc) return rc;
+  if (proof) memcpy(proof, hp, 34);
+  return PLK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int plk_prover_rounds_dev(plk_prover_t* P, const uint8_t* const d_polys[13], const uint8_t chal[5],
+                          const uint8_t rand9[9], int flags, uint8_t proof[34]) {
+  if (!P || !d_polys || !chal || !rand9) { plk_set_error("plk_prover_rounds_dev: NULL argument"); return PLK_ERR_ARG; }
+  for (int i = 0; i < 13; i++)
+    if (!d_polys[i]) { plk_set_error("plk_prover_rounds_dev: polynomial %d is NULL", i); return PLK_ERR_ARG; }
+  int rc = rounds(P, d_polys, chal, rand9);
+  if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
+  return finish(P, (flags & PLK_PROVE_STRICT) != 0, 0, proof);
+}
+
+int plk_prover_prove(plk_prover_t* P, const plk_circuit_t* c, const uint8_t chal[5], const uint8_t rand9[9],
+                     uint8_t proof[34]) {
+  if (!P || !c || !chal || !rand9) { plk_set_error("plk_prover_prove: NULL argument"); return PLK_ERR_ARG; }
+  if (!P->have_circuit_tables) {
+    plk_set_error("plk_prover_prove: prover created without h / k1_h / k2_h / h_pows_inv");
+    return PLK_ERR_ARG;
+  }
+  const uint64_t n = P->n;
+  const uint8_t* parts[11] = {c->q_m, c->q_l, c->q_r, c->q_o, c->q_c, c->copy_a, c->copy_b, c->copy_c, c->a, c->b, c->c};
+  for (int i = 0; i < 11; i++)
+    if (!parts[i]) { plk_set_error("plk_prover_prove: circuit array %d is NULL", i); return PLK_ERR_ARG; }
+  // upload: q_m q_l q_r q_o q_c | copy_a copy_b copy_c (2n each) | a b c
+  std::vector<uint8_t> h(14 * n);
+  memcpy(&h[0], c->q_m, n); memcpy(&h[n], c->q_l, n); memcpy(&h[2 * n], c->q_r, n); memcpy(&h[3 * n], c->q_o, n);
+  memcpy(&h[4 * n], c->q_c, n);
+  memcpy(&h[5 * n], c->copy_a, 2 * n); memcpy(&h[7 * n], c->copy_b, 2 * n); memcpy(&h[9 * n], c->copy_c, 2 * n);
+  memcpy(&h[11 * n], c->a, n); memcpy(&h[12 * n], c->b, n); memcpy(&h[13 * n], c->c, n);
+  for (size_t i = 0; i < 14 * n; i++)
+    if (!(i >= 5 * n && i < 11 * n)) h[i] %= HFP;   // HF values (hf_new reduces), copies stay raw
+  PLK_HIP(hipMemcpyAsync(P->d_cir, h.data(), h.size(), hipMemcpyHostToDevice, P->st));
+  // challenges are needed by the grand product before rounds() uploads the scalar file
+  uint8_t* S0 = P->hS0;
+  memset(S0, 0, NSLOT);
+  S0[S_ONE] = 1; S0[S_NEG1] = 16;
+  S0[S_ALPHA] = chal[0] % HFP; S0[S_BETA] = chal[1] % HFP; S0[S_GAMMA] = chal[2] % HFP;
+  S0[S_Z] = chal[3] % HFP; S0[S_V] = chal[4] % HFP;
+  S0[S_OMEGA] = 4; S0[S_K1] = 2; S0[S_K2] = 3;
+  PLK_HIP(hipMemcpyAsync(P->d_S, S0, NSLOT, hipMemcpyHostToDevice, P->st));
+  PLK_HIP(hipMemsetAsync(P->d_stat + ST_GATE, 0, 4 * (NSTAT - ST_GATE), P->st));
+  // stage A: checks + sigma, 11 interpolations, grand product, acc_x and L1(x)
+  for (int i = 0; i < 13; i++) PLK_HIP(hipMemsetAsync(P->d_polys[i], 0, n, P->st));
+  hipLaunchKernelGGL(circuit_check_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, P->st, P->d_cir, n,
+                     P->d_h3, P->d_vals, P->d_stat);
+  PLK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(interpolate_kernel, dim3((unsigned)((11 * n + 255) / 256)), dim3(256), 0, P->st, P->d_hinv, n,
+                     P->d_vals, 11, P->d_outs);
+  PLK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(grand_product_kernel, dim3(1), dim3(64), 0, P->st, P->d_vals, n,
+                     (const uint8_t* const*)P->d_outs, P->d_S, P->ACCV);
+  PLK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(unit_vector_kernel, dim3(1), dim3(256), 0, P->st, P->E0, n);
+  PLK_HIP(hipGetLastError());
+  // acc_x and L1(x) = interpolate_at_h(e_0) (src/plonk.h:362, 381-387)
+  hipLaunchKernelGGL(interpolate_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, P->st, P->d_hinv, n,
+                     P->ACCV, 1, P->d_outs + 11);
+  PLK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(interpolate_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, P->st, P->d_hinv, n,
+                     P->E0, 1, P->d_outs + 12);
+  PLK_HIP(hipGetLastError());
+  // acc_x(omega^n) must be 1 (src/plonk.h:366-368): evaluate into the status word
+  {
+    P->h_om = h_pow(4, n);
+    PLK_HIP(hipMemcpyAsync(P->d_S + S_ACCW + 1, &P->h_om, 1, hipMemcpyHostToDevice, P->st));   // x slot
+    EvArgs a{};
+    a.p[0] = P->d_polys[11];
+    a.len[0] = n;
+    a.xslot[0] = S_ACCW + 1;
+    a.out[0] = S_ACCW;
+    a.ne = 1;
+    hipLaunchKernelGGL(eval_partial_kernel, dim3(EV_BLOCKS, 1), dim3(256), 0, P->st, a, P->d_S, P->d_part);
+    hipLaunchKernelGGL(eval_final_kernel, dim3(1), dim3(64), 0, P->st, a, P->d_part, P->d_S);
+    PLK_HIP(hipGetLastError());
+    PLK_HIP(hipMemcpyAsync(P->d_stat + ST_ACC, P->d_S + S_ACCW, 1, hipMemcpyDeviceToDevice, P->st));
+  }
+  const uint8_t* pl[13];
+  for (int i = 0; i < 13; i++) pl[i] = P->d_polys[i];
+  int rc = rounds(P, pl, chal, rand9);
+  if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
+  return finish(P, 1, 1, proof);
+}
+
+}  // extern "C"

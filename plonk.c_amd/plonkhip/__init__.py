@@ -48,7 +48,26 @@ SIGNATURES = {
     "plk_poly_mul_workspace": (_sz, [_sz, _sz]),
     "plk_poly_mul_dev": (C.c_int, [_vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp]),
     "plk_ntt_dev": (C.c_int, [_vp, C.c_int, C.c_int, _vp]),
+    "plk_prover_create": (C.c_int, [_vp, C.POINTER(_vp)]),
+    "plk_prover_destroy": (None, [_vp]),
+    "plk_prover_device_bytes": (_sz, [_vp]),
+    "plk_prover_prove": (C.c_int, [_vp, _vp, _u8p, _u8p, _u8p]),
+    "plk_prover_rounds_dev": (C.c_int, [_vp, C.POINTER(_vp), _u8p, _u8p, C.c_int, _u8p]),
 }
+
+PLK_PROVE_STRICT = 1
+
+
+class PlonkDesc(C.Structure):
+    """plk_plonk_desc_t"""
+    _fields_ = [("n", _sz), ("h", _u8p), ("k1_h", _u8p), ("k2_h", _u8p), ("h_pows_inv", _u8p),
+                ("z_h", _u8p), ("z_h_len", _sz), ("srs_g1", _u8p), ("srs_len", _sz)]
+
+
+class Circuit(C.Structure):
+    """plk_circuit_t"""
+    _fields_ = [(k, _u8p) for k in ("q_m", "q_l", "q_r", "q_o", "q_c", "copy_a", "copy_b",
+                                    "copy_c", "a", "b", "c")]
 
 
 class PlonkHipError(RuntimeError):
@@ -217,3 +236,50 @@ def parse_result(res_bytes):
     return {"log": int.from_bytes(b[72:76], "little"),
             "irregular": int.from_bytes(b[76:80], "little"),
             "g1": b[80:83]}
+
+
+# ---------------------------------------------------------------- device prover
+class Prover:
+    """plk_prover_t: plonk_new's setup on the device (SRS + Z_H [+ circuit tables]),
+    plonk_prove as `prove` (circuit) or `rounds_dev` (device-resident interpolated polys)."""
+
+    def __init__(self, n, z_h, srs_g1, h=None, k1_h=None, k2_h=None, h_pows_inv=None):
+        self._keep = [_u8(x) if x is not None else None for x in (h, k1_h, k2_h, h_pows_inv, z_h, srs_g1)]
+        hh, k1, k2, hi, zh, srs = self._keep
+        d = PlonkDesc(n, *(None if x is None else _p(x) for x in (hh, k1, k2, hi)), _p(zh), zh.size,
+                      _p(srs), srs.size // 3)
+        self._h = _vp()
+        _check("plk_prover_create", lib().plk_prover_create(C.byref(d), C.byref(self._h)))
+        self.n = n
+
+    def close(self):
+        if self._h:
+            lib().plk_prover_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def device_bytes(self):
+        return int(lib().plk_prover_device_bytes(self._h))
+
+    def prove(self, q_m, q_l, q_r, q_o, q_c, copy_a, copy_b, copy_c, a, b, c, chal, rand):
+        """copy_*: n (type, index) pairs, flattened or not."""
+        arrs = [_u8(x).reshape(-1) for x in (q_m, q_l, q_r, q_o, q_c, copy_a, copy_b, copy_c, a, b, c)]
+        cir = Circuit(*(_p(x) for x in arrs))
+        ch, rd = _u8(chal), _u8(rand)
+        out = np.zeros(34, np.uint8)
+        _check("plk_prover_prove", lib().plk_prover_prove(self._h, C.byref(cir), _p(ch), _p(rd), _p(out)))
+        return bytes(out)
+
+    def rounds_dev(self, polys, chal, rand, strict=False):
+        """polys: 13 device tensors / pointers (n bytes each)."""
+        arr = (_vp * 13)(*[_ptr(p) for p in polys])
+        ch, rd = _u8(chal), _u8(rand)
+        out = np.zeros(34, np.uint8)
+        _check("plk_prover_rounds_dev", lib().plk_prover_rounds_dev(
+            self._h, arr, _p(ch), _p(rd), PLK_PROVE_STRICT if strict else 0, _p(out)))
+        return bytes(out)

@@ -1,0 +1,120 @@
+"""Device prover (plk_prover_*, plonk.c_amd/csrc/prove.hip) against the reference prover.
+
+* n = 4: every proof the compiled reference produced (tests/golden/prove.json, 26 instances,
+  two SRS kinds) is reproduced byte for byte by plk_prover_prove, and every instance the
+  reference rejects (failed assert, exit) is rejected.
+* larger n: rounds 1-5 from synthetic interpolated polynomials (prove-shaped, non-strict:
+  GF(17) has no subgroup of that order, so no satisfiable circuit exists) against the CPU
+  restatement oracle/prove_ref.py, which is itself pinned to the same fixtures
+  (tests/test_prove_cpu.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+import gen
+from conftest import load_golden
+from prove_ref import Prover as RefProver, ProveError
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(g, case):
+    key = "short" if case["srs_n"] == 4 else str(case["srs_mode"])
+    return {k: bytes.fromhex(v) for k, v in g["setups"][key].items()}
+
+
+def _circuit(case):
+    gt, cp, w = case["gates"], case["copies"], case["wires"]
+    return dict(q_m=gt[0:4], q_l=gt[4:8], q_r=gt[8:12], q_o=gt[12:16], q_c=gt[16:20],
+                copy_a=cp[0:8], copy_b=cp[8:16], copy_c=cp[16:24], a=w[0:4], b=w[4:8], c=w[8:12])
+
+
+def test_prove_fixture_proofs(hip):
+    g = load_golden("prove.json")
+    provers = {}
+    for case in g["proofs"]:
+        key = (case["srs_n"], case["srs_mode"])
+        if key not in provers:
+            s = _setup(g, case)
+            provers[key] = hip.Prover(4, s["z_h"], s["g1s"], s["h"], s["k1_h"], s["k2_h"], s["h_pows_inv"])
+        got = provers[key].prove(**_circuit(case), chal=case["chal"], rand=case["rand"])
+        assert got.hex() == case["proof"], (case["chal"], case["rand"], case["srs_mode"])
+
+
+def test_prove_rejects_what_the_reference_rejects(hip):
+    g = load_golden("prove.json")
+    for case in g["failures"]:
+        s = _setup(g, case)
+        pr = hip.Prover(4, s["z_h"], s["g1s"], s["h"], s["k1_h"], s["k2_h"], s["h_pows_inv"])
+        if case["proof"] is None:
+            with pytest.raises(hip.PlonkHipError):
+                pr.prove(**_circuit(case), chal=case["chal"], rand=case["rand"])
+        else:
+            assert pr.prove(**_circuit(case), chal=case["chal"], rand=case["rand"]).hex() == case["proof"]
+
+
+def _synthetic(n, seed, srs_len):
+    """13 random 'interpolated' polynomials of length n, Z_H = x^n - 1, random SRS."""
+    r = gen.splitmix64(seed, 13 * n + 64)
+    polys = [(r[i * n:(i + 1) * n] % np.uint64(17)).astype(np.uint8) for i in range(13)]
+    chal = [int(x % np.uint64(17)) for x in r[13 * n:13 * n + 5]]
+    rnd = [int(x % np.uint64(17)) for x in r[13 * n + 5:13 * n + 14]]
+    chal[3] = max(chal[3], 2)            # z: avoid the degenerate z in {0, 1}
+    zh = np.zeros(n + 1, np.uint8)
+    zh[0], zh[n] = 16, 1
+    pts, _ = gen.msm_inputs(seed ^ 0x5A5A, srs_len, "full")
+    return polys, chal, rnd, zh, pts
+
+
+@pytest.mark.parametrize("n,seed", [(8, 1), (37, 2), (256, 3), (1000, 4), (3000, 5)])
+def test_rounds_shape_vs_oracle(hip, oracle, n, seed):
+    srs_len = 2 * n + 8
+    polys, chal, rnd, zh, pts = _synthetic(n, seed, srs_len)
+    ref = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes())
+    want = ref.rounds(polys, chal, rnd, strict=False)
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    got = pr.rounds_dev(dev, chal, rnd, strict=False)
+    assert got.hex() == want.hex()
+    # strict mode: synthetic numerators are not divisible by Z_H -- the reference exits
+    with pytest.raises(hip.PlonkHipError):
+        pr.rounds_dev(dev, chal, rnd, strict=True)
+    with pytest.raises(ProveError):
+        ref.rounds(polys, chal, rnd, strict=True)
+
+
+def test_rounds_general_divisor(hip, oracle):
+    """Z_H that is not x^m + c (H not a subgroup, e.g. n = 3): general long division path."""
+    n = 3
+    srs_len = 16
+    polys, chal, rnd, _, pts = _synthetic(n, 11, srs_len)
+    zh = np.frombuffer(oracle.poly_mul(oracle.poly_mul([16, 1], [13, 1]), [1, 1]), np.uint8)  # (x-1)(x-4)(x-16)
+    ref = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes())
+    want = ref.rounds(polys, chal, rnd, strict=False)
+    pr = hip.Prover(n, zh, pts)
+    got = pr.rounds_dev([torch.from_numpy(p).to("cuda") for p in polys], chal, rnd)
+    assert got.hex() == want.hex()
+
+
+def test_rounds_srs_too_short(hip, oracle):
+    n = 64
+    polys, chal, rnd, zh, pts = _synthetic(n, 21, n + 3)   # w_z(x) needs ~2n points
+    ref = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes())
+    with pytest.raises(ProveError):
+        ref.rounds(polys, chal, rnd, strict=False)
+    pr = hip.Prover(n, zh, pts)
+    with pytest.raises(hip.PlonkHipError) as e:
+        pr.rounds_dev([torch.from_numpy(p).to("cuda") for p in polys], chal, rnd)
+    assert e.value.code == hip.PLK_ERR_RANGE
+
+
+def test_rounds_deterministic_large(hip):
+    """n = 2^16 prove-shaped run twice: identical bytes (no races in the pipeline)."""
+    n = 1 << 16
+    polys, chal, rnd, zh, pts = _synthetic(n, 31, 2 * n + 8)
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    a = pr.rounds_dev(dev, chal, rnd)
+    b = pr.rounds_dev(dev, chal, rnd)
+    assert a == b and len(a) == 34
