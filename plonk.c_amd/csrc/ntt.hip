@@ -359,6 +359,27 @@ __global__ __launch_bounds__(256) void polymul_direct_kernel(const uint8_t* lg, 
   (void)nz;   // trimmed length: trim_kernel
 }
 
+// Tail of a split product (see plk_poly_mul_launch): out[i] += sum_j t[j] g[i - base - j] for
+// i in [base, rl), where out[i] for i >= ntt_len is not yet written (taken as 0).
+__global__ __launch_bounds__(256) void polymul_tail_kernel(const uint8_t* __restrict__ g, uint64_t lg,
+                                                           const uint8_t* __restrict__ t, int lt, uint64_t base,
+                                                           uint64_t ntt_len, uint8_t* __restrict__ out8,
+                                                           uint64_t rl) {
+  __shared__ uint32_t T[64];
+  if ((int)threadIdx.x < lt) T[threadIdx.x] = t[threadIdx.x] % 17u;
+  __syncthreads();
+  for (uint64_t i = base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rl;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t acc = i < ntt_len ? out8[i] : 0u;
+    const uint64_t o0 = i - base;
+    for (int j = 0; j < lt; j++) {
+      const int64_t o = (int64_t)o0 - j;
+      if (o >= 0 && (uint64_t)o < lg) acc += T[j] * (g[o] % 17u);
+    }
+    out8[i] = (uint8_t)(acc % 17u);
+  }
+}
+
 // ------------------------------------------------------------------------------ host side
 namespace {
 
@@ -449,10 +470,27 @@ static int log2_ceil(uint64_t v) {
   return k;
 }
 
+// NTT size of a product.  A result just above a power of two (la + lb - 1 = 2^K + e, e small,
+// as every prover shape n+2, 2n+3, 4n+6 at n = 2^m is) is split: the longer operand's last e
+// coefficients t are taken out, the rest times the other operand fills exactly 2^K, and
+// x^(la-e) t(x) b(x) is added by polymul_tail_kernel -- half the transform size for O(e n) MACs.
+constexpr uint64_t PLK_SPLIT_MAX = 16;
+static int product_plan(uint64_t la, uint64_t lb, uint64_t* e_out) {
+  const uint64_t rl = la + lb - 1;
+  int k = log2_ceil(rl);
+  uint64_t e = 0;
+  const uint64_t lg = la > lb ? la : lb;
+  if (k - 1 > PLK_SMALL_LOG) {
+    const uint64_t ex = rl - (1ull << (k - 1));
+    if (ex <= PLK_SPLIT_MAX && ex < lg) { e = ex; k -= 1; }
+  }
+  if (e_out) *e_out = e;
+  return k;
+}
+
 size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb) {
   if (la == 0 || lb == 0) return 0;
-  const uint64_t rl = la + lb - 1;
-  const int k = log2_ceil(rl);
+  const int k = product_plan(la, lb, nullptr);
   if ((la < lb ? la : lb) <= PLK_DIRECT_MAX || k <= PLK_SMALL_LOG) return 0;
   return (size_t)2 * 4 * (1ull << k);
 }
@@ -483,10 +521,11 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
     PLK_HIP(hipGetLastError());
     return PLK_OK;
   }
-  const int k = log2_ceil(rl);
+  uint64_t e = 0;
+  const int k = product_plan(la, lb, &e);
   if (k > bb::TWO_ADICITY) return PLK_ERR_RANGE;
   const uint32_t ninv = bb::hpow(1ull << k, bb::P - 2);   // normal form on purpose
-  if (k <= PLK_SMALL_LOG) {
+  if (k <= PLK_SMALL_LOG) {   // (never split: product_plan only splits above 2^(SMALL_LOG+1))
     const size_t lds = (size_t)4 * (2 * col_stride(1 << k) + 2 * (1 << k));
     hipLaunchKernelGGL(polymul_small_kernel, dim3(1), dim3(1024), lds, st, d_a, la, d_b, lb, k, tw_fwd(), tw_inv(),
                        d_out, ninv, d_nz);
@@ -496,6 +535,24 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
   if (!d_work) return PLK_ERR_ARG;
   uint32_t* A = (uint32_t*)d_work;
   uint32_t* B = A + (1ull << k);
+  if (e) {
+    // a := the longer operand; a0 = a[0, la - e) times b fills 2^k, tail a[la - e, la) direct
+    const bool swap = lb > la;
+    const uint8_t* lgp = swap ? d_b : d_a;
+    const uint8_t* shp = swap ? d_a : d_b;
+    const uint64_t llg = swap ? lb : la, lsh = swap ? la : lb;
+    const uint64_t sa = llg - e;
+    int rc = plk_wave_poly_mul_launch(lgp, sa, shp, lsh, k, d_out, A, B, ninv, st);
+    if (rc) return rc;
+    const uint64_t span = rl - sa;
+    const uint64_t blocks64 = (span + 255) / 256;
+    hipLaunchKernelGGL(polymul_tail_kernel, dim3((unsigned)(blocks64 > 8192 ? 8192 : blocks64)), dim3(256), 0, st,
+                       shp, lsh, lgp + sa, (int)e, sa, sa + lsh - 1, d_out, rl);
+    PLK_HIP(hipGetLastError());
+    if (d_nz) hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d_out, rl, d_nz);
+    PLK_HIP(hipGetLastError());
+    return PLK_OK;
+  }
   int rc = plk_wave_poly_mul_launch(d_a, la, d_b, lb, k, d_out, A, B, ninv, st);
   if (rc) return rc;
   if (d_nz) hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d_out, rl, d_nz);

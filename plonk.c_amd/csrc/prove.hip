@@ -114,15 +114,73 @@ __global__ __launch_bounds__(256) void lincomb_kernel(LcArgs a, const uint8_t* _
   }
 }
 
+// 16 coefficients per thread and iteration (uint4 loads / stores); every pointer 16-byte
+// aligned (checked on the host, else lincomb_kernel).
+__device__ __forceinline__ void load16(const uint8_t* p, uint64_t len, uint64_t i, uint32_t (&w)[4]) {
+  if (i + 16 <= len) {
+    const uint4 q = *reinterpret_cast<const uint4*>(p + i);
+    w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
+    return;
+  }
+  w[0] = w[1] = w[2] = w[3] = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++)
+    if (i + k < len) w[k >> 2] |= (uint32_t)p[i + k] << (8 * (k & 3));
+}
+
+__global__ __launch_bounds__(256) void lincomb16_kernel(LcArgs a, const uint8_t* __restrict__ S) {
+  uint32_t cf[LC_MAX];
+#pragma unroll
+  for (int t = 0; t < LC_MAX; t++) cf[t] = t < a.nt ? S[a.slot[t]] : 0u;
+  const uint32_t sc = S[a.scale];
+  const uint32_t c0 = a.c0 >= 0 ? S[a.c0] : 0u, c1 = a.c1 >= 0 ? S[a.c1] : 0u;
+  const uint32_t x = a.twist >= 0 ? S[a.twist] : 1u;
+  uint32_t tw[16];   // x^k; x^i = 1 for i = 0 mod 16 when x != 0
+  tw[0] = 1;
+#pragma unroll
+  for (int k = 1; k < 16; k++) tw[k] = tw[k - 1] * x % HFP;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; i < a.out_len; i += stride) {
+    uint32_t acc[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) acc[k] = 0;
+    if (i == 0) { acc[0] = c0; acc[1] = c1; }
+#pragma unroll
+    for (int t = 0; t < LC_MAX; t++) {
+      if (t < a.nt && i < a.len[t]) {
+        uint32_t w[4];
+        load16(a.p[t], a.len[t], i, w);
+#pragma unroll
+        for (int k = 0; k < 16; k++) acc[k] += cf[t] * ((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+      }
+    }
+    uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      uint32_t v = acc[k] % HFP * sc % HFP;
+      if (a.twist >= 0) v = v * (x == 0 ? (i + k == 0 ? 1u : 0u) : tw[k]) % HFP;
+      o[k >> 2] |= v << (8 * (k & 3));
+    }
+    if (i + 16 <= a.out_len) {
+      *reinterpret_cast<uint4*>(a.out + i) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if (i + k < a.out_len) a.out[i + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
+    }
+  }
+}
+
 // ------------------------------------------------------------------ poly_eval (batched)
 // Horner of src/poly.h:265-272 == sum c_i x^i mod 17; x^i = x^(i mod 16) for x != 0.
 constexpr int EV_MAX = 12;
-constexpr int EV_BLOCKS = 64;
+constexpr int EV_BLOCKS = 256;
 struct EvArgs {
   const uint8_t* p[EV_MAX];
   uint64_t len[EV_MAX];
   int xslot[EV_MAX];
   int out[EV_MAX];
+  int vec[EV_MAX];   // pointer 16-byte aligned: uint4 loads
   int ne;
 };
 
@@ -137,13 +195,28 @@ __global__ __launch_bounds__(256) void eval_partial_kernel(EvArgs a, const uint8
   const uint8_t* p = a.p[e];
   const uint64_t n = a.len[e];
   uint32_t acc = 0;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint32_t w = i == 0 ? 1u : (x == 0 ? 0u : pw[i & 15]);
-    acc += w * p[i];
-    if ((i & 0xFFFF) == 0) acc %= HFP;   // never overflows: < 2^16 terms of <= 256 between folds
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x == 0) {                       // poly_eval(p, 0) = p[0]
+    if (gid == 0 && n) acc = p[0];
+  } else if (a.vec[e]) {              // 16 coefficients per step: i = 0 mod 16 so x^(i+k) = x^k
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
+    for (uint64_t i = gid * 16; i < n; i += stride) {
+      uint32_t w[4];
+      load16(p, n, i, w);
+      uint32_t s = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) s += pw[k] * ((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+      acc = (acc + s) % HFP;
+    }
+  } else {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
+    for (uint64_t i = gid * 16; i < n; i += stride) {
+      uint32_t s = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) s += i + k < n ? pw[k] * p[i + k] : 0u;
+      acc = (acc + s) % HFP;
+    }
   }
-  acc %= HFP;
   __shared__ uint32_t red[256];
   red[threadIdx.x] = acc;
   __syncthreads();
@@ -170,12 +243,12 @@ __global__ __launch_bounds__(256) void divide_binomial_kernel(const uint8_t* __r
                                                               uint64_t m, uint32_t lead, uint32_t c,
                                                               uint8_t* __restrict__ q, uint64_t ql,
                                                               uint32_t* __restrict__ rem_flag) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= m) return;
+  const uint64_t r0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t r = r0 < m ? r0 : m;   // lanes past m idle but stay for the wave vote
   const uint32_t li = hinv(lead);
   const uint32_t nc = hneg(c);
   uint32_t prev = 0;   // q[j + m]
-  if (nl > m && r < ql) {
+  if (r < m && nl > m && r < ql) {
     uint64_t j = r + ((ql - 1 - r) / m) * m;   // top of the chain
     for (;;) {
       const uint32_t v = (num[j + m] + nc * prev) % HFP * li % HFP;
@@ -185,10 +258,11 @@ __global__ __launch_bounds__(256) void divide_binomial_kernel(const uint8_t* __r
       j -= m;
     }
   }
-  if (r < nl) {
-    const uint32_t rv = (num[r] + nc * prev) % HFP;   // prev = q[r] (0 if none)
-    if (rv) atomicOr(rem_flag, 1u);
-  }
+  const uint32_t rv = (r < m && r < nl) ? (num[r] + nc * prev) % HFP : 0u;   // prev = q[r] (0 if none)
+  // one flag word for the whole grid: vote per block, and skip the atomic once it is set
+  // (same-address atomics from every wave serialise in one L2 channel)
+  if (__syncthreads_or(rv != 0) && threadIdx.x == 0 && __hip_atomic_load(rem_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+    atomicOr(rem_flag, 1u);
 }
 
 // (b) divisor d1 x + d0: the long division gives q[j] = b num[j+1] + a q[j+1] with
@@ -590,8 +664,17 @@ int lincomb(plk_prover* P, std::initializer_list<std::pair<const uint8_t*, uint6
   a.twist = twist;
   a.out = out;
   a.out_len = out_len;
-  const uint64_t blocks = std::min<uint64_t>((out_len + 255) / 256, 2048);
-  hipLaunchKernelGGL(lincomb_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, a, P->d_S);
+  bool vec = ((uintptr_t)out % 16) == 0;
+  for (int i = 0; i < t; i++) vec = vec && ((uintptr_t)a.p[i] % 16) == 0;
+  if (vec) {
+    const uint64_t blocks = std::min<uint64_t>((out_len + 4095) / 4096, 2048);
+    hipLaunchKernelGGL(lincomb16_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, a,
+                       P->d_S);
+  } else {
+    const uint64_t blocks = std::min<uint64_t>((out_len + 255) / 256, 2048);
+    hipLaunchKernelGGL(lincomb_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, a,
+                       P->d_S);
+  }
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }
@@ -604,6 +687,7 @@ int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64
     a.len[e] = std::get<1>(t);
     a.xslot[e] = std::get<2>(t);
     a.out[e] = std::get<3>(t);
+    a.vec[e] = ((uintptr_t)a.p[e] % 16) == 0;
     e++;
   }
   a.ne = e;
@@ -887,7 +971,8 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   {
     TrimArgs t{};
     const uint8_t* cps[9] = {cA, cB, cC, cZ, cTlo, cTmid, cThi, cWz, cWzw};
-    for (int i = 0; i < 9; i++) { t.p[i] = cps[i]; t.len[i] = P->cmax; t.dst[i] = ST_LEN0 + i; }
+    const uint64_t ub[9] = {L.la, L.la, L.la, L.lzx, std::min<uint64_t>(part, L.ltx), lmid, lhi, L.lwq, L.lwo};
+    for (int i = 0; i < 9; i++) { t.p[i] = cps[i]; t.len[i] = std::max<uint64_t>(ub[i], 1); t.dst[i] = ST_LEN0 + i; }
     t.p[9] = P->TX; t.len[9] = L.ltx; t.dst[9] = ST_TXLEN;
     hipLaunchKernelGGL(trim_many_kernel, dim3(10), dim3(256), 0, P->st, t, P->d_stat);
     PLK_HIP(hipGetLastError());

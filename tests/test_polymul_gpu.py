@@ -38,7 +38,10 @@ def test_survey_digests(hip, oracle):
 SHAPES = [(1, 1), (33, 33), (32, 1000), (33, 1000), (2048, 2049), (2049, 2048), (4097, 4),
           (4097, 33), (3000, 5000), (1 << 12, 1 << 12), ((1 << 13) + 1, 999),
           (1 << 15, (1 << 15) + 1), (100000, 3), (70000, 90000), ((1 << 19), (1 << 19)),
-          ((1 << 20) + 3, (1 << 20) + 5), (3 * (1 << 20) + 4, (1 << 20) + 3)]
+          ((1 << 20) + 3, (1 << 20) + 5), (3 * (1 << 20) + 4, (1 << 20) + 3),
+          # split products: la + lb - 1 = 2^K + e, e <= 16 (tail of the longer operand direct)
+          (4097, 4100), (8193, 8196), (8196, 8193), (8200, 8201), (8200, 8202), (16386, 100),
+          ((1 << 16) + 2, (1 << 16)), (3 * (1 << 14) + 4, (1 << 14) + 3)]
 
 
 @pytest.mark.parametrize("la,lb", SHAPES)

@@ -1,0 +1,19 @@
+#!/usr/bin/env python3
+"""Prove-shaped pipeline timing at n = 2^k gates (tuning aid; run under rocprofv3 for the
+per-kernel split).  Usage: python tools/prove_bench.py [k ...]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "plonk.c_amd"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import plonkhip as hip  # noqa: E402
+from bench import prove_component  # noqa: E402
+
+hip.init(0)
+dev = torch.device("cuda", 0)
+ks = [int(x) for x in sys.argv[1:]] or [16, 18, 20]
+print(json.dumps({"prove_2^%d" % k: prove_component(torch, hip, dev, k) for k in ks}))
