@@ -33,7 +33,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--log2n", type=int, default=22)
-    ap.add_argument("--msm-batch", type=int, default=8,
+    ap.add_argument("--msm-batch", type=int, default=40,
                     help="MSMs per kernel launch (plk_msm_g1_batch_dev); every MSM is one step")
     ap.add_argument("--rotate-mib", type=int, default=640)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -315,6 +315,14 @@ def main():
             "device_us_per_msm": round(avg1 * 1e3, 2), "median_us": round(med1 * 1e3, 2),
             "GB_s": round(MSM_BYTES_PER_POINT * n / (avg1 * 1e-3) / 1e9, 1),
             "note": "unbatched: one launch per MSM, back-to-back on one stream"}
+        B8 = 8
+        r8 = torch.zeros((B8, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
+        avg8, med8 = event_avg_ms(torch, st, lambda i: hip.msm_g1_batch_dev(
+            pts[(i * B8) % sets], 3 * n, sc[(i * B8) % sets], n, n, B8, r8[0], st), 16)
+        comp["msm_2^%d_8_per_launch" % args.log2n] = {
+            "device_us_per_launch": round(avg8 * 1e3, 2),
+            "GB_s": round(MSM_BYTES_PER_POINT * n * B8 / (avg8 * 1e-3) / 1e9, 1),
+            "note": "8 MSMs per launch (the prover's commitments are 9 per launch)"}
         line["components"] = comp
     if rank == 0:
         print(json.dumps(line), flush=True)

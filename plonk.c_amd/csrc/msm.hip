@@ -29,6 +29,12 @@
 
 #include <stdlib.h>
 
+// Diagnostic builds only (tools/msm_lab.hip): bit 0 replaces the LDS table by arithmetic,
+// bit 1 replaces the ticketed atomics by a plain store.  Always 0 in libplonkhip.
+#ifndef PLK_MSM_DIAG
+#define PLK_MSM_DIAG 0
+#endif
+
 __constant__ uint32_t c_ytab[512];             // E[idx], see above
 __constant__ uint8_t c_exp[PLK_GROUP_ORDER * 4];  // EXP[k] = {x, y, inf, 0}
 __constant__ uint8_t c_inv101[PLK_GF_P];       // a^-1 mod 101 (0 -> 0), for the raw fold
@@ -56,7 +62,11 @@ __device__ __forceinline__ uint32_t encode(uint32_t x, uint32_t y, uint32_t f) {
 __device__ __forceinline__ uint32_t point_term(uint32_t k, uint32_t c, const uint32_t* tab, uint32_t lane4,
                                                bool& bad) {
   const uint32_t idx = (k >> 16) & 0x1FFu;
+#if PLK_MSM_DIAG & 1
+  const uint32_t e = idx * 0x9E37u + lane4;
+#else
   const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + ((idx << 7) | lane4));
+#endif
   const uint32_t d = e - k;
   bad |= d >= 256u;
   return (d & 0xFFu) * c;
@@ -126,20 +136,22 @@ __device__ __forceinline__ uint32_t group_sum(const Group& g, const uint32_t* ta
 
 // One launch = a batch of gridDim.y MSMs of n points each (points/scalars of MSM b at
 // pts + b * pstride, sc + b * sstride; result record res[b]); gridDim.x blocks per MSM,
-// each striding over its MSM's 16-point groups with the next group's loads in flight.
+// each striding over its MSM's 16-point groups, G groups in flight per thread.
 //
 // Finish without a second launch: every block reduces its points to a partial log (< 102)
 // and adds   partial | 1 << 32 | (irregular ? 1 << 48 : 0)   with ONE 64-bit device-scope
-// atomic to the shard word res[b].shard[s], s = (linear block id) mod 8 -- blocks are dealt
-// round-robin over the 8 XCDs, so a shard is (for speed only) one XCD's blocks and no
-// word sees more than ~32 arrivals (one hot word for 256 arrivals costs ~3 us).  The block
+// atomic to the shard word res[b].shard[s][0], s = (linear block id) mod 8 -- blocks are
+// dealt round-robin over the 8 XCDs, so a shard is (for speed only) one XCD's blocks.  The
+// shard words sit on separate 128-byte lines: device-scope atomics to one line serialise at
+// ~10 ns each (256 arrivals on one word: +2.8 us per launch; 8 words on one line: no
+// better; 8 lines: -1.7 us, tools/msm_lab.hip).  The block
 // whose ticket comes back as (shard size - 1) owns the shard's complete sum (old + own add,
 // no fence or re-read needed), re-arms the shard word and adds the shard total to
 // res[b].top the same way; the last shard's finisher writes log / irregular / g1 and
 // re-arms top.  Every word is zero again when the launch ends.
-template <bool ALIGNED, int NT, bool SHARDED>
-__global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* __restrict__ pts_base, uint64_t pstride,
-                                                      const uint8_t* __restrict__ sc_base, uint64_t sstride,
+template <bool ALIGNED, int NT, int G>
+__global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, uint64_t pstride,
+                                                      const uint8_t* sc_base, uint64_t sstride,
                                                       uint64_t n, PlkMsmResult* res_base) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[TAB_ENTRIES * COPIES];
   __shared__ uint32_t wsum[NT / PLK_WAVE];
@@ -161,25 +173,52 @@ __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* __restrict_
     // 16 points per thread-step: 48 B of points (3 x dwordx4) + 16 B of scalars (1 x dwordx4)
     const uint4* p4 = reinterpret_cast<const uint4*>(pts);
     const uint4* s4 = reinterpret_cast<const uint4*>(sc);
+    const uint64_t last = ngroups - 1;
+    // Each iteration issues the loads of G groups (g, g + stride, ..., g + (G-1) stride;
+    // indices clamped to the last group -- a cache hit -- and masked in the sums) and then
+    // consumes them in issue order within the same iteration: no loaded register is carried
+    // around the loop (a loop-carried prefetch makes the register allocator copy the
+    // arrived group at the latch, i.e. wait for it, serialising loads and compute), the
+    // compiler's vmcnt bookkeeping is exact (vmcnt(4 (G-1-j)) before group j) and a thread
+    // has up to 64 G bytes in flight.  Block-uniform trip count; the first iteration is
+    // peeled so the table fill sits between its loads and its compute.
+    const uint64_t span = stride * G;
+    const uint32_t iters = (uint32_t)((ngroups - (uint64_t)blockIdx.x * NT + span - 1) / span);
     uint64_t g = tid;
-    // ... then the first group, unconditionally: a clamped index (threads past the end
-    // re-read group 0 and drop its sum) so the loads cannot be sunk below the fill, and
-    // the compiler's vmcnt bookkeeping sees 4 table words older than 4 group loads ...
-    asm volatile("" ::: "memory");
-    Group cur = load_group(p4, s4, g < ngroups ? g : 0);
-    asm volatile("" ::: "memory");
-    fill.store(tab);                                  // ... LDS fill waits for the table words only
-    __syncthreads();
-    for (;;) {
-      const uint64_t nx = g + stride;
-      const bool more = nx < ngroups;
-      Group nxt;
-      if (more) nxt = load_group(p4, s4, nx);
-      const uint32_t part = group_sum(cur, tab, lane4, bad) % PLK_GROUP_ORDER;
-      acc += g < ngroups ? part : 0u;
-      if (!more) break;
-      cur = nxt;
-      g = nx;
+    {
+      Group cur[G];
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < G; j++) {
+        const uint64_t gj = g + j * stride;
+        cur[j] = load_group(p4, s4, gj < last ? gj : last);
+        asm volatile("" ::: "memory");               // keep group j's loads older than j+1's
+      }
+      if (!(PLK_MSM_DIAG & 1)) {
+        fill.store(tab);                              // ... LDS fill waits for the table words only
+        __syncthreads();
+      }
+#pragma unroll
+      for (int j = 0; j < G; j++) {
+        const uint32_t part = group_sum(cur[j], tab, lane4, bad) % PLK_GROUP_ORDER;
+        acc += g + j * stride < ngroups ? part : 0u;
+      }
+    }
+    for (uint32_t it = 1; it < iters; it++) {
+      g += span;
+      Group cur[G];
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < G; j++) {
+        const uint64_t gj = g + j * stride;
+        cur[j] = load_group(p4, s4, gj < last ? gj : last);
+        asm volatile("" ::: "memory");
+      }
+#pragma unroll
+      for (int j = 0; j < G; j++) {
+        const uint32_t part = group_sum(cur[j], tab, lane4, bad) % PLK_GROUP_ORDER;
+        acc += g + j * stride < ngroups ? part : 0u;
+      }
     }
     // tail (n mod 16 points), one point per thread of the first block
     const uint64_t base = ngroups << 4;
@@ -212,24 +251,28 @@ __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* __restrict_
     bs += wsum[k];
     bb_ |= wbad[k];
   }
+  if (PLK_MSM_DIAG & 2) {
+    res->pad[blockIdx.x % 11] = bs + bb_;
+    return;
+  }
   const uint32_t X = gridDim.x;
   unsigned long long add =
       (unsigned long long)(bs % PLK_GROUP_ORDER) | (1ull << 32) | ((unsigned long long)(bb_ != 0) << 48);
-  uint32_t arrivals = X;                       // expected arrivals on res->top
-  if (SHARDED) {
+  {
     const uint32_t lin = blockIdx.y * X + blockIdx.x;
     const uint32_t sh = lin % PLK_MSM_SHARDS;
     // blocks of this MSM in shard sh: x in [0, X) with (y X + x) = sh (mod 8)
     const uint32_t r = (sh + PLK_MSM_SHARDS - (blockIdx.y * X) % PLK_MSM_SHARDS) % PLK_MSM_SHARDS;
     const uint32_t in_shard = r < X ? (X - r + PLK_MSM_SHARDS - 1) / PLK_MSM_SHARDS : 0u;
-    const unsigned long long old = atomicAdd(&res->shard[sh], add);
+    unsigned long long* word = reinterpret_cast<unsigned long long*>(&res->shard[sh][0]);
+    const unsigned long long old = atomicAdd(word, add);
     if (((old >> 32) & 0xFFFFull) != in_shard - 1) return;
     const unsigned long long tot = old + add;
-    atomicExch(&res->shard[sh], 0ull);
+    atomicExch(word, 0ull);
     add = (unsigned long long)((uint32_t)(tot & 0xFFFFFFFFull) % PLK_GROUP_ORDER) | (1ull << 32) |
           ((unsigned long long)((tot >> 48) != 0) << 48);
-    arrivals = X < PLK_MSM_SHARDS ? X : PLK_MSM_SHARDS;
   }
+  const uint32_t arrivals = X < PLK_MSM_SHARDS ? X : PLK_MSM_SHARDS;   // shards with blocks
   const unsigned long long old = atomicAdd(&res->top, add);
   if (((old >> 32) & 0xFFFFull) != arrivals - 1) return;
   const unsigned long long tot = old + add;
@@ -332,31 +375,62 @@ int plk_msm_upload_tables(const uint32_t* ytab, const uint8_t* exp4, const uint8
   return PLK_OK;
 }
 
-// Launch geometry: one 16-point group per thread per pass.  Big MSMs use 1024-thread
-// blocks (one 64 KB table per CU, 16 waves, the CU's share of loads in flight at once);
-// small ones 256-thread blocks so they still spread over many CUs.  A batch shares the
-// chip: ~256 blocks in total, so each block loops over its MSM's groups with the next
-// group's loads in flight instead of paying table fill + drain per 16 KB.
-// Overridable for tuning with PLK_MSM_THREADS / PLK_MSM_MAX_BLOCKS.
-void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks) {
-  static int env_threads = -1, env_blocks = -1;
+// Launch geometry.  Big MSMs use 512-thread blocks, two per CU (two 64 KB tables, 16
+// waves); small ones 256-thread blocks so they still spread over many CUs.  A batch shares
+// the chip: <= 512 blocks in total, so each block loops over its MSM's groups instead of
+// paying table fill + finish per 16 KB.  G (groups in flight per thread and iteration) is
+// the largest power of two <= min(2, groups per thread) (G = 4 measured slower).
+// Overridable for tuning with PLK_MSM_THREADS / PLK_MSM_MAX_BLOCKS / PLK_MSM_G.
+namespace {
+int env_int(const char* name) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : 0;
+}
+}  // namespace
+
+void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* gpt) {
+  static int env_threads = -1, env_blocks = -1, env_g = -1;
   if (env_threads < 0) {
-    const char* t = getenv("PLK_MSM_THREADS");
-    const char* b = getenv("PLK_MSM_MAX_BLOCKS");
-    env_threads = t ? atoi(t) : 0;
-    env_blocks = b ? atoi(b) : 0;
+    env_threads = env_int("PLK_MSM_THREADS");
+    env_blocks = env_int("PLK_MSM_MAX_BLOCKS");
+    env_g = env_int("PLK_MSM_G");
   }
   const uint64_t groups = n >> 4;
-  int th = groups >= 256ull * 1024 ? 1024 : 256;
+  int th = groups >= 64ull * 1024 ? 512 : 256;
   if (env_threads == 256 || env_threads == 512 || env_threads == 1024) th = env_threads;
-  uint64_t b = (groups + th - 1) / th;
-  uint64_t cap = env_blocks > 0 ? (uint64_t)env_blocks : (th == 1024 ? 256 : 1024);
+  // two 64 KB tables per CU: 512 resident blocks fill the chip once
+  uint64_t cap = env_blocks > 0 ? (uint64_t)env_blocks : 512;
   if (batch > 1) cap = cap / (uint64_t)batch > 1 ? cap / (uint64_t)batch : 1;
+  uint64_t b = (groups + th - 1) / th;
   if (b > cap) b = cap;
   if (b < 1) b = 1;
+  const uint64_t per_thread = groups / (b * (uint64_t)th);
+  int g = 1;
+  const int gmax = (env_g == 1 || env_g == 2 || env_g == 4) ? env_g : 2;
+  while (g < gmax && (uint64_t)(2 * g) <= per_thread) g *= 2;
   *threads = th;
   *blocks = (int)b;
+  if (gpt) *gpt = g;
 }
+
+namespace {
+template <bool A, int T>
+void go_g(int g, dim3 grid, hipStream_t st, const uint8_t* p, uint64_t ps, const uint8_t* s, uint64_t ss, uint64_t n,
+          PlkMsmResult* r) {
+  if (!A || g == 1)
+    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 1>), grid, dim3(T), 0, st, p, ps, s, ss, n, r);
+  else if (g == 2)
+    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 2>), grid, dim3(T), 0, st, p, ps, s, ss, n, r);
+  else
+    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 4>), grid, dim3(T), 0, st, p, ps, s, ss, n, r);
+}
+template <int T>
+void go_t(bool aligned, int g, dim3 grid, hipStream_t st, const uint8_t* p, uint64_t ps, const uint8_t* s, uint64_t ss,
+          uint64_t n, PlkMsmResult* r) {
+  if (aligned) go_g<true, T>(g, grid, st, p, ps, s, ss, n, r);
+  else go_g<false, T>(g, grid, st, p, ps, s, ss, n, r);
+}
+}  // namespace
 
 int plk_msm_batch_launch(const uint8_t* d_pts, uint64_t pstride, const uint8_t* d_sc, uint64_t sstride, uint64_t n,
                          int batch, PlkMsmResult* d_res, hipStream_t st) {
@@ -365,29 +439,14 @@ int plk_msm_batch_launch(const uint8_t* d_pts, uint64_t pstride, const uint8_t* 
     plk_set_error("plk_msm batch %d too large", batch);
     return PLK_ERR_RANGE;
   }
-  int threads, blocks;
-  plk_msm_geometry(n, batch, &threads, &blocks);
-  static int sharded = -1;
-  if (sharded < 0) {
-    const char* e = getenv("PLK_MSM_SHARDED");
-    sharded = e ? atoi(e) != 0 : 0;
-  }
+  int threads, blocks, g;
+  plk_msm_geometry(n, batch, &threads, &blocks, &g);
   const bool aligned = ((uintptr_t)d_pts % 16 == 0) && ((uintptr_t)d_sc % 16 == 0) &&
                        (batch == 1 || (pstride % 16 == 0 && sstride % 16 == 0));
   const dim3 grid(blocks, batch);
-#define PLK_MSM_GO(A, T, S) \
-  hipLaunchKernelGGL((msm_dlog_kernel<A, T, S>), grid, dim3(T), 0, st, d_pts, pstride, d_sc, sstride, n, d_res)
-  if (threads == 1024) {
-    if (aligned) { if (sharded) PLK_MSM_GO(true, 1024, true); else PLK_MSM_GO(true, 1024, false); }
-    else { if (sharded) PLK_MSM_GO(false, 1024, true); else PLK_MSM_GO(false, 1024, false); }
-  } else if (threads == 512) {
-    if (aligned) { if (sharded) PLK_MSM_GO(true, 512, true); else PLK_MSM_GO(true, 512, false); }
-    else { if (sharded) PLK_MSM_GO(false, 512, true); else PLK_MSM_GO(false, 512, false); }
-  } else {
-    if (aligned) { if (sharded) PLK_MSM_GO(true, 256, true); else PLK_MSM_GO(true, 256, false); }
-    else { if (sharded) PLK_MSM_GO(false, 256, true); else PLK_MSM_GO(false, 256, false); }
-  }
-#undef PLK_MSM_GO
+  if (threads == 1024) go_t<1024>(aligned, g, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
+  else if (threads == 512) go_t<512>(aligned, g, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
+  else go_t<256>(aligned, g, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }

@@ -6,8 +6,9 @@
 #include "../../include/plonkhip.h"
 
 typedef plk_msm_result_t PlkMsmResult;
-static_assert(sizeof(plk_msm_result_t) == 128, "MSM result record is 128 bytes");
-static_assert(offsetof(plk_msm_result_t, log) == 72 && offsetof(plk_msm_result_t, g1) == 80,
+static_assert(sizeof(plk_msm_result_t) == 1152, "MSM result record is 1152 bytes");
+static_assert(offsetof(plk_msm_result_t, log) == 8 && offsetof(plk_msm_result_t, irregular) == 12 &&
+                  offsetof(plk_msm_result_t, g1) == 16 && offsetof(plk_msm_result_t, shard) == 128,
               "offsets used by plonkhip/__init__.py");
 #define PLK_MSM_SHARDS 8      // ticket shards per MSM record (one per XCD)
 
@@ -28,7 +29,7 @@ void plk_set_error(const char* fmt, ...);
 
 // msm.hip
 int plk_msm_upload_tables(const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101);
-void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks);
+void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* groups_per_thread);
 int plk_msm_batch_launch(const uint8_t* d_pts, uint64_t pstride, const uint8_t* d_sc, uint64_t sstride, uint64_t n,
                          int batch, PlkMsmResult* d_res, hipStream_t st);
 int plk_msm_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsmResult* d_res, hipStream_t st);

@@ -22,8 +22,8 @@ LIB_PATH = os.path.join(PKG_DIR, "libplonkhip.so")
 HEADER_PATH = os.path.join(REPO_DIR, "include", "plonkhip.h")
 
 PLK_OK, PLK_ERR_HIP, PLK_ERR_ARG, PLK_ERR_RANGE, PLK_ERR_NODEV, PLK_ERR_NOMEM = range(6)
-MSM_RESULT_BYTES = 128
-MSM_LOG_OFFSET, MSM_IRREGULAR_OFFSET, MSM_G1_OFFSET = 72, 76, 80
+MSM_RESULT_BYTES = 1152
+MSM_LOG_OFFSET, MSM_IRREGULAR_OFFSET, MSM_G1_OFFSET = 8, 12, 16
 
 _u8p = C.POINTER(C.c_uint8)
 _vp = C.c_void_p
@@ -231,11 +231,11 @@ def ntt_dev(data, log_n, inverse=False, stream=None):
 
 
 def parse_result(res_bytes):
-    """Decode a 128-byte plk_msm_result_t copied to the host."""
+    """Decode a plk_msm_result_t (MSM_RESULT_BYTES) copied to the host."""
     b = bytes(res_bytes)
-    return {"log": int.from_bytes(b[72:76], "little"),
-            "irregular": int.from_bytes(b[76:80], "little"),
-            "g1": b[80:83]}
+    return {"log": int.from_bytes(b[MSM_LOG_OFFSET:MSM_LOG_OFFSET + 4], "little"),
+            "irregular": int.from_bytes(b[MSM_IRREGULAR_OFFSET:MSM_IRREGULAR_OFFSET + 4], "little"),
+            "g1": b[MSM_G1_OFFSET:MSM_G1_OFFSET + 3]}
 
 
 # ---------------------------------------------------------------- device prover

@@ -92,13 +92,17 @@ def test_dropin_headers_compile_and_link(tmp_path):
 
 
 def test_struct_layouts(tmp_path):
-    (tmp_path / "l.c").write_text('#include "prelude.h"\n#include <stdio.h>\n'
-                                  "int main(void){ printf(\"%zu %zu %zu %zu\", sizeof(G1), "
-                                  "sizeof(HF), sizeof(GF), sizeof(plk_msm_result_t)); return 0; }\n")
+    import plonkhip
+    (tmp_path / "l.c").write_text('#include "prelude.h"\n#include <stdio.h>\n#include <stddef.h>\n'
+                                  "int main(void){ printf(\"%zu %zu %zu %zu %zu %zu %zu\", sizeof(G1), "
+                                  "sizeof(HF), sizeof(GF), sizeof(plk_msm_result_t), "
+                                  "offsetof(plk_msm_result_t, log), offsetof(plk_msm_result_t, irregular), "
+                                  "offsetof(plk_msm_result_t, g1)); return 0; }\n")
     r = _gcc([str(tmp_path / "l.c"), "-o", str(tmp_path / "l")])
     assert r.returncode == 0, r.stderr
     out = subprocess.run([str(tmp_path / "l")], capture_output=True, text=True).stdout
-    assert out == "3 1 1 128"
+    assert out == "3 1 1 %d %d %d %d" % (plonkhip.MSM_RESULT_BYTES, plonkhip.MSM_LOG_OFFSET,
+                                         plonkhip.MSM_IRREGULAR_OFFSET, plonkhip.MSM_G1_OFFSET)
 
 
 @pytest.mark.skipif(not os.path.isdir(REF_SRC), reason="reference sources not present")

@@ -88,13 +88,13 @@ def main():
                               "GBs_dev": round(4 * n * B / (avg * 1e-3) / 1e9, 1)}
     # correctness spot check: every record agrees with a fresh single launch
     torch.cuda.synchronize()
-    bad = int(res[:, 76:80].view(torch.int32).sum().item())
+    bad = int(res[:, hip.MSM_IRREGULAR_OFFSET:hip.MSM_IRREGULAR_OFFSET + 4].view(torch.int32).sum().item())
     r1 = torch.zeros((1, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
     hip.msm_g1_dev(pts[0], sc[0], n, r1[0], st)
     torch.cuda.synchronize()
     out["irregular"] = bad
-    out["set0_g1"] = bytes(r1[0, 80:83].cpu().numpy()).hex()
-    out["set0_batch_g1"] = bytes(res[0, 80:83].cpu().numpy()).hex()
+    out["set0_g1"] = bytes(r1[0, hip.MSM_G1_OFFSET:hip.MSM_G1_OFFSET + 3].cpu().numpy()).hex()
+    out["set0_batch_g1"] = bytes(res[0, hip.MSM_G1_OFFSET:hip.MSM_G1_OFFSET + 3].cpu().numpy()).hex()
     print(json.dumps(out), flush=True)
 
 
