@@ -26,19 +26,29 @@ constexpr uint32_t PINV = neg_inv_p();
 static_assert(P * (0u - PINV) == 1u, "p * p^{-1} == 1 mod 2^32");
 constexpr uint32_t R2 = (uint32_t)((((unsigned __int128)1) << 64) % P);   // R^2 mod p: mmul(x, R2) = x R
 
+// a * b * R^-1 mod p for a < 2p, b < p (a * b < p 2^32, so REDC applies).  The 64-bit
+// REDC sum t + m p < 2p 2^32, so its high word is < 2p and one unsigned min(u, u - p)
+// (u - p wraps to a huge value when u < p) finishes -- 32-bit ops only after the two
+// v_mad_u64_u32.
 __host__ __device__ __forceinline__ uint32_t mmul(uint32_t a, uint32_t b) {
-  uint64_t t = (uint64_t)a * b;
-  uint32_t m = (uint32_t)t * PINV;
-  uint64_t u = (t + (uint64_t)m * P) >> 32;
-  return u >= P ? (uint32_t)(u - P) : (uint32_t)u;
+  const uint64_t t = (uint64_t)a * b;
+  const uint32_t m = (uint32_t)t * PINV;
+  const uint32_t u = (uint32_t)((t + (uint64_t)m * P) >> 32);
+  const uint32_t v = u - P;
+  return v < u ? v : u;
 }
 __host__ __device__ __forceinline__ uint32_t madd(uint32_t a, uint32_t b) {
-  uint32_t s = a + b;                        // a, b < 2^31: no wrap
-  return s >= P ? s - P : s;
+  const uint32_t s = a + b;                  // a, b < p < 2^31: no wrap
+  const uint32_t t = s - P;
+  return t < s ? t : s;
 }
 __host__ __device__ __forceinline__ uint32_t msub(uint32_t a, uint32_t b) {
-  return a >= b ? a - b : a + P - b;
+  const uint32_t d = a - b;                  // wraps when a < b ...
+  const uint32_t e = d + P;                  // ... and then d + p < p is the answer
+  return e < d ? e : d;
 }
+// a - b + p in [1, 2p): a valid first operand of mmul (DIF butterflies skip one reduction)
+__host__ __device__ __forceinline__ uint32_t msub_lazy(uint32_t a, uint32_t b) { return a + P - b; }
 
 // host-side helpers (plain modular arithmetic, used to build tables)
 inline uint32_t hpow(uint64_t b, uint64_t e) {

@@ -12,7 +12,7 @@ static_assert(offsetof(plk_msm_result_t, log) == 8 && offsetof(plk_msm_result_t,
               "offsets used by plonkhip/__init__.py");
 #define PLK_MSM_SHARDS 8      // ticket shards per MSM record (one per XCD)
 
-#define PLK_NTT_SMALL_LOG 12   // universal small twiddle table covers tiles up to 2^12 rows
+#define PLK_NTT_SMALL_LOG 13   // universal small twiddle table covers tiles up to 2^13 rows
 #define PLK_SMALL_LOG 12       // poly_mul with N <= 2^12: one workgroup does everything
 #define PLK_DIRECT_MAX 32      // poly_mul with min(la, lb) <= 32: direct convolution
 

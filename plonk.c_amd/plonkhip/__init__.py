@@ -18,7 +18,7 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "libplonkhip.so")
+LIB_PATH = os.environ.get("PLK_LIB") or os.path.join(PKG_DIR, "libplonkhip.so")   # PLK_LIB: tuning builds only
 HEADER_PATH = os.path.join(REPO_DIR, "include", "plonkhip.h")
 
 PLK_OK, PLK_ERR_HIP, PLK_ERR_ARG, PLK_ERR_RANGE, PLK_ERR_NODEV, PLK_ERR_NOMEM = range(6)
