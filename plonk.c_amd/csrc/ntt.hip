@@ -500,6 +500,37 @@ static size_t pass_lds(int M, int C, bool center) {
   return (center ? 2 : 1) * C * (size_t)col_stride((int)rows) * 4 + (center ? 2 : 1) * rows * 4 + (size_t)C * M * 4;
 }
 
+// m products of one transform size 2^k through the wave engine (workspace 2^(k+3) bytes each);
+// es[i] > 0: the split plan (product_plan) -- the longer operand's last es[i] coefficients are
+// multiplied in directly by polymul_tail_kernel after the transform.
+static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, void* d_work, hipStream_t st) {
+  const uint32_t ninv = bb::hpow(1ull << k, bb::P - 2);   // normal form on purpose
+  WJob w[64];
+  for (int i = 0; i < m; i++) {
+    const PlkPolyMulJob& j = g[i];
+    const uint64_t e = es ? es[i] : 0;
+    const bool swap = e && j.lb > j.la;                   // a := the longer operand when splitting
+    const uint8_t* lgp = swap ? j.b : j.a;
+    const uint8_t* shp = swap ? j.a : j.b;
+    const uint64_t llg = swap ? j.lb : j.la, lsh = swap ? j.la : j.lb;
+    uint32_t* A = (uint32_t*)d_work + ((size_t)2 * i << k);
+    w[i] = WJob{lgp, shp, llg - e, lsh, j.out, llg - e + lsh - 1, A, A + (1ull << k)};
+  }
+  int rc = plk_wave_poly_mul_batch_launch(w, m, k, ninv, st);
+  if (rc) return rc;
+  for (int i = 0; i < m; i++) {
+    const uint64_t e = es ? es[i] : 0;
+    if (!e) continue;
+    const uint64_t rl = g[i].la + g[i].lb - 1, sa = w[i].la, lsh = w[i].lb;
+    const uint64_t span = rl - sa;
+    const uint64_t blocks64 = (span + 255) / 256;
+    hipLaunchKernelGGL(polymul_tail_kernel, dim3((unsigned)(blocks64 > 8192 ? 8192 : blocks64)), dim3(256), 0, st,
+                       w[i].b8, lsh, w[i].a8 + sa, (int)e, sa, sa + lsh - 1, g[i].out, rl);
+    PLK_HIP(hipGetLastError());
+  }
+  return PLK_OK;
+}
+
 // d_out must hold la+lb-1 bytes; *d_nz (if not NULL) receives the trimmed length (0 means "all zero" ->
 // the caller reports length 1).
 int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
@@ -533,30 +564,61 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
     return PLK_OK;
   }
   if (!d_work) return PLK_ERR_ARG;
-  uint32_t* A = (uint32_t*)d_work;
-  uint32_t* B = A + (1ull << k);
-  if (e) {
-    // a := the longer operand; a0 = a[0, la - e) times b fills 2^k, tail a[la - e, la) direct
-    const bool swap = lb > la;
-    const uint8_t* lgp = swap ? d_b : d_a;
-    const uint8_t* shp = swap ? d_a : d_b;
-    const uint64_t llg = swap ? lb : la, lsh = swap ? la : lb;
-    const uint64_t sa = llg - e;
-    int rc = plk_wave_poly_mul_launch(lgp, sa, shp, lsh, k, d_out, A, B, ninv, st);
-    if (rc) return rc;
-    const uint64_t span = rl - sa;
-    const uint64_t blocks64 = (span + 255) / 256;
-    hipLaunchKernelGGL(polymul_tail_kernel, dim3((unsigned)(blocks64 > 8192 ? 8192 : blocks64)), dim3(256), 0, st,
-                       shp, lsh, lgp + sa, (int)e, sa, sa + lsh - 1, d_out, rl);
-    PLK_HIP(hipGetLastError());
-    if (d_nz) hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d_out, rl, d_nz);
-    PLK_HIP(hipGetLastError());
-    return PLK_OK;
-  }
-  int rc = plk_wave_poly_mul_launch(d_a, la, d_b, lb, k, d_out, A, B, ninv, st);
+  const PlkPolyMulJob job{d_a, la, d_b, lb, d_out};
+  int rc = ntt_group(&job, 1, k, e ? &e : nullptr, d_work, st);
   if (rc) return rc;
   if (d_nz) hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d_out, rl, d_nz);
   PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
+// Several independent products: direct / one-workgroup ones one by one, the NTT ones grouped
+// by transform size and run as batches through the wave engine (one launch per pass for the
+// whole group; job i of a group uses 2^(k+3) bytes of d_work at offset i 2^(k+3)).  The
+// prover's round-3 products come in such groups (7 at 2^21, then 3 + 2 at 2^22 for n = 2^20).
+int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, size_t work_bytes, hipStream_t st) {
+  int ks[64];
+  uint64_t es[64];
+  if (nj > 64) {
+    plk_set_error("poly_mul batch of %d products (max 64)", nj);
+    return PLK_ERR_RANGE;
+  }
+  for (int i = 0; i < nj; i++) {
+    const PlkPolyMulJob& j = jobs[i];
+    ks[i] = -1;
+    if (j.la == 0 || j.lb == 0) return PLK_ERR_ARG;
+    const uint64_t mn = j.la < j.lb ? j.la : j.lb;
+    const int k = product_plan(j.la, j.lb, &es[i]);
+    if (mn > PLK_DIRECT_MAX && k > PLK_SMALL_LOG) {
+      if (mn * 256 >= bb::P || k > bb::TWO_ADICITY) return PLK_ERR_RANGE;
+      ks[i] = k;
+      continue;
+    }
+    const int rc = plk_poly_mul_launch(j.a, j.la, j.b, j.lb, j.out, nullptr, nullptr, st);
+    if (rc) return rc;
+  }
+  bool done[64] = {false};
+  for (int i = 0; i < nj; i++) {
+    if (ks[i] < 0 || done[i]) continue;
+    const int k = ks[i];
+    const size_t per = (size_t)8 << k;
+    const int cap = (int)(work_bytes / per);
+    if (cap < 1) {
+      plk_set_error("poly_mul batch: workspace %zu bytes < %zu", work_bytes, per);
+      return PLK_ERR_ARG;
+    }
+    PlkPolyMulJob g[64];
+    uint64_t ge[64];
+    int m = 0;
+    for (int q = i; q < nj && m < cap; q++)
+      if (!done[q] && ks[q] == k) {
+        g[m] = jobs[q];
+        ge[m++] = es[q];
+        done[q] = true;
+      }
+    const int rc = ntt_group(g, m, k, ge, d_work, st);
+    if (rc) return rc;
+  }
   return PLK_OK;
 }
 

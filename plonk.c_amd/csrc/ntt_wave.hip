@@ -41,10 +41,20 @@ constexpr int WT_MAX_HI12 = 8;                 // widest high-bit pass with 2^12
 constexpr int WT_MAX_HI13 = 10;                // ... with 2^13 tiles
 
 __device__ __forceinline__ int wphys(int e) { return e + (e >> 5); }
+__device__ __forceinline__ uint32_t wpad(uint32_t i) { return i + (i >> 6); }   // padded W13 index
+constexpr int W13_WORDS = 4096 + 64;
 
 struct WPass {
   int k;    // log2 N
   int lo;   // lowest bit of the pass
+};
+
+// A batch of independent transforms of one size: job j owns the u32 arrays A (and B for a
+// product), optionally reads its inputs as bytes (a8/la, b8/lb) in the first forward pass
+// and writes its product as bytes (out8, out_len) in the last inverse pass.
+constexpr int WT_MAX_JOBS = 8;
+struct WJobs {
+  WJob j[WT_MAX_JOBS];
 };
 
 struct WTw {
@@ -106,7 +116,11 @@ struct Eng {
       for (int k = 0; k < E; k++) {
         if (k & (1 << q)) continue;
         const uint32_t rr = blow + ((uint32_t)(k & ((1 << q) - 1)) << LB);   // row mod 2^s
-        const uint32_t w = Tsm[(1u << s) + rr];
+        // lo = 0 passes (M = TB) index W13[i] = w_{2^13}^i (i < 4096, the top level of the
+        // small table): w_{2^(s+1)}^rr = W13[rr << (12 - s)], stored padded (one word per 64)
+        // so the 2^(12-s)-strided reads of the low stages spread over the banks; high passes
+        // read the 2^M-entry prefix T[2^s + rr]
+        const uint32_t w = M == TB ? Tsm[wpad(rr << (12 - s))] : Tsm[(1u << s) + rr];
         const uint32_t u = v[k], x = v[k | (1 << q)];
         if (!INV) {
           v[k] = bb::madd(u, x);
@@ -175,8 +189,15 @@ __device__ __forceinline__ uint32_t block_tile() {
   return (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
 }
 
-template <int M, int NT>
-__device__ __forceinline__ void load_small_tw(uint32_t* Tsm, const uint32_t* small) {
+// the pass's stage twiddles into LDS: W13 (4096 words) for a lo = 0 pass, else the first 2^M
+// entries of the small table
+template <int M, int TB, int NT>
+__device__ __forceinline__ void load_pass_tw(uint32_t* Tsm, const uint32_t* small) {
+  if (M == TB) {
+#pragma unroll
+    for (int i = 0; i < 4096 / NT; i++) Tsm[wpad(i * NT + threadIdx.x)] = small[4096 + i * NT + threadIdx.x];
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < ((1 << M) + NT - 1) / NT; i++) {
     const int j = i * NT + (int)threadIdx.x;
@@ -186,20 +207,21 @@ __device__ __forceinline__ void load_small_tw(uint32_t* Tsm, const uint32_t* sma
 
 }  // namespace
 
-// Forward (DIF) pass over 1 or 2 arrays (blockIdx.y), u32 in place, or the first pass
-// reading bytes (zero padded, reduced mod 17, to Montgomery).
-template <int TB, int R, int M, bool FROM_U8>
-__global__ __launch_bounds__(WT_NT) void wt_fwd_kernel(WPass p, uint32_t* d0, uint32_t* d1, const uint8_t* a8,
-                                                       const uint8_t* b8, uint64_t la, uint64_t lb8, WTw tw) {
+// Forward (DIF) pass over ARR (1 or 2) arrays of each job (blockIdx.y = job * ARR + array),
+// u32 in place, or the first pass reading bytes (zero padded, reduced mod 17, to Montgomery).
+template <int TB, int R, int M, bool FROM_U8, int ARR>
+__global__ __launch_bounds__(WT_NT) void wt_fwd_kernel(WPass p, WJobs jobs, WTw tw) {
   using G = Eng<TB, R, M>;
   static_assert(G::NT == WT_NT, "tile block size");
-  __shared__ uint32_t Tsm[1 << M];
+  __shared__ uint32_t Tsm[M == TB ? W13_WORDS : 1 << M];
   __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
-  uint32_t* d = blockIdx.y == 0 ? d0 : d1;
-  const uint8_t* s8 = blockIdx.y == 0 ? a8 : b8;
-  const uint64_t ls = blockIdx.y == 0 ? la : lb8;
+  const WJob& jb = jobs.j[blockIdx.y / ARR];
+  const bool second = ARR == 2 && (blockIdx.y & 1);
+  uint32_t* d = second ? jb.B : jb.A;
+  const uint8_t* s8 = second ? jb.b8 : jb.a8;
+  const uint64_t ls = second ? jb.lb : jb.la;
 
   const uint32_t b0 = G::template base_q<0>(tid, false);
   constexpr int L0 = G::lbq(0, false);
@@ -222,7 +244,7 @@ __global__ __launch_bounds__(WT_NT) void wt_fwd_kernel(WPass p, uint32_t* d0, ui
       ch[k] = tw.hi[ex >> 12];
     }
   }
-  load_small_tw<M, G::NT>(Tsm, tw.small);
+  load_pass_tw<M, TB, G::NT>(Tsm, tw.small);
   __syncthreads();
   G::template pass<false>(v, tid, bufs, 0, Tsm);
 #pragma unroll
@@ -237,14 +259,17 @@ __global__ __launch_bounds__(WT_NT) void wt_fwd_kernel(WPass p, uint32_t* d0, ui
 // Inverse (DIT) pass, u32 in place; the final pass (TO_U8) scales by N^-1 (normal form,
 // which also leaves Montgomery form), reduces mod 17 and writes bytes for idx < out_len.
 template <int TB, int R, int M, bool TO_U8>
-__global__ __launch_bounds__(WT_NT) void wt_inv_kernel(WPass p, uint32_t* d, WTw tw, uint8_t* out8, uint64_t out_len,
-                                                       uint32_t ninv) {
+__global__ __launch_bounds__(WT_NT) void wt_inv_kernel(WPass p, WJobs jobs, WTw tw, uint32_t ninv) {
   using G = Eng<TB, R, M>;
   static_assert(G::NT == WT_NT, "tile block size");
-  __shared__ uint32_t Tsm[1 << M];
+  __shared__ uint32_t Tsm[M == TB ? W13_WORDS : 1 << M];
   __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
+  const WJob& jb = jobs.j[blockIdx.y];
+  uint32_t* d = jb.A;
+  uint8_t* out8 = jb.out8;
+  const uint64_t out_len = jb.out_len;
 
   const uint32_t b0 = G::template base_q<0>(tid, true);
   constexpr int L0 = G::lbq(0, true);
@@ -260,7 +285,7 @@ __global__ __launch_bounds__(WT_NT) void wt_inv_kernel(WPass p, uint32_t* d, WTw
       ch[k] = tw.hi[ex >> 12];
     }
   }
-  load_small_tw<M, G::NT>(Tsm, tw.small);
+  load_pass_tw<M, TB, G::NT>(Tsm, tw.small);
   if (G::HIGH) {
 #pragma unroll
     for (int k = 0; k < G::E; k++) v[k] = bb::mmul(v[k], bb::mmul(cl[k], ch[k]));
@@ -280,18 +305,19 @@ __global__ __launch_bounds__(WT_NT) void wt_inv_kernel(WPass p, uint32_t* d, WTw
 // Center of poly_mul: last forward pass (lo = 0) of a and b, pointwise product, first
 // inverse pass, all in registers of one block; result written over a.  The last DIF round
 // and the first DIT round both have local bits [0, R), so no exchange sits in between.
-// 2^12 tiles keep both stage tables in LDS; 2^13 tiles read them from the (L2-resident)
-// global tables so two blocks still fit a CU.
+// Stage twiddles: W13 forward and inverse in LDS (2 x 16 KB); 2^13 tiles are held to <= 64
+// VGPRs (8 waves per SIMD) so two blocks share a CU.
 template <int TB, int R>
-__global__ __launch_bounds__(WT_NT) void wt_center_kernel(WPass p, uint32_t* d0, const uint32_t* d1, WTw twf, WTw twi) {
+__global__ __launch_bounds__(WT_NT, TB == 13 ? 8 : 1) void wt_center_kernel(WPass p, WJobs jobs, WTw twf, WTw twi) {
   using G = Eng<TB, R, TB>;
   static_assert(G::NT == WT_NT, "tile block size");
   static_assert(G::lbq(G::NR - 1, false) == 0 && G::lbq(0, true) == 0, "center mapping");
-  constexpr bool LDS_TW = TB <= 12;
-  __shared__ uint32_t Tlds[LDS_TW ? 2 << TB : 1];
+  __shared__ uint32_t Tlds[2 * W13_WORDS];
   __shared__ uint32_t bufs[(G::DBUF ? 2 : 1) * G::BUF];
-  const uint32_t* Tf = LDS_TW ? Tlds : twf.small;
-  const uint32_t* Ti = LDS_TW ? Tlds + (1 << TB) : twi.small;
+  const uint32_t* Tf = Tlds;
+  const uint32_t* Ti = Tlds + W13_WORDS;
+  uint32_t* d0 = jobs.j[blockIdx.y].A;
+  const uint32_t* d1 = jobs.j[blockIdx.y].B;
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
   const uint32_t b0 = G::template base_q<0>(tid, false);
@@ -303,11 +329,9 @@ __global__ __launch_bounds__(WT_NT) void wt_center_kernel(WPass p, uint32_t* d0,
     va[k] = d0[idx];
     vb[k] = d1[idx];
   }
-  if (LDS_TW) {
-    load_small_tw<TB, G::NT>(Tlds, twf.small);
-    load_small_tw<TB, G::NT>(Tlds + (1 << TB), twi.small);
-    __syncthreads();
-  }
+  load_pass_tw<TB, TB, G::NT>(Tlds, twf.small);
+  load_pass_tw<TB, TB, G::NT>(Tlds + W13_WORDS, twi.small);
+  __syncthreads();
   G::template pass<false>(va, tid, bufs, 0, Tf);
   G::template pass<false>(vb, tid, bufs, G::XCH, Tf);
 #pragma unroll
@@ -347,26 +371,23 @@ WTw to_wtw(const PlkTwTables& t, bool inv) {
   return inv ? WTw{t.small_i, t.lo_i, t.hi_i} : WTw{t.small_f, t.lo_f, t.hi_f};
 }
 
-template <int TB, int M, bool U8>
-void launch_fwd(WPass p, uint32_t* d0, uint32_t* d1, const uint8_t* a8, const uint8_t* b8, uint64_t la, uint64_t lb,
-                WTw tw, int arrays, hipStream_t st) {
+template <int TB, int M, bool U8, int ARR>
+void launch_fwd(WPass p, const WJobs& jobs, int nj, WTw tw, hipStream_t st) {
   constexpr int R = TB - 10;                    // 1024 threads per tile
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB);
-  hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8>), dim3(tiles, arrays), dim3(WT_NT), 0, st, p, d0, d1, a8, b8, la,
-                     lb, tw);
+  hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, ARR>), dim3(tiles, ARR * nj), dim3(WT_NT), 0, st, p, jobs, tw);
 }
 template <int TB, int M, bool U8>
-void launch_inv(WPass p, uint32_t* d, WTw tw, uint8_t* out8, uint64_t out_len, uint32_t ninv, hipStream_t st) {
+void launch_inv(WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipStream_t st) {
   constexpr int R = TB - 10;
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB);
-  hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8>), dim3(tiles), dim3(WT_NT), 0, st, p, d, tw, out8, out_len, ninv);
+  hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8>), dim3(tiles, nj), dim3(WT_NT), 0, st, p, jobs, tw, ninv);
 }
 
 // pass widths: 1..8 for both tile sizes, 9..10 for 2^13 tiles, M = TB for the lo = 0 pass
-template <int TB, bool U8>
-int fwd_m(int M, WPass p, uint32_t* d0, uint32_t* d1, const uint8_t* a8, const uint8_t* b8, uint64_t la, uint64_t lb,
-          WTw tw, int arrays, hipStream_t st) {
-#define PLK_FWD(m) launch_fwd<TB, m, U8>(p, d0, d1, a8, b8, la, lb, tw, arrays, st)
+template <int TB, bool U8, int ARR>
+int fwd_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, hipStream_t st) {
+#define PLK_FWD(m) launch_fwd<TB, m, U8, ARR>(p, jobs, nj, tw, st)
   switch (M) {
     case 1: PLK_FWD(1); break;
     case 2: PLK_FWD(2); break;
@@ -382,7 +403,7 @@ int fwd_m(int M, WPass p, uint32_t* d0, uint32_t* d1, const uint8_t* a8, const u
         if (M == 10) { PLK_FWD(10); break; }
       }
       if constexpr (!U8) {
-        if (M == TB) { launch_fwd<TB, TB, false>(p, d0, d1, a8, b8, la, lb, tw, arrays, st); break; }
+        if (M == TB) { launch_fwd<TB, TB, false, ARR>(p, jobs, nj, tw, st); break; }
       }
       plk_set_error("wave plan: unsupported pass width %d (tile bits %d)", M, TB);
       return PLK_ERR_ARG;
@@ -393,8 +414,8 @@ int fwd_m(int M, WPass p, uint32_t* d0, uint32_t* d1, const uint8_t* a8, const u
 }
 
 template <int TB, bool U8>
-int inv_m(int M, WPass p, uint32_t* d, WTw tw, uint8_t* out8, uint64_t out_len, uint32_t ninv, hipStream_t st) {
-#define PLK_INV(m) launch_inv<TB, m, U8>(p, d, tw, out8, out_len, ninv, st)
+int inv_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipStream_t st) {
+#define PLK_INV(m) launch_inv<TB, m, U8>(p, jobs, nj, tw, ninv, st)
   switch (M) {
     case 1: PLK_INV(1); break;
     case 2: PLK_INV(2); break;
@@ -410,7 +431,7 @@ int inv_m(int M, WPass p, uint32_t* d, WTw tw, uint8_t* out8, uint64_t out_len, 
         if (M == 10) { PLK_INV(10); break; }
       }
       if constexpr (!U8) {
-        if (M == TB) { launch_inv<TB, TB, false>(p, d, tw, out8, out_len, ninv, st); break; }
+        if (M == TB) { launch_inv<TB, TB, false>(p, jobs, nj, tw, ninv, st); break; }
       }
       plk_set_error("wave plan: unsupported pass width %d (tile bits %d)", M, TB);
       return PLK_ERR_ARG;
@@ -421,8 +442,7 @@ int inv_m(int M, WPass p, uint32_t* d, WTw tw, uint8_t* out8, uint64_t out_len, 
 }
 
 template <int TB>
-int wave_poly_mul_t(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, int k, uint8_t* d_out,
-                    uint32_t* A, uint32_t* B, uint32_t ninv, hipStream_t st) {
+int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t st) {
   const PlkTwTables t = plk_ntt_tables();
   const WTw twf = to_wtw(t, false), twi = to_wtw(t, true);
   int Ms[4];
@@ -432,18 +452,16 @@ int wave_poly_mul_t(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_
   int rc;
   for (int i = 0; i < np - 1; i++) {
     const WPass p{k, lo[i]};
-    rc = i == 0 ? fwd_m<TB, true>(Ms[i], p, A, B, d_a, d_b, la, lb, twf, 2, st)
-                : fwd_m<TB, false>(Ms[i], p, A, B, nullptr, nullptr, 0, 0, twf, 2, st);
+    rc = i == 0 ? fwd_m<TB, true, 2>(Ms[i], p, jobs, nj, twf, st) : fwd_m<TB, false, 2>(Ms[i], p, jobs, nj, twf, st);
     if (rc) return rc;
   }
   const uint32_t tiles = (uint32_t)((1ull << k) >> TB);
-  hipLaunchKernelGGL((wt_center_kernel<TB, TB - 10>), dim3(tiles), dim3(WT_NT), 0, st, WPass{k, 0}, A, B, twf, twi);
+  hipLaunchKernelGGL((wt_center_kernel<TB, TB - 10>), dim3(tiles, nj), dim3(WT_NT), 0, st, WPass{k, 0}, jobs, twf,
+                     twi);
   PLK_HIP(hipGetLastError());
-  const uint64_t rl = la + lb - 1;
   for (int i = np - 2; i >= 0; i--) {
     const WPass p{k, lo[i]};
-    rc = i == 0 ? inv_m<TB, true>(Ms[i], p, A, twi, d_out, rl, ninv, st)
-                : inv_m<TB, false>(Ms[i], p, A, twi, nullptr, 0, 0u, st);
+    rc = i == 0 ? inv_m<TB, true>(Ms[i], p, jobs, nj, twi, ninv, st) : inv_m<TB, false>(Ms[i], p, jobs, nj, twi, 0u, st);
     if (rc) return rc;
   }
   return PLK_OK;
@@ -452,6 +470,8 @@ int wave_poly_mul_t(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_
 template <int TB>
 int wave_ntt_t(uint32_t* d, int k, int inverse, hipStream_t st) {
   const PlkTwTables t = plk_ntt_tables();
+  WJobs jobs{};
+  jobs.j[0].A = d;
   int Ms[4];
   const int np = wave_plan(k, TB, Ms);
   int lo[4];
@@ -459,8 +479,8 @@ int wave_ntt_t(uint32_t* d, int k, int inverse, hipStream_t st) {
   for (int s = 0; s < np; s++) {
     const int i = inverse ? np - 1 - s : s;
     const WPass p{k, lo[i]};
-    const int rc = inverse ? inv_m<TB, false>(Ms[i], p, d, to_wtw(t, true), nullptr, 0, 0u, st)
-                           : fwd_m<TB, false>(Ms[i], p, d, d, nullptr, nullptr, 0, 0, to_wtw(t, false), 1, st);
+    const int rc = inverse ? inv_m<TB, false>(Ms[i], p, jobs, 1, to_wtw(t, true), 0u, st)
+                           : fwd_m<TB, false, 1>(Ms[i], p, jobs, 1, to_wtw(t, false), st);
     if (rc) return rc;
   }
   return PLK_OK;
@@ -470,10 +490,15 @@ int wave_ntt_t(uint32_t* d, int k, int inverse, hipStream_t st) {
 
 bool plk_wave_ntt_supported(int k) { return k > 12 && k <= bb::TWO_ADICITY; }
 
-int plk_wave_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, int k,
-                             uint8_t* d_out, uint32_t* A, uint32_t* B, uint32_t ninv, hipStream_t st) {
-  return tile_bits(k) == 13 ? wave_poly_mul_t<13>(d_a, la, d_b, lb, k, d_out, A, B, ninv, st)
-                            : wave_poly_mul_t<12>(d_a, la, d_b, lb, k, d_out, A, B, ninv, st);
+int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, uint32_t ninv, hipStream_t st) {
+  for (int j0 = 0; j0 < nj; j0 += WT_MAX_JOBS) {
+    const int m = nj - j0 < WT_MAX_JOBS ? nj - j0 : WT_MAX_JOBS;
+    WJobs w{};
+    for (int i = 0; i < m; i++) w.j[i] = jobs[j0 + i];
+    const int rc = tile_bits(k) == 13 ? wave_poly_mul_t<13>(w, m, k, ninv, st) : wave_poly_mul_t<12>(w, m, k, ninv, st);
+    if (rc) return rc;
+  }
+  return PLK_OK;
 }
 
 int plk_wave_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st) {

@@ -51,9 +51,26 @@ size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb);
 int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
                         uint32_t* d_nz, void* d_work, hipStream_t st);
 int plk_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st);
+struct PlkPolyMulJob {
+  const uint8_t* a;
+  uint64_t la;
+  const uint8_t* b;
+  uint64_t lb;
+  uint8_t* out;   // la + lb - 1 bytes
+};
+int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, size_t work_bytes, hipStream_t st);
 
-// ntt_wave.hip (transforms of 2^13 .. 2^27 points)
+// ntt_wave.hip (transforms of 2^13 .. 2^27 points).  One product job: u32 work arrays A, B
+// (2^k each), byte inputs a8[0, la), b8[0, lb), byte output out8[0, out_len).
+struct WJob {
+  const uint8_t* a8;
+  const uint8_t* b8;
+  uint64_t la, lb;
+  uint8_t* out8;
+  uint64_t out_len;
+  uint32_t* A;
+  uint32_t* B;
+};
 bool plk_wave_ntt_supported(int k);
-int plk_wave_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, int k,
-                             uint8_t* d_out, uint32_t* A, uint32_t* B, uint32_t ninv, hipStream_t st);
+int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, uint32_t ninv, hipStream_t st);
 int plk_wave_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st);

@@ -771,12 +771,18 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   // commitments: a b c z t_lo t_mid t_hi w_z w_zw
   P->cmax = std::max(std::max(L.la, L.lzx), std::max(std::max(n + 2, L.ltx), std::max(L.lwq, L.lwo)));
   P->cstride = (P->cmax + 15) & ~(size_t)15;
-  // poly_mul workspace: the largest product shape
+  // poly_mul workspace: the largest batch of round 3 (rounds()), or a single product
   size_t ws = 0;
-  const uint64_t shapes[][2] = {{2, L.lz},       {3, L.lz},       {L.la, L.la},   {L.lab, n},    {L.la, n},
-                                {L.la, L.la},    {L.l2a, L.la},   {L.l2b, L.lzx}, {L.l2b, L.lzw}, {L.lz1, n},
-                                {L.lzx, n}};
+  const uint64_t shapes[][2] = {{2, L.lz}, {3, L.lz}, {L.lzx, n}};
   for (const auto& s : shapes) ws = std::max(ws, plk_poly_mul_workspace_bytes(s[0], s[1]));
+  const uint64_t g1[][2] = {{L.la, L.la}, {L.la, n}, {L.la, n}, {L.la, n}, {L.la, L.la}, {L.la, L.la}, {L.lz1, n}};
+  const uint64_t g2[][2] = {{L.lab, n}, {L.l2a, L.la}, {L.l2a, L.la}};
+  const uint64_t g3[][2] = {{L.l2b, L.lzx}, {L.l2b, L.lzw}};
+  size_t w1 = 0, w2 = 0, w3 = 0;
+  for (const auto& s : g1) w1 += plk_poly_mul_workspace_bytes(s[0], s[1]);
+  for (const auto& s : g2) w2 += plk_poly_mul_workspace_bytes(s[0], s[1]);
+  for (const auto& s : g3) w3 += plk_poly_mul_workspace_bytes(s[0], s[1]);
+  ws = std::max(ws, std::max(w1, std::max(w2, w3)));
   Bump B;
   const size_t o_srs = B.take(3 * P->srs_len + 16), o_zh = B.take(zl + 16), o_h3 = B.take(3 * n + 16),
                o_hinv = B.take(P->have_circuit_tables ? n * n + 16 : 16), o_S = B.take(NSLOT),
@@ -914,27 +920,29 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   // ---- round 2: z_x = (b9 + b8 x + b7 x^2) Z_H + acc_x  (1 poly_mul)
   RC(pmul(P, dS + P_BLZ, 3, P->d_zh, L.lz, P->zB));
   RC(lincomb(P, {{P->zB, L.lz + 2}, {ACC, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cZ, L.lzx));
-  // ---- round 3: t(x) numerator (12 poly_mul), src/plonk.h:386-503
-  RC(pmul(P, cA, L.la, cB, L.la, P->AB));
-  RC(pmul(P, P->AB, L.lab, QM, n, P->ABQM));
-  RC(pmul(P, cA, L.la, QL, n, P->AQL));
-  RC(pmul(P, cB, L.la, QR, n, P->BQR));
-  RC(pmul(P, cC, L.la, QO, n, P->CQO));
+  // ---- round 3: t(x) numerator (12 poly_mul), src/plonk.h:386-503.  The linear factors
+  // first, then the 12 products in three batches of independent ones (one launch per NTT pass
+  // for a whole batch): 7 first-level products, the 3 products of those, the last 2.
   RC(lincomb(P, {{cA, L.la}}, {S_ONE}, S_GAMMA, S_BETA, S_ALPHA, -1, P->A2, L.la));   // alpha (a + gamma + beta x)
   RC(lincomb(P, {{cB, L.la}}, {S_ONE}, S_GAMMA, S_BK1, S_ONE, -1, P->B2, L.la));      // b + gamma + beta k1 x
   RC(lincomb(P, {{cC, L.la}}, {S_ONE}, S_GAMMA, S_BK2, S_ONE, -1, P->C2, L.la));      // c + gamma + beta k2 x
-  RC(pmul(P, P->A2, L.la, P->B2, L.la, P->T2a));
-  RC(pmul(P, P->T2a, L.l2a, P->C2, L.la, P->T2b));
-  RC(pmul(P, P->T2b, L.l2b, cZ, L.lzx, P->T2));
   RC(lincomb(P, {{cA, L.la}, {S1, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ALPHA, -1, P->A3, L.la));
   RC(lincomb(P, {{cB, L.la}, {S2, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ONE, -1, P->B3, L.la));
   RC(lincomb(P, {{cC, L.la}, {S3, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ONE, -1, P->C3, L.la));
   RC(lincomb(P, {{cZ, L.lzx}}, {S_ONE}, -1, -1, S_ONE, S_OMEGA, P->ZW, L.lzw));       // z(omega x)
-  RC(pmul(P, P->A3, L.la, P->B3, L.la, P->T3a));
-  RC(pmul(P, P->T3a, L.l2a, P->C3, L.la, P->T3b));
-  RC(pmul(P, P->T3b, L.l2b, P->ZW, L.lzw, P->T3));
   RC(lincomb(P, {{cZ, L.lzx}}, {S_ONE}, S_NEG1, -1, S_ALPHA2, -1, P->Z1, L.lz1));     // alpha^2 (z - 1)
-  RC(pmul(P, P->Z1, L.lz1, L1, n, P->T4));
+  {
+    const PlkPolyMulJob g1[] = {{cA, L.la, cB, L.la, P->AB},      {cA, L.la, QL, n, P->AQL},
+                                {cB, L.la, QR, n, P->BQR},        {cC, L.la, QO, n, P->CQO},
+                                {P->A2, L.la, P->B2, L.la, P->T2a}, {P->A3, L.la, P->B3, L.la, P->T3a},
+                                {P->Z1, L.lz1, L1, n, P->T4}};
+    RC(plk_poly_mul_batch_launch(g1, 7, P->work, P->work_bytes, P->st));
+    const PlkPolyMulJob g2[] = {{P->AB, L.lab, QM, n, P->ABQM}, {P->T2a, L.l2a, P->C2, L.la, P->T2b},
+                                {P->T3a, L.l2a, P->C3, L.la, P->T3b}};
+    RC(plk_poly_mul_batch_launch(g2, 3, P->work, P->work_bytes, P->st));
+    const PlkPolyMulJob g3[] = {{P->T2b, L.l2b, cZ, L.lzx, P->T2}, {P->T3b, L.l2b, P->ZW, L.lzw, P->T3}};
+    RC(plk_poly_mul_batch_launch(g3, 2, P->work, P->work_bytes, P->st));
+  }
   RC(lincomb(P,
              {{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {P->BQR, L.lq1}, {P->CQO, L.lq1}, {QC, n}, {P->T2, L.l2},
               {P->T3, L.l3}, {P->T4, L.lt4}},

@@ -118,3 +118,57 @@ def test_rounds_deterministic_large(hip):
     a = pr.rounds_dev(dev, chal, rnd)
     b = pr.rounds_dev(dev, chal, rnd)
     assert a == b and len(a) == 34
+
+
+_BIG = {}
+
+
+def _big_case(oracle):
+    """n = 2^16 prove-shaped instance and its CPU answer (~11 s of oracle time, computed once)."""
+    if not _BIG:
+        n = 1 << 16
+        polys, chal, rnd, zh, pts = _synthetic(n, 41, 2 * n + 8)
+        ref = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes())
+        _BIG.update(n=n, polys=polys, chal=chal, rnd=rnd, zh=zh, pts=pts,
+                    want=ref.rounds(polys, chal, rnd, strict=False))
+    return _BIG
+
+
+def test_rounds_2_16_vs_oracle(hip, oracle):
+    """n = 2^16: the batched round-3 products (2^17..2^19 transforms) against the oracle."""
+    c = _big_case(oracle)
+    pr = hip.Prover(c["n"], c["zh"], c["pts"])
+    got = pr.rounds_dev([torch.from_numpy(p).to("cuda") for p in c["polys"]], c["chal"], c["rnd"])
+    assert got.hex() == c["want"].hex()
+
+
+_TILE13_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path[:0] = sys.argv[1:2]
+import plonkhip as hip
+hip.init(0)
+d = np.load(sys.argv[2])
+n = int(d["n"])
+polys = [torch.from_numpy(d["p%d" % i]).to("cuda") for i in range(13)]
+pr = hip.Prover(n, d["zh"], d["pts"])
+print(pr.rounds_dev(polys, [int(x) for x in d["chal"]], [int(x) for x in d["rnd"]]).hex())
+"""
+
+
+def test_rounds_2_16_tiles13_vs_oracle(hip, oracle, tmp_path):
+    """Same instance with every transform on the 2^13-element tile engine (PLK_NTT_T13_MIN_K
+    = 13, read once per process: a child process), so the batched prover runs the tile size
+    that 2^21..2^23 products use at n = 2^20."""
+    import os
+    import subprocess
+    import sys
+    c = _big_case(oracle)
+    f = tmp_path / "case.npz"
+    np.savez(f, n=c["n"], zh=c["zh"], pts=c["pts"], chal=np.array(c["chal"]), rnd=np.array(c["rnd"]),
+             **{"p%d" % i: p for i, p in enumerate(c["polys"])})
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plonk.c_amd")
+    env = dict(os.environ, PLK_NTT_T13_MIN_K="13")
+    r = subprocess.run([sys.executable, "-c", _TILE13_SCRIPT, pkg, str(f)], capture_output=True, text=True,
+                       env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == c["want"].hex()
