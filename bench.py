@@ -131,6 +131,14 @@ def components(torch, hip, dev, st):
     out["ntt_2^20_forward"] = {"ms": round(avg, 4), "Gelem_s": round((1 << k) / (avg * 1e-3) / 1e9, 2),
                                "passes": 2, "alg_bytes": 2 * 4 * (1 << k) * 2,
                                "GB_s_alg": round(2 * 8 * (1 << k) / (avg * 1e-3) / 1e9, 1)}
+    # the same transform, 8 independent arrays sharing each pass's launch (plk_ntt_batch_dev)
+    nb = 8
+    bb_ = [torch.randint(0, 2013265921, (nb, 1 << k), dtype=torch.int64, device=dev).to(torch.int32)
+           for _ in range(2)]
+    avg, med = event_avg_ms(torch, st, lambda i: hip.ntt_batch_dev(bb_[i % 2], k, nb, False, st), 20)
+    out["ntt_2^20_forward_batch8"] = {"ms_per_launch": round(avg, 4),
+                                      "Gelem_s": round(nb * (1 << k) / (avg * 1e-3) / 1e9, 2),
+                                      "GB_s_alg": round(nb * 2 * 8 * (1 << k) / (avg * 1e-3) / 1e9, 1)}
     # poly_mul 2^19 x 2^19 -> 2^20 - 1 coefficients (device-resident, 3 launches)
     la = lb = 1 << 19
     a = torch.randint(0, 17, (la,), dtype=torch.int16, device=dev).to(torch.uint8)

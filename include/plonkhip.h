@@ -110,6 +110,9 @@ int plk_poly_mul_dev(const uint8_t *d_a, size_t la, const uint8_t *d_b, size_t l
 /* Radix-2 NTT over BabyBear p = 15*2^27+1 on 2^log_n Montgomery-form u32, in place:
  * forward = DIF natural -> bit-reversed; inverse = DIT bit-reversed -> natural, unscaled. */
 int plk_ntt_dev(uint32_t *d_data, int log_n, int inverse, void *stream);
+/* batch independent transforms of 2^log_n points, array b at d_data + b 2^log_n; the arrays
+ * share each pass's launch (the prover's products run the same way). */
+int plk_ntt_batch_dev(uint32_t *d_data, int log_n, int batch, int inverse, void *stream);
 
 /* ---- device-resident prover (replaces plonk_new / plonk_prove / plonk_free,
  * src/plonk.h:53-139, 223-656, 120-139) ---------------------------------------------------

@@ -329,7 +329,17 @@ int plk_poly_mul_dev(const uint8_t* d_a, size_t la, const uint8_t* d_b, size_t l
 int plk_ntt_dev(uint32_t* d_data, int log_n, int inverse, void* stream) {
   int rc = ensure();
   if (rc) return rc;
-  return plk_ntt_launch(d_data, log_n, inverse, pick(stream));
+  return plk_ntt_launch(d_data, log_n, 1, inverse, pick(stream));
+}
+
+int plk_ntt_batch_dev(uint32_t* d_data, int log_n, int batch, int inverse, void* stream) {
+  int rc = ensure();
+  if (rc) return rc;
+  if (!d_data || batch < 1) {
+    plk_set_error("plk_ntt_batch_dev: null data or batch %d", batch);
+    return PLK_ERR_ARG;
+  }
+  return plk_ntt_launch(d_data, log_n, batch, inverse, pick(stream));
 }
 
 }  // extern "C"

@@ -624,19 +624,23 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
 
 // Standalone forward NTT (DIF, natural -> bit-reversed), in place on Montgomery-form u32,
 // or inverse (DIT, bit-reversed -> natural, NOT scaled by N^-1).  Same passes as poly_mul.
-int plk_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st) {
-  if (k < 1 || k > bb::TWO_ADICITY) return PLK_ERR_RANGE;
-  if (plk_wave_ntt_supported(k)) return plk_wave_ntt_launch(d, k, inverse, st);
+// batch independent arrays at d + b 2^k share each pass's launch (up to 8 per launch).
+int plk_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st) {
+  if (k < 1 || k > bb::TWO_ADICITY || batch < 1) return PLK_ERR_RANGE;
+  if (plk_wave_ntt_supported(k)) return plk_wave_ntt_launch(d, k, batch, inverse, st);
   // k <= 12: one workgroup-tile pass (lo = 0, a single tile holds the whole array)
   const Tw tw = inverse ? tw_inv() : tw_fwd();
   const Pass p{k, 0, k, 1};
   const size_t lds = pass_lds(p.M, p.C, false);
-  if (inverse)
-    hipLaunchKernelGGL((ntt_pass_kernel<true, IN_U32, OUT_U32>), dim3(1, 1), dim3(NTT_THREADS), lds, st, p, d, d,
-                       nullptr, nullptr, 0, 0, tw, nullptr, 0, 0u, nullptr);
-  else
-    hipLaunchKernelGGL((ntt_pass_kernel<false, IN_U32, OUT_U32>), dim3(1, 1), dim3(NTT_THREADS), lds, st, p, d, d,
-                       nullptr, nullptr, 0, 0, tw, nullptr, 0, 0u, nullptr);
+  for (int b = 0; b < batch; b++) {
+    uint32_t* db = d + ((uint64_t)b << k);
+    if (inverse)
+      hipLaunchKernelGGL((ntt_pass_kernel<true, IN_U32, OUT_U32>), dim3(1, 1), dim3(NTT_THREADS), lds, st, p, db, db,
+                         nullptr, nullptr, 0, 0, tw, nullptr, 0, 0u, nullptr);
+    else
+      hipLaunchKernelGGL((ntt_pass_kernel<false, IN_U32, OUT_U32>), dim3(1, 1), dim3(NTT_THREADS), lds, st, p, db, db,
+                         nullptr, nullptr, 0, 0, tw, nullptr, 0, 0u, nullptr);
+  }
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }

@@ -468,10 +468,8 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
 }
 
 template <int TB>
-int wave_ntt_t(uint32_t* d, int k, int inverse, hipStream_t st) {
+int wave_ntt_t(const WJobs& jobs, int nj, int k, int inverse, hipStream_t st) {
   const PlkTwTables t = plk_ntt_tables();
-  WJobs jobs{};
-  jobs.j[0].A = d;
   int Ms[4];
   const int np = wave_plan(k, TB, Ms);
   int lo[4];
@@ -479,8 +477,8 @@ int wave_ntt_t(uint32_t* d, int k, int inverse, hipStream_t st) {
   for (int s = 0; s < np; s++) {
     const int i = inverse ? np - 1 - s : s;
     const WPass p{k, lo[i]};
-    const int rc = inverse ? inv_m<TB, false>(Ms[i], p, jobs, 1, to_wtw(t, true), 0u, st)
-                           : fwd_m<TB, false, 1>(Ms[i], p, jobs, 1, to_wtw(t, false), st);
+    const int rc = inverse ? inv_m<TB, false>(Ms[i], p, jobs, nj, to_wtw(t, true), 0u, st)
+                           : fwd_m<TB, false, 1>(Ms[i], p, jobs, nj, to_wtw(t, false), st);
     if (rc) return rc;
   }
   return PLK_OK;
@@ -501,6 +499,14 @@ int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, uint32_t nin
   return PLK_OK;
 }
 
-int plk_wave_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st) {
-  return tile_bits(k) == 13 ? wave_ntt_t<13>(d, k, inverse, st) : wave_ntt_t<12>(d, k, inverse, st);
+// batch independent in-place transforms of 2^k points: array i at d + i 2^k, <= 8 per launch
+int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st) {
+  for (int j0 = 0; j0 < batch; j0 += WT_MAX_JOBS) {
+    const int m = batch - j0 < WT_MAX_JOBS ? batch - j0 : WT_MAX_JOBS;
+    WJobs w{};
+    for (int i = 0; i < m; i++) w.j[i].A = d + ((uint64_t)(j0 + i) << k);
+    const int rc = tile_bits(k) == 13 ? wave_ntt_t<13>(w, m, k, inverse, st) : wave_ntt_t<12>(w, m, k, inverse, st);
+    if (rc) return rc;
+  }
+  return PLK_OK;
 }

@@ -50,7 +50,7 @@ void plk_ntt_free_tables(void);
 size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb);
 int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
                         uint32_t* d_nz, void* d_work, hipStream_t st);
-int plk_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st);
+int plk_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st);
 struct PlkPolyMulJob {
   const uint8_t* a;
   uint64_t la;
@@ -73,4 +73,4 @@ struct WJob {
 };
 bool plk_wave_ntt_supported(int k);
 int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, uint32_t ninv, hipStream_t st);
-int plk_wave_ntt_launch(uint32_t* d, int k, int inverse, hipStream_t st);
+int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st);

@@ -48,6 +48,7 @@ SIGNATURES = {
     "plk_poly_mul_workspace": (_sz, [_sz, _sz]),
     "plk_poly_mul_dev": (C.c_int, [_vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp]),
     "plk_ntt_dev": (C.c_int, [_vp, C.c_int, C.c_int, _vp]),
+    "plk_ntt_batch_dev": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, _vp]),
     "plk_prover_create": (C.c_int, [_vp, C.POINTER(_vp)]),
     "plk_prover_destroy": (None, [_vp]),
     "plk_prover_device_bytes": (_sz, [_vp]),
@@ -228,6 +229,11 @@ def poly_mul_dev(a, la, b, lb, out, nz, work, stream=None):
 def ntt_dev(data, log_n, inverse=False, stream=None):
     _check("plk_ntt_dev", lib().plk_ntt_dev(_ptr(data), int(log_n), 1 if inverse else 0,
                                             _stream(stream)))
+
+
+def ntt_batch_dev(data, log_n, batch, inverse=False, stream=None):
+    _check("plk_ntt_batch_dev", lib().plk_ntt_batch_dev(_ptr(data), int(log_n), int(batch), 1 if inverse else 0,
+                                                        _stream(stream)))
 
 
 def parse_result(res_bytes):

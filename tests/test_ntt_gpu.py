@@ -102,3 +102,21 @@ def test_forward_vs_numpy_reference(hip, k):
     torch.cuda.synchronize()
     back = d.cpu().numpy().view(np.uint32).astype(np.uint64)
     assert np.array_equal(back, (x.astype(np.uint64) * np.uint64(1 << k)) % np.uint64(P))
+
+
+@pytest.mark.parametrize("k,batch", [(10, 3), (14, 9), (20, 8), (22, 3)])
+def test_batch_matches_single(hip, k, batch):
+    """plk_ntt_batch_dev (arrays sharing each pass's launch, <= 8 per launch) is bit-identical
+    to plk_ntt_dev on every array, forward and inverse."""
+    import torch
+    st = torch.cuda.current_stream()
+    g = torch.Generator(device="cpu").manual_seed(k * 100 + batch)
+    x = torch.randint(0, P, (batch, 1 << k), generator=g, dtype=torch.int64).to(torch.int32).cuda()
+    for inv in (False, True):
+        one = x.clone()
+        for b in range(batch):
+            hip.ntt_dev(one[b], k, inv, st)
+        many = x.clone()
+        hip.ntt_batch_dev(many, k, batch, inv, st)
+        torch.cuda.synchronize()
+        assert torch.equal(one, many), (k, batch, inv)
