@@ -1,11 +1,17 @@
 #!/bin/bash
-# Summarise a tools/profile_bench.sh run (merged back under gpurun_out/prof_<tag>/) into
-# the tracked profiles/ directory:  bash tools/collect_profiles.sh <tag> [round] [msms per launch]
+# Copy the summaries of a tools/round_profile.sh run (gpurun_out/prof_<tag>/) into the tracked
+# profiles/ directory:  bash tools/collect_profiles.sh <tag> <round>
 set -eu
 TAG=$1
 R=${2:-$TAG}
 P=gpurun_out/prof_$TAG
-python3 tools/kstats.py $P/trace/run_results.db --json profiles/${R}_bench_kernel_stats.json > profiles/${R}_bench_kernel_stats.txt
-python3 tools/pmc_summary.py $P/pmc/run_results.db msm_dlog_kernel --latest 22 ${3:-40} profiles/msm_pmc_latest.json > profiles/${R}_msm_pmc.json
+grep '^{' $P/bench.json > profiles/${R}_bench.json
 grep '^{' $P/bench_traced.json > profiles/${R}_bench_traced.json
+cp $P/bench_kernel_stats.txt profiles/${R}_bench_kernel_stats.txt
+cp $P/bench_kernel_stats.json profiles/${R}_bench_kernel_stats.json
+cp $P/msm_pmc.json profiles/${R}_msm_pmc.json
+cp $P/msm_pmc_latest.json profiles/msm_pmc_latest.json
+cp "$P/prove_2^20_breakdown.txt" "profiles/${R}_prove_2^20_breakdown.txt"
+cp $P/ntt_bench.json profiles/${R}_ntt_bench.json
+tail -1 $P/gpu_tests.log > profiles/${R}_gpu_tests.txt
 echo "wrote profiles/${R}_*"
