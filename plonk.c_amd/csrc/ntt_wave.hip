@@ -36,7 +36,15 @@
 
 namespace {
 
-constexpr int WT_NT = 1024;                    // threads per tile block
+#ifndef PLK_NTT_R12
+#define PLK_NTT_R12 2          // register bits per thread for 2^12 tiles (1024 threads)
+#endif
+#ifndef PLK_NTT_R13
+#define PLK_NTT_R13 3          // ... for 2^13 tiles
+#endif
+// register bits per thread for a tile size; the block has 2^(TB-R) threads
+constexpr int wt_r(int TB) { return TB == 13 ? PLK_NTT_R13 : PLK_NTT_R12; }
+constexpr int wt_nt(int TB) { return 1 << (TB - wt_r(TB)); }
 constexpr int WT_MAX_HI12 = 8;                 // widest high-bit pass with 2^12 tiles
 constexpr int WT_MAX_HI13 = 10;                // ... with 2^13 tiles
 
@@ -210,9 +218,9 @@ __device__ __forceinline__ void load_pass_tw(uint32_t* Tsm, const uint32_t* smal
 // Forward (DIF) pass over ARR (1 or 2) arrays of each job (blockIdx.y = job * ARR + array),
 // u32 in place, or the first pass reading bytes (zero padded, reduced mod 17, to Montgomery).
 template <int TB, int R, int M, bool FROM_U8, int ARR>
-__global__ __launch_bounds__(WT_NT) void wt_fwd_kernel(WPass p, WJobs jobs, WTw tw) {
+__global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WJobs jobs, WTw tw) {
   using G = Eng<TB, R, M>;
-  static_assert(G::NT == WT_NT, "tile block size");
+  static_assert(G::NT == wt_nt(TB), "tile block size");
   __shared__ uint32_t Tsm[M == TB ? W13_WORDS : 1 << M];
   __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
   const uint32_t tid = threadIdx.x;
@@ -259,9 +267,9 @@ __global__ __launch_bounds__(WT_NT) void wt_fwd_kernel(WPass p, WJobs jobs, WTw 
 // Inverse (DIT) pass, u32 in place; the final pass (TO_U8) scales by N^-1 (normal form,
 // which also leaves Montgomery form), reduces mod 17 and writes bytes for idx < out_len.
 template <int TB, int R, int M, bool TO_U8>
-__global__ __launch_bounds__(WT_NT) void wt_inv_kernel(WPass p, WJobs jobs, WTw tw, uint32_t ninv) {
+__global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, WTw tw, uint32_t ninv) {
   using G = Eng<TB, R, M>;
-  static_assert(G::NT == WT_NT, "tile block size");
+  static_assert(G::NT == wt_nt(TB), "tile block size");
   __shared__ uint32_t Tsm[M == TB ? W13_WORDS : 1 << M];
   __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
   const uint32_t tid = threadIdx.x;
@@ -308,9 +316,10 @@ __global__ __launch_bounds__(WT_NT) void wt_inv_kernel(WPass p, WJobs jobs, WTw 
 // Stage twiddles: W13 forward and inverse in LDS (2 x 16 KB); 2^13 tiles are held to <= 64
 // VGPRs (8 waves per SIMD) so two blocks share a CU.
 template <int TB, int R>
-__global__ __launch_bounds__(WT_NT, TB == 13 ? 8 : 1) void wt_center_kernel(WPass p, WJobs jobs, WTw twf, WTw twi) {
+__global__ __launch_bounds__(wt_nt(TB), TB == 13 && wt_nt(TB) == 1024 ? 8 : 1) void wt_center_kernel(WPass p, WJobs jobs,
+                                                                                                     WTw twf, WTw twi) {
   using G = Eng<TB, R, TB>;
-  static_assert(G::NT == WT_NT, "tile block size");
+  static_assert(G::NT == wt_nt(TB), "tile block size");
   static_assert(G::lbq(G::NR - 1, false) == 0 && G::lbq(0, true) == 0, "center mapping");
   __shared__ uint32_t Tlds[2 * W13_WORDS];
   __shared__ uint32_t bufs[(G::DBUF ? 2 : 1) * G::BUF];
@@ -373,15 +382,15 @@ WTw to_wtw(const PlkTwTables& t, bool inv) {
 
 template <int TB, int M, bool U8, int ARR>
 void launch_fwd(WPass p, const WJobs& jobs, int nj, WTw tw, hipStream_t st) {
-  constexpr int R = TB - 10;                    // 1024 threads per tile
+  constexpr int R = wt_r(TB);
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB);
-  hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, ARR>), dim3(tiles, ARR * nj), dim3(WT_NT), 0, st, p, jobs, tw);
+  hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, ARR>), dim3(tiles, ARR * nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw);
 }
 template <int TB, int M, bool U8>
 void launch_inv(WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipStream_t st) {
-  constexpr int R = TB - 10;
+  constexpr int R = wt_r(TB);
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB);
-  hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8>), dim3(tiles, nj), dim3(WT_NT), 0, st, p, jobs, tw, ninv);
+  hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8>), dim3(tiles, nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw, ninv);
 }
 
 // pass widths: 1..8 for both tile sizes, 9..10 for 2^13 tiles, M = TB for the lo = 0 pass
@@ -456,7 +465,7 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
     if (rc) return rc;
   }
   const uint32_t tiles = (uint32_t)((1ull << k) >> TB);
-  hipLaunchKernelGGL((wt_center_kernel<TB, TB - 10>), dim3(tiles, nj), dim3(WT_NT), 0, st, WPass{k, 0}, jobs, twf,
+  hipLaunchKernelGGL((wt_center_kernel<TB, wt_r(TB)>), dim3(tiles, nj), dim3(wt_nt(TB)), 0, st, WPass{k, 0}, jobs, twf,
                      twi);
   PLK_HIP(hipGetLastError());
   for (int i = np - 2; i >= 0; i--) {
