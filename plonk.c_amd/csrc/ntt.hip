@@ -29,6 +29,8 @@
 #include "plk_device.h"
 #include "plk_internal.h"
 
+#include <stdlib.h>
+
 #include <vector>
 
 __constant__ uint32_t c_mont17[17];            // v * R mod p for v = 0..16
@@ -397,6 +399,15 @@ Tw tw_inv() { return Tw{g_tw.d_small_i, g_tw.d_lo_i, g_tw.d_hi_i}; }
 
 }  // namespace
 
+static struct {
+  uint32_t *d_small_f = nullptr, *d_small_i = nullptr, *d_lo_f = nullptr, *d_hi_f = nullptr, *d_lo_i = nullptr,
+           *d_hi_i = nullptr;
+} g_tw29;
+
+PlkTwTables plk_ntt_tables29(void) {
+  return PlkTwTables{g_tw29.d_small_f, g_tw29.d_small_i, g_tw29.d_lo_f, g_tw29.d_hi_f, g_tw29.d_lo_i, g_tw29.d_hi_i};
+}
+
 PlkTwTables plk_ntt_tables(void) {
   return PlkTwTables{g_tw.d_small_f, g_tw.d_small_i, g_tw.d_lo_f, g_tw.d_hi_f, g_tw.d_lo_i, g_tw.d_hi_i};
 }
@@ -443,6 +454,48 @@ int plk_ntt_init_tables(void) {
       y = y * si2 % bb::P;
     }
   }
+  {
+    // F29 tables, same layouts (root of order 2^26; hi holds 2^14 entries)
+    const uint32_t w26 = f29::hpow(f29::GENERATOR, (f29::P - 1) >> f29::TWO_ADICITY);
+    const uint32_t w26i = f29::hpow(w26, f29::P - 2);
+    std::vector<uint32_t> sf2(SM), si2(SM), lf2(4096), hf2(1 << 14), li2(4096), hi2(1 << 14);
+    sf2[0] = si2[0] = f29::to_mont(1);
+    for (int j = 0; (1 << j) < SM; j++) {
+      const uint32_t wf = f29::hpow(w26, 1ull << (25 - j));   // order 2^(j+1)
+      const uint32_t wi = f29::hpow(w26i, 1ull << (25 - j));
+      uint64_t xf = 1, xi = 1;
+      for (int r = 0; r < (1 << j); r++) {
+        sf2[(1 << j) + r] = f29::to_mont((uint32_t)xf);
+        si2[(1 << j) + r] = f29::to_mont((uint32_t)xi);
+        xf = xf * wf % f29::P;
+        xi = xi * wi % f29::P;
+      }
+    }
+    uint64_t x = 1, y = 1;
+    for (int i = 0; i < 4096; i++) {
+      lf2[i] = f29::to_mont((uint32_t)x);
+      li2[i] = f29::to_mont((uint32_t)y);
+      x = x * w26 % f29::P;
+      y = y * w26i % f29::P;
+    }
+    const uint64_t st4 = f29::hpow(w26, 4096), st4i = f29::hpow(w26i, 4096);
+    x = 1, y = 1;
+    for (int i = 0; i < (1 << 14); i++) {
+      hf2[i] = f29::to_mont((uint32_t)x);
+      hi2[i] = f29::to_mont((uint32_t)y);
+      x = x * st4 % f29::P;
+      y = y * st4i % f29::P;
+    }
+    auto up2 = [](uint32_t** d, const std::vector<uint32_t>& h) -> int {
+      PLK_HIP(hipMalloc((void**)d, h.size() * 4));
+      PLK_HIP(hipMemcpy(*d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+      return PLK_OK;
+    };
+    int rc2;
+    if ((rc2 = up2(&g_tw29.d_small_f, sf2)) || (rc2 = up2(&g_tw29.d_small_i, si2)) || (rc2 = up2(&g_tw29.d_lo_f, lf2)) ||
+        (rc2 = up2(&g_tw29.d_hi_f, hf2)) || (rc2 = up2(&g_tw29.d_lo_i, li2)) || (rc2 = up2(&g_tw29.d_hi_i, hi2)))
+      return rc2;
+  }
   uint32_t m17[17];
   for (int v = 0; v < 17; v++) m17[v] = bb::to_mont((uint32_t)v);
   PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_mont17), m17, sizeof m17));
@@ -461,6 +514,9 @@ int plk_ntt_init_tables(void) {
 void plk_ntt_free_tables(void) {
   (void)hipFree(g_tw.d_small_f); (void)hipFree(g_tw.d_small_i); (void)hipFree(g_tw.d_lo_f);
   (void)hipFree(g_tw.d_hi_f); (void)hipFree(g_tw.d_lo_i); (void)hipFree(g_tw.d_hi_i);
+  (void)hipFree(g_tw29.d_small_f); (void)hipFree(g_tw29.d_small_i); (void)hipFree(g_tw29.d_lo_f);
+  (void)hipFree(g_tw29.d_hi_f); (void)hipFree(g_tw29.d_lo_i); (void)hipFree(g_tw29.d_hi_i);
+  g_tw29.d_small_f = g_tw29.d_small_i = g_tw29.d_lo_f = g_tw29.d_hi_f = g_tw29.d_lo_i = g_tw29.d_hi_i = nullptr;
   g_tw = TwHost{};
 }
 
@@ -504,7 +560,18 @@ static size_t pass_lds(int M, int C, bool center) {
 // es[i] > 0: the split plan (product_plan) -- the longer operand's last es[i] coefficients are
 // multiplied in directly by polymul_tail_kernel after the transform.
 static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, void* d_work, hipStream_t st) {
-  const uint32_t ninv = bb::hpow(1ull << k, bb::P - 2);   // normal form on purpose
+  // F29 (lazy reduction, fewer VALU per butterfly) whenever every convolution term fits it
+  static int no29 = -1;
+  if (no29 < 0) {
+    const char* e = getenv("PLK_NTT_NO_F29");
+    no29 = e && atoi(e) != 0;
+  }
+  bool use29 = !no29 && k <= f29::TWO_ADICITY;
+  for (int i = 0; i < m; i++) {
+    const uint64_t mn = g[i].la < g[i].lb ? g[i].la : g[i].lb;
+    if (mn * 256 >= f29::P) use29 = false;
+  }
+  const uint32_t ninv = use29 ? f29::hpow(1ull << k, f29::P - 2) : bb::hpow(1ull << k, bb::P - 2);   // normal form
   WJob w[64];
   for (int i = 0; i < m; i++) {
     const PlkPolyMulJob& j = g[i];
@@ -516,7 +583,7 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
     uint32_t* A = (uint32_t*)d_work + ((size_t)2 * i << k);
     w[i] = WJob{lgp, shp, llg - e, lsh, j.out, llg - e + lsh - 1, A, A + (1ull << k)};
   }
-  int rc = plk_wave_poly_mul_batch_launch(w, m, k, ninv, st);
+  int rc = plk_wave_poly_mul_batch_launch(w, m, k, use29 ? 1 : 0, ninv, st);
   if (rc) return rc;
   for (int i = 0; i < m; i++) {
     const uint64_t e = es ? es[i] : 0;

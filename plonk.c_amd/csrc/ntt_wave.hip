@@ -42,6 +42,14 @@ namespace {
 #ifndef PLK_NTT_R13
 #define PLK_NTT_R13 3          // ... for 2^13 tiles
 #endif
+#ifndef PLK_NTT_RC13
+#define PLK_NTT_RC13 3         // register bits per thread of the 2^13-tile center kernel
+#endif
+#ifndef PLK_NTT_CW13
+#define PLK_NTT_CW13 1         // waves per SIMD it must fit (tuning)
+#endif
+constexpr int wt_rc(int TB) { return TB == 13 ? PLK_NTT_RC13 : PLK_NTT_R12; }
+constexpr int wt_ntc(int TB) { return 1 << (TB - wt_rc(TB)); }
 // register bits per thread for a tile size; the block has 2^(TB-R) threads
 constexpr int wt_r(int TB) { return TB == 13 ? PLK_NTT_R13 : PLK_NTT_R12; }
 constexpr int wt_nt(int TB) { return 1 << (TB - wt_r(TB)); }
@@ -49,8 +57,6 @@ constexpr int WT_MAX_HI12 = 8;                 // widest high-bit pass with 2^12
 constexpr int WT_MAX_HI13 = 10;                // ... with 2^13 tiles
 
 __device__ __forceinline__ int wphys(int e) { return e + (e >> 5); }
-__device__ __forceinline__ uint32_t wpad(uint32_t i) { return i + (i >> 6); }   // padded W13 index
-constexpr int W13_WORDS = 4096 + 64;
 
 struct WPass {
   int k;    // log2 N
@@ -67,15 +73,52 @@ struct WJobs {
 
 struct WTw {
   const uint32_t* small;   // T[2^j + r] = w_{2^(j+1)}^r (Montgomery), 2^PLK_NTT_SMALL_LOG entries
-  const uint32_t* lo;      // w_{2^27}^i, i < 4096
-  const uint32_t* hi;      // w_{2^27}^(4096 i)
+  const uint32_t* lo;      // w_{2^ADIC}^i, i < 4096 (ADIC = the field's 2-adicity)
+  const uint32_t* hi;      // w_{2^ADIC}^(4096 i)
+};
+
+// Field policies.  FBB: BabyBear, values fully reduced in [0, p).  F29: p = 7 2^26 + 1, values
+// lazy in [0, 2p) (plk_device.h): DIF butterfly 7 VALU instead of 10, DIT 9 instead of 11.
+struct FBB {
+  static constexpr int ADIC = bb::TWO_ADICITY;
+  __device__ static __forceinline__ void dif(uint32_t& u, uint32_t& x, uint32_t w) {
+    const uint32_t a = u, b = x;
+    u = bb::madd(a, b);
+    x = bb::mmul(bb::msub_lazy(a, b), w);
+  }
+  __device__ static __forceinline__ void dit(uint32_t& u, uint32_t& x, uint32_t w) {
+    const uint32_t xw = bb::mmul(x, w), a = u;
+    u = bb::madd(a, xw);
+    x = bb::msub(a, xw);
+  }
+  __device__ static __forceinline__ uint32_t mul(uint32_t a, uint32_t b) { return bb::mmul(a, b); }
+  __device__ static __forceinline__ uint32_t from_byte(uint32_t b) { return bb::mmul(b % 17u, bb::R2); }
+  __device__ static __forceinline__ uint32_t out17(uint32_t v, uint32_t ninv) { return bb::mmul(v, ninv) % 17u; }
+};
+struct F29 {
+  static constexpr int ADIC = f29::TWO_ADICITY;
+  __device__ static __forceinline__ void dif(uint32_t& u, uint32_t& x, uint32_t w) {
+    const uint32_t a = u, b = x;                 // a, b < 2p
+    u = f29::red2(a + b);                        // < 4p -> < 2p
+    x = f29::mmul(a + f29::P2 - b, w);           // (0, 4p) x [0, p) -> [0, 2p)
+  }
+  __device__ static __forceinline__ void dit(uint32_t& u, uint32_t& x, uint32_t w) {
+    const uint32_t xw = f29::mmul(x, w), a = u;  // [0, 2p)
+    u = f29::red2(a + xw);
+    x = f29::red2(a + f29::P2 - xw);
+  }
+  __device__ static __forceinline__ uint32_t mul(uint32_t a, uint32_t b) { return f29::mmul(a, b); }
+  __device__ static __forceinline__ uint32_t from_byte(uint32_t b) { return f29::mmul(b % 17u, f29::R2); }
+  __device__ static __forceinline__ uint32_t out17(uint32_t v, uint32_t ninv) {
+    return f29::red1(f29::mmul(v, ninv)) % 17u;
+  }
 };
 
 // Tile engine: TB tile bits, R local bits per thread (E = 2^R registers, 2^(TB-R) threads
 // per tile), a pass of M row bits.  HIGH = the pass is over high index bits (lo > 0):
 // exactly the passes with M < TB.  Tiles of 2^12 use double-buffered exchanges (one barrier
 // each); 2^13 tiles a single buffer (two barriers) so two blocks fit a CU's LDS.
-template <int TB, int R, int M>
+template <int TB, int R, int M, class F = FBB>
 struct Eng {
   static constexpr int E = 1 << R;
   static constexpr int NT = 1 << (TB - R);
@@ -124,20 +167,13 @@ struct Eng {
       for (int k = 0; k < E; k++) {
         if (k & (1 << q)) continue;
         const uint32_t rr = blow + ((uint32_t)(k & ((1 << q) - 1)) << LB);   // row mod 2^s
-        // lo = 0 passes (M = TB) index W13[i] = w_{2^13}^i (i < 4096, the top level of the
-        // small table): w_{2^(s+1)}^rr = W13[rr << (12 - s)], stored padded (one word per 64)
-        // so the 2^(12-s)-strided reads of the low stages spread over the banks; high passes
-        // read the 2^M-entry prefix T[2^s + rr]
-        const uint32_t w = M == TB ? Tsm[wpad(rr << (12 - s))] : Tsm[(1u << s) + rr];
-        const uint32_t u = v[k], x = v[k | (1 << q)];
-        if (!INV) {
-          v[k] = bb::madd(u, x);
-          v[k | (1 << q)] = bb::mmul(bb::msub_lazy(u, x), w);
-        } else {
-          const uint32_t xw = bb::mmul(x, w);
-          v[k] = bb::madd(u, xw);
-          v[k | (1 << q)] = bb::msub(u, xw);
-        }
+        // T[2^s + rr] = w_{2^(s+1)}^rr: consecutive rows read consecutive words (no bank
+        // conflicts) and the address is linear in the register index, so it folds into the
+        // ds_read offset.  (A padded W13 table read at W13[rr << (12 - s)] halved the LDS but
+        // needed ~4 VALU of address math per butterfly.)
+        const uint32_t w = Tsm[(1u << s) + rr];
+        if (!INV) F::dif(v[k], v[k | (1 << q)], w);
+        else F::dit(v[k], v[k | (1 << q)], w);
       }
     }
   }
@@ -187,7 +223,7 @@ struct Eng {
     const int sh = p.lo - cb;
     const uint32_t L = ((tile & ((1u << sh) - 1)) << cb) | c;
     const uint32_t f = __brev(r) >> (32 - M);
-    return (L * f) << (27 - p.lo - M);   // w_{2^(lo+M)}^(L f); L f < 2^(lo+M)
+    return (L * f) << (F::ADIC - p.lo - M);   // w_{2^(lo+M)}^(L f) in w_{2^ADIC} units
   }
 };
 
@@ -197,15 +233,9 @@ __device__ __forceinline__ uint32_t block_tile() {
   return (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
 }
 
-// the pass's stage twiddles into LDS: W13 (4096 words) for a lo = 0 pass, else the first 2^M
-// entries of the small table
-template <int M, int TB, int NT>
+// the pass's stage twiddles into LDS: the first 2^M entries of the table T
+template <int M, int NT>
 __device__ __forceinline__ void load_pass_tw(uint32_t* Tsm, const uint32_t* small) {
-  if (M == TB) {
-#pragma unroll
-    for (int i = 0; i < 4096 / NT; i++) Tsm[wpad(i * NT + threadIdx.x)] = small[4096 + i * NT + threadIdx.x];
-    return;
-  }
 #pragma unroll
   for (int i = 0; i < ((1 << M) + NT - 1) / NT; i++) {
     const int j = i * NT + (int)threadIdx.x;
@@ -217,11 +247,11 @@ __device__ __forceinline__ void load_pass_tw(uint32_t* Tsm, const uint32_t* smal
 
 // Forward (DIF) pass over ARR (1 or 2) arrays of each job (blockIdx.y = job * ARR + array),
 // u32 in place, or the first pass reading bytes (zero padded, reduced mod 17, to Montgomery).
-template <int TB, int R, int M, bool FROM_U8, int ARR>
+template <int TB, int R, int M, bool FROM_U8, int ARR, class F>
 __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WJobs jobs, WTw tw) {
-  using G = Eng<TB, R, M>;
+  using G = Eng<TB, R, M, F>;
   static_assert(G::NT == wt_nt(TB), "tile block size");
-  __shared__ uint32_t Tsm[M == TB ? W13_WORDS : 1 << M];
+  __shared__ uint32_t Tsm[1 << M];
   __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
@@ -237,7 +267,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WJobs jobs, 
 #pragma unroll
   for (int k = 0; k < G::E; k++) {
     const uint64_t idx = G::index(p, tile, b0 + ((uint32_t)k << L0));
-    if (FROM_U8) v[k] = idx < ls ? bb::mmul((uint32_t)(s8[idx] % 17u), bb::R2) : 0u;
+    if (FROM_U8) v[k] = idx < ls ? F::from_byte(s8[idx]) : 0u;
     else v[k] = d[idx];
   }
   // column factor table words of the elements this thread stores (HIGH passes)
@@ -252,25 +282,25 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WJobs jobs, 
       ch[k] = tw.hi[ex >> 12];
     }
   }
-  load_pass_tw<M, TB, G::NT>(Tsm, tw.small);
+  load_pass_tw<M, G::NT>(Tsm, tw.small);
   __syncthreads();
   G::template pass<false>(v, tid, bufs, 0, Tsm);
 #pragma unroll
   for (int k = 0; k < G::E; k++) {
     const uint32_t e = bf + ((uint32_t)k << LF);
     uint32_t x = v[k];
-    if (G::HIGH) x = bb::mmul(x, bb::mmul(cl[k], ch[k]));
+    if (G::HIGH) x = F::mul(x, F::mul(cl[k], ch[k]));
     d[G::index(p, tile, e)] = x;
   }
 }
 
 // Inverse (DIT) pass, u32 in place; the final pass (TO_U8) scales by N^-1 (normal form,
 // which also leaves Montgomery form), reduces mod 17 and writes bytes for idx < out_len.
-template <int TB, int R, int M, bool TO_U8>
+template <int TB, int R, int M, bool TO_U8, class F>
 __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, WTw tw, uint32_t ninv) {
-  using G = Eng<TB, R, M>;
+  using G = Eng<TB, R, M, F>;
   static_assert(G::NT == wt_nt(TB), "tile block size");
-  __shared__ uint32_t Tsm[M == TB ? W13_WORDS : 1 << M];
+  __shared__ uint32_t Tsm[1 << M];
   __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
@@ -293,10 +323,10 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
       ch[k] = tw.hi[ex >> 12];
     }
   }
-  load_pass_tw<M, TB, G::NT>(Tsm, tw.small);
+  load_pass_tw<M, G::NT>(Tsm, tw.small);
   if (G::HIGH) {
 #pragma unroll
-    for (int k = 0; k < G::E; k++) v[k] = bb::mmul(v[k], bb::mmul(cl[k], ch[k]));
+    for (int k = 0; k < G::E; k++) v[k] = F::mul(v[k], F::mul(cl[k], ch[k]));
   }
   __syncthreads();
   G::template pass<true>(v, tid, bufs, 0, Tsm);
@@ -306,25 +336,24 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   for (int k = 0; k < G::E; k++) {
     const uint64_t idx = G::index(p, tile, bf + ((uint32_t)k << LF));
     if (!TO_U8) d[idx] = v[k];
-    else if (idx < out_len) out8[idx] = (uint8_t)(bb::mmul(v[k], ninv) % 17u);
+    else if (idx < out_len) out8[idx] = (uint8_t)F::out17(v[k], ninv);
   }
 }
 
 // Center of poly_mul: last forward pass (lo = 0) of a and b, pointwise product, first
 // inverse pass, all in registers of one block; result written over a.  The last DIF round
 // and the first DIT round both have local bits [0, R), so no exchange sits in between.
-// Stage twiddles: W13 forward and inverse in LDS (2 x 16 KB); 2^13 tiles are held to <= 64
-// VGPRs (8 waves per SIMD) so two blocks share a CU.
-template <int TB, int R>
-__global__ __launch_bounds__(wt_nt(TB), TB == 13 && wt_nt(TB) == 1024 ? 8 : 1) void wt_center_kernel(WPass p, WJobs jobs,
+// Stage twiddles: the forward and inverse tables T in LDS (2 x 2^TB words).
+template <int TB, int R, class F>
+__global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_center_kernel(WPass p, WJobs jobs,
                                                                                                      WTw twf, WTw twi) {
-  using G = Eng<TB, R, TB>;
-  static_assert(G::NT == wt_nt(TB), "tile block size");
+  using G = Eng<TB, R, TB, F>;
+  static_assert(G::NT == wt_ntc(TB), "tile block size");
   static_assert(G::lbq(G::NR - 1, false) == 0 && G::lbq(0, true) == 0, "center mapping");
-  __shared__ uint32_t Tlds[2 * W13_WORDS];
+  __shared__ uint32_t Tlds[2 << TB];
   __shared__ uint32_t bufs[(G::DBUF ? 2 : 1) * G::BUF];
   const uint32_t* Tf = Tlds;
-  const uint32_t* Ti = Tlds + W13_WORDS;
+  const uint32_t* Ti = Tlds + (1 << TB);
   uint32_t* d0 = jobs.j[blockIdx.y].A;
   const uint32_t* d1 = jobs.j[blockIdx.y].B;
   const uint32_t tid = threadIdx.x;
@@ -338,13 +367,13 @@ __global__ __launch_bounds__(wt_nt(TB), TB == 13 && wt_nt(TB) == 1024 ? 8 : 1) v
     va[k] = d0[idx];
     vb[k] = d1[idx];
   }
-  load_pass_tw<TB, TB, G::NT>(Tlds, twf.small);
-  load_pass_tw<TB, TB, G::NT>(Tlds + W13_WORDS, twi.small);
+  load_pass_tw<TB, G::NT>(Tlds, twf.small);
+  load_pass_tw<TB, G::NT>(Tlds + (1 << TB), twi.small);
   __syncthreads();
   G::template pass<false>(va, tid, bufs, 0, Tf);
   G::template pass<false>(vb, tid, bufs, G::XCH, Tf);
 #pragma unroll
-  for (int k = 0; k < G::E; k++) va[k] = bb::mmul(va[k], vb[k]);
+  for (int k = 0; k < G::E; k++) va[k] = F::mul(va[k], vb[k]);
   G::template pass<true>(va, tid, bufs, 2 * G::XCH, Ti);
   constexpr int LF = G::lbq(G::NR - 1, true);
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, true);
@@ -380,23 +409,23 @@ WTw to_wtw(const PlkTwTables& t, bool inv) {
   return inv ? WTw{t.small_i, t.lo_i, t.hi_i} : WTw{t.small_f, t.lo_f, t.hi_f};
 }
 
-template <int TB, int M, bool U8, int ARR>
+template <int TB, int M, bool U8, int ARR, class F>
 void launch_fwd(WPass p, const WJobs& jobs, int nj, WTw tw, hipStream_t st) {
   constexpr int R = wt_r(TB);
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB);
-  hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, ARR>), dim3(tiles, ARR * nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw);
+  hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, ARR, F>), dim3(tiles, ARR * nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw);
 }
-template <int TB, int M, bool U8>
+template <int TB, int M, bool U8, class F>
 void launch_inv(WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipStream_t st) {
   constexpr int R = wt_r(TB);
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB);
-  hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8>), dim3(tiles, nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw, ninv);
+  hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8, F>), dim3(tiles, nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw, ninv);
 }
 
 // pass widths: 1..8 for both tile sizes, 9..10 for 2^13 tiles, M = TB for the lo = 0 pass
-template <int TB, bool U8, int ARR>
+template <int TB, bool U8, int ARR, class F>
 int fwd_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, hipStream_t st) {
-#define PLK_FWD(m) launch_fwd<TB, m, U8, ARR>(p, jobs, nj, tw, st)
+#define PLK_FWD(m) launch_fwd<TB, m, U8, ARR, F>(p, jobs, nj, tw, st)
   switch (M) {
     case 1: PLK_FWD(1); break;
     case 2: PLK_FWD(2); break;
@@ -412,7 +441,7 @@ int fwd_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, hipStream_t st) {
         if (M == 10) { PLK_FWD(10); break; }
       }
       if constexpr (!U8) {
-        if (M == TB) { launch_fwd<TB, TB, false, ARR>(p, jobs, nj, tw, st); break; }
+        if (M == TB) { launch_fwd<TB, TB, false, ARR, F>(p, jobs, nj, tw, st); break; }
       }
       plk_set_error("wave plan: unsupported pass width %d (tile bits %d)", M, TB);
       return PLK_ERR_ARG;
@@ -422,9 +451,9 @@ int fwd_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, hipStream_t st) {
   return PLK_OK;
 }
 
-template <int TB, bool U8>
+template <int TB, bool U8, class F>
 int inv_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipStream_t st) {
-#define PLK_INV(m) launch_inv<TB, m, U8>(p, jobs, nj, tw, ninv, st)
+#define PLK_INV(m) launch_inv<TB, m, U8, F>(p, jobs, nj, tw, ninv, st)
   switch (M) {
     case 1: PLK_INV(1); break;
     case 2: PLK_INV(2); break;
@@ -440,7 +469,7 @@ int inv_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipS
         if (M == 10) { PLK_INV(10); break; }
       }
       if constexpr (!U8) {
-        if (M == TB) { launch_inv<TB, TB, false>(p, jobs, nj, tw, ninv, st); break; }
+        if (M == TB) { launch_inv<TB, TB, false, F>(p, jobs, nj, tw, ninv, st); break; }
       }
       plk_set_error("wave plan: unsupported pass width %d (tile bits %d)", M, TB);
       return PLK_ERR_ARG;
@@ -450,9 +479,9 @@ int inv_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipS
   return PLK_OK;
 }
 
-template <int TB>
+template <int TB, class F>
 int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t st) {
-  const PlkTwTables t = plk_ntt_tables();
+  const PlkTwTables t = F::ADIC == f29::TWO_ADICITY ? plk_ntt_tables29() : plk_ntt_tables();
   const WTw twf = to_wtw(t, false), twi = to_wtw(t, true);
   int Ms[4];
   const int np = wave_plan(k, TB, Ms);
@@ -461,16 +490,17 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
   int rc;
   for (int i = 0; i < np - 1; i++) {
     const WPass p{k, lo[i]};
-    rc = i == 0 ? fwd_m<TB, true, 2>(Ms[i], p, jobs, nj, twf, st) : fwd_m<TB, false, 2>(Ms[i], p, jobs, nj, twf, st);
+    rc = i == 0 ? fwd_m<TB, true, 2, F>(Ms[i], p, jobs, nj, twf, st) : fwd_m<TB, false, 2, F>(Ms[i], p, jobs, nj, twf, st);
     if (rc) return rc;
   }
   const uint32_t tiles = (uint32_t)((1ull << k) >> TB);
-  hipLaunchKernelGGL((wt_center_kernel<TB, wt_r(TB)>), dim3(tiles, nj), dim3(wt_nt(TB)), 0, st, WPass{k, 0}, jobs, twf,
+  hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F>), dim3(tiles, nj), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, jobs, twf,
                      twi);
   PLK_HIP(hipGetLastError());
   for (int i = np - 2; i >= 0; i--) {
     const WPass p{k, lo[i]};
-    rc = i == 0 ? inv_m<TB, true>(Ms[i], p, jobs, nj, twi, ninv, st) : inv_m<TB, false>(Ms[i], p, jobs, nj, twi, 0u, st);
+    rc = i == 0 ? inv_m<TB, true, F>(Ms[i], p, jobs, nj, twi, ninv, st)
+                : inv_m<TB, false, F>(Ms[i], p, jobs, nj, twi, 0u, st);
     if (rc) return rc;
   }
   return PLK_OK;
@@ -486,8 +516,8 @@ int wave_ntt_t(const WJobs& jobs, int nj, int k, int inverse, hipStream_t st) {
   for (int s = 0; s < np; s++) {
     const int i = inverse ? np - 1 - s : s;
     const WPass p{k, lo[i]};
-    const int rc = inverse ? inv_m<TB, false>(Ms[i], p, jobs, nj, to_wtw(t, true), 0u, st)
-                           : fwd_m<TB, false, 1>(Ms[i], p, jobs, nj, to_wtw(t, false), st);
+    const int rc = inverse ? inv_m<TB, false, FBB>(Ms[i], p, jobs, nj, to_wtw(t, true), 0u, st)
+                           : fwd_m<TB, false, 1, FBB>(Ms[i], p, jobs, nj, to_wtw(t, false), st);
     if (rc) return rc;
   }
   return PLK_OK;
@@ -497,12 +527,14 @@ int wave_ntt_t(const WJobs& jobs, int nj, int k, int inverse, hipStream_t st) {
 
 bool plk_wave_ntt_supported(int k) { return k > 12 && k <= bb::TWO_ADICITY; }
 
-int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, uint32_t ninv, hipStream_t st) {
+int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, int field, uint32_t ninv, hipStream_t st) {
   for (int j0 = 0; j0 < nj; j0 += WT_MAX_JOBS) {
     const int m = nj - j0 < WT_MAX_JOBS ? nj - j0 : WT_MAX_JOBS;
     WJobs w{};
     for (int i = 0; i < m; i++) w.j[i] = jobs[j0 + i];
-    const int rc = tile_bits(k) == 13 ? wave_poly_mul_t<13>(w, m, k, ninv, st) : wave_poly_mul_t<12>(w, m, k, ninv, st);
+    const bool t13 = tile_bits(k) == 13;
+    const int rc = field == 1 ? (t13 ? wave_poly_mul_t<13, F29>(w, m, k, ninv, st) : wave_poly_mul_t<12, F29>(w, m, k, ninv, st))
+                              : (t13 ? wave_poly_mul_t<13, FBB>(w, m, k, ninv, st) : wave_poly_mul_t<12, FBB>(w, m, k, ninv, st));
     if (rc) return rc;
   }
   return PLK_OK;

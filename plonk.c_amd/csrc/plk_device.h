@@ -67,6 +67,58 @@ constexpr uint32_t GENERATOR = 31;           // generates F_p^*
 }  // namespace bb
 
 // ----------------------------------------------------------------------------------------
+// F29: p = 7 * 2^26 + 1 = 469762049 < 2^29, Montgomery R = 2^32, values kept LAZILY in
+// [0, 2p).  Because 8p < 2^32, REDC of any product of a value < 4p and one < 2p lands in
+// [0, 2p) with no final subtraction, and sums / differences of two lazy values stay < 4p:
+// a DIF butterfly is 7 VALU (BabyBear: 10).  Exact for poly_mul when every convolution term
+// fits: min(la, lb) * 256 < p, i.e. min(la, lb) <= 1835007 (the 2^20-gate prover's largest
+// product has min = 2^20 + 3); larger products use BabyBear.
+// ----------------------------------------------------------------------------------------
+namespace f29 {
+constexpr uint32_t P = 469762049u;           // 7 * 2^26 + 1
+constexpr int TWO_ADICITY = 26;
+constexpr uint32_t GENERATOR = 3;            // generates F_p^*
+constexpr uint32_t neg_inv_p() {
+  uint32_t x = 1;
+  for (int i = 0; i < 5; i++) x *= 2u - P * x;
+  return 0u - x;
+}
+constexpr uint32_t PINV = neg_inv_p();
+static_assert(P * (0u - PINV) == 1u, "p * p^{-1} == 1 mod 2^32");
+static_assert(8ull * P < (1ull << 32), "lazy reduction needs 8p < 2^32");
+constexpr uint32_t R2 = (uint32_t)((((unsigned __int128)1) << 64) % P);
+constexpr uint32_t P2 = 2 * P;
+
+// a * b * R^-1 mod p in [0, 2p) for a * b < p 2^32 (e.g. a < 4p, b < 2p)
+__host__ __device__ __forceinline__ uint32_t mmul(uint32_t a, uint32_t b) {
+  const uint64_t t = (uint64_t)a * b;
+  const uint32_t m = (uint32_t)t * PINV;
+  return (uint32_t)((t + (uint64_t)m * P) >> 32);
+}
+// [0, 4p) -> [0, 2p)
+__host__ __device__ __forceinline__ uint32_t red2(uint32_t x) {
+  const uint32_t y = x - P2;
+  return y < x ? y : x;
+}
+// [0, 2p) -> [0, p)
+__host__ __device__ __forceinline__ uint32_t red1(uint32_t x) {
+  const uint32_t y = x - P;
+  return y < x ? y : x;
+}
+inline uint32_t hpow(uint64_t b, uint64_t e) {
+  uint64_t r = 1;
+  b %= P;
+  while (e) {
+    if (e & 1) r = r * b % P;
+    b = b * b % P;
+    e >>= 1;
+  }
+  return (uint32_t)r;
+}
+inline uint32_t to_mont(uint32_t x) { return (uint32_t)(((uint64_t)x << 32) % P); }
+}  // namespace f29
+
+// ----------------------------------------------------------------------------------------
 // E(F101): y^2 = x^3 + 3 has 102 points and is cyclic (102 = 2*3*17).  The MSM maps every
 // canonical point to its discrete log in Z/102 w.r.t. a fixed generator g0 of order 102,
 // so sum c_i * P_i becomes sum c_i * log(P_i) mod 102 -- an exact group isomorphism.

@@ -44,7 +44,8 @@ struct PlkTwTables {
   const uint32_t *lo_f, *hi_f;         // w_{2^27}^i = lo[i & 4095] * hi[i >> 12]
   const uint32_t *lo_i, *hi_i;         // same for the inverse root
 };
-PlkTwTables plk_ntt_tables(void);
+PlkTwTables plk_ntt_tables(void);      // BabyBear
+PlkTwTables plk_ntt_tables29(void);    // F29 (roots of order 2^26; lo/hi: w_{2^26}^i = lo[i & 4095] hi[i >> 12])
 int plk_ntt_init_tables(void);
 void plk_ntt_free_tables(void);
 size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb);
@@ -72,5 +73,7 @@ struct WJob {
   uint32_t* B;
 };
 bool plk_wave_ntt_supported(int k);
-int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, uint32_t ninv, hipStream_t st);
+// field 0 = BabyBear, 1 = F29 (lazy; only when every job's min(la, lb) * 256 < f29::P);
+// ninv = 2^-k mod p in normal form for that field
+int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, int field, uint32_t ninv, hipStream_t st);
 int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st);

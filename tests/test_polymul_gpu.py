@@ -82,3 +82,19 @@ def test_device_api(hip, oracle):
     torch.cuda.synchronize()
     n = int(nz[0].item()) or 1
     assert bytes(out[:n].cpu().numpy()) == oracle.poly_mul_ntt(a, b)
+
+
+@pytest.mark.parametrize("m", [1835007, 1835008])
+def test_field_boundary_worst_case(hip, m):
+    """Products run over F29 (p = 7 2^26 + 1, lazy reduction) while every convolution term
+    fits, min(la, lb) * 256 < p, i.e. min(la, lb) <= 1835007, and over BabyBear above.  All
+    coefficients 16 make every term its maximum: c_i = 256 min(i + 1, la, lb, la + lb - 1 - i),
+    and 256 = 1 (mod 17)."""
+    la, lb = m, m + 1000
+    a = np.full(la, 16, np.uint8)
+    b = np.full(lb, 16, np.uint8)
+    i = np.arange(la + lb - 1, dtype=np.int64)
+    want = (np.minimum(np.minimum(i + 1, la), np.minimum(lb, la + lb - 1 - i)) % 17).astype(np.uint8)
+    nz = np.flatnonzero(want)
+    want = want[:int(nz[-1]) + 1]
+    assert hip.poly_mul(a, b) == want.tobytes()
