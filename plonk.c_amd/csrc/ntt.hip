@@ -31,6 +31,7 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
 #include <vector>
 
 __constant__ uint32_t c_mont17[17];            // v * R mod p for v = 0..16
@@ -361,26 +362,58 @@ __global__ __launch_bounds__(256) void polymul_direct_kernel(const uint8_t* lg, 
   (void)nz;   // trimmed length: trim_kernel
 }
 
-// Tail of a split product (see plk_poly_mul_launch): out[i] += sum_j t[j] g[i - base - j] for
-// i in [base, rl), where out[i] for i >= ntt_len is not yet written (taken as 0).
-__global__ __launch_bounds__(256) void polymul_tail_kernel(const uint8_t* __restrict__ g, uint64_t lg,
-                                                           const uint8_t* __restrict__ t, int lt, uint64_t base,
-                                                           uint64_t ntt_len, uint8_t* __restrict__ out8,
-                                                           uint64_t rl) {
-  __shared__ uint32_t T[64];
-  if ((int)threadIdx.x < lt) T[threadIdx.x] = t[threadIdx.x] % 17u;
-  __syncthreads();
-  for (uint64_t i = base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rl;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t acc = i < ntt_len ? out8[i] : 0u;
-    const uint64_t o0 = i - base;
-    for (int j = 0; j < lt; j++) {
-      const int64_t o = (int64_t)o0 - j;
-      if (o >= 0 && (uint64_t)o < lg) acc += T[j] * (g[o] % 17u);
+// Batched tails of split products (one launch for a whole product group, blockIdx.y = job):
+// out[i] += sum_{j < lt} t[j] g[i - base - j] for i in [base, rl), out[i] for i >= ntt_len not
+// yet written (taken as 0).  16 outputs per thread: o0 = i0 - base is a multiple of 16, so the
+// g window [o0 - 16, o0 + 16) is two aligned uint4 loads when g is 16-byte aligned and in range.
+struct TailJob {
+  const uint8_t* g;
+  uint64_t lg;
+  const uint8_t* t;
+  int lt;           // <= 16
+  uint64_t base, ntt_len, rl;
+  uint8_t* out8;
+};
+constexpr int TAIL_MAX_JOBS = 8;
+struct TailJobs {
+  TailJob j[TAIL_MAX_JOBS];
+};
+
+__global__ __launch_bounds__(256) void polymul_tail_batch_kernel(TailJobs J) {
+  const TailJob& jb = J.j[blockIdx.y];
+  uint32_t T[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) T[j] = j < jb.lt ? jb.t[j] % 17u : 0u;
+  const bool al = ((uintptr_t)jb.g % 16) == 0;
+  const uint64_t span = jb.rl - jb.base;
+  for (uint64_t o0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; o0 < span;
+       o0 += (uint64_t)gridDim.x * blockDim.x * 16) {
+    uint32_t win[32];   // g[o0 - 16 + q], 0 outside [0, lg)
+    if (al && o0 >= 16 && o0 + 16 <= jb.lg) {
+      const uint4 a = *reinterpret_cast<const uint4*>(jb.g + o0 - 16);
+      const uint4 b = *reinterpret_cast<const uint4*>(jb.g + o0);
+      const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int q = 0; q < 32; q++) win[q] = (w[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 32; q++) {
+        const int64_t o = (int64_t)o0 - 16 + q;
+        win[q] = (o >= 0 && (uint64_t)o < jb.lg) ? jb.g[o] : 0u;
+      }
     }
-    out8[i] = (uint8_t)(acc % 17u);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint64_t i = jb.base + o0 + k;
+      if (o0 + k >= span) break;
+      uint32_t acc = i < jb.ntt_len ? jb.out8[i] : 0u;
+#pragma unroll
+      for (int j = 0; j < 16; j++) acc += T[j] * (win[16 + k - j] % 17u);
+      jb.out8[i] = (uint8_t)(acc % 17u);
+    }
   }
 }
+
 
 // ------------------------------------------------------------------------------ host side
 namespace {
@@ -529,7 +562,7 @@ static int log2_ceil(uint64_t v) {
 // NTT size of a product.  A result just above a power of two (la + lb - 1 = 2^K + e, e small,
 // as every prover shape n+2, 2n+3, 4n+6 at n = 2^m is) is split: the longer operand's last e
 // coefficients t are taken out, the rest times the other operand fills exactly 2^K, and
-// x^(la-e) t(x) b(x) is added by polymul_tail_kernel -- half the transform size for O(e n) MACs.
+// x^(la-e) t(x) b(x) is added by polymul_tail_batch_kernel -- half the transform size for O(e n) MACs.
 constexpr uint64_t PLK_SPLIT_MAX = 16;
 static int product_plan(uint64_t la, uint64_t lb, uint64_t* e_out) {
   const uint64_t rl = la + lb - 1;
@@ -558,7 +591,7 @@ static size_t pass_lds(int M, int C, bool center) {
 
 // m products of one transform size 2^k through the wave engine (workspace 2^(k+3) bytes each);
 // es[i] > 0: the split plan (product_plan) -- the longer operand's last es[i] coefficients are
-// multiplied in directly by polymul_tail_kernel after the transform.
+// multiplied in directly by polymul_tail_batch_kernel after the transform.
 static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, void* d_work, hipStream_t st) {
   // F29 (lazy reduction, fewer VALU per butterfly) whenever every convolution term fits it
   static int no29 = -1;
@@ -585,15 +618,24 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
   }
   int rc = plk_wave_poly_mul_batch_launch(w, m, k, use29 ? 1 : 0, ninv, st);
   if (rc) return rc;
-  for (int i = 0; i < m; i++) {
-    const uint64_t e = es ? es[i] : 0;
-    if (!e) continue;
-    const uint64_t rl = g[i].la + g[i].lb - 1, sa = w[i].la, lsh = w[i].lb;
-    const uint64_t span = rl - sa;
-    const uint64_t blocks64 = (span + 255) / 256;
-    hipLaunchKernelGGL(polymul_tail_kernel, dim3((unsigned)(blocks64 > 8192 ? 8192 : blocks64)), dim3(256), 0, st,
-                       w[i].b8, lsh, w[i].a8 + sa, (int)e, sa, sa + lsh - 1, g[i].out, rl);
-    PLK_HIP(hipGetLastError());
+  // the tails of the split products, one launch per 8
+  TailJobs tj{};
+  int nt = 0;
+  uint64_t maxspan = 0;
+  for (int i = 0; i <= m; i++) {
+    if (i < m && es && es[i]) {
+      const uint64_t rl = g[i].la + g[i].lb - 1, sa = w[i].la, lsh = w[i].lb;
+      tj.j[nt++] = TailJob{w[i].b8, lsh, w[i].a8 + sa, (int)es[i], sa, sa + lsh - 1, rl, g[i].out};
+      maxspan = std::max<uint64_t>(maxspan, rl - sa);
+    }
+    if (nt && (nt == TAIL_MAX_JOBS || i == m)) {
+      const uint64_t blocks64 = (maxspan + 16 * 256 - 1) / (16 * 256);
+      hipLaunchKernelGGL(polymul_tail_batch_kernel, dim3((unsigned)std::min<uint64_t>(blocks64, 4096), nt), dim3(256), 0,
+                         st, tj);
+      PLK_HIP(hipGetLastError());
+      nt = 0;
+      maxspan = 0;
+    }
   }
   return PLK_OK;
 }

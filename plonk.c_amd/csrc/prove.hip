@@ -171,6 +171,67 @@ __global__ __launch_bounds__(256) void lincomb16_kernel(LcArgs a, const uint8_t*
   }
 }
 
+// several independent lincombs in one launch (blockIdx.y = which), all 16-byte aligned
+constexpr int LCB_MAX = 8;
+struct LcBatch {
+  LcArgs a[LCB_MAX];
+};
+__global__ __launch_bounds__(256) void lincomb16_batch_kernel(LcBatch b, const uint8_t* __restrict__ S) {
+  const LcArgs& a = b.a[blockIdx.y];
+  uint32_t cf[LC_MAX];
+#pragma unroll
+  for (int t = 0; t < LC_MAX; t++) cf[t] = t < a.nt ? S[a.slot[t]] : 0u;
+  const uint32_t sc = S[a.scale];
+  const uint32_t c0 = a.c0 >= 0 ? S[a.c0] : 0u, c1 = a.c1 >= 0 ? S[a.c1] : 0u;
+  const uint32_t x = a.twist >= 0 ? S[a.twist] : 1u;
+  uint32_t tw[16];
+  tw[0] = 1;
+#pragma unroll
+  for (int k = 1; k < 16; k++) tw[k] = tw[k - 1] * x % HFP;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; i < a.out_len; i += stride) {
+    uint32_t acc[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) acc[k] = 0;
+    if (i == 0) { acc[0] = c0; acc[1] = c1; }
+#pragma unroll
+    for (int t = 0; t < LC_MAX; t++) {
+      if (t < a.nt && i < a.len[t]) {
+        uint32_t w[4];
+        load16(a.p[t], a.len[t], i, w);
+#pragma unroll
+        for (int k = 0; k < 16; k++) acc[k] += cf[t] * ((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+      }
+    }
+    uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      uint32_t v = acc[k] % HFP * sc % HFP;
+      if (a.twist >= 0) v = v * (x == 0 ? (i + k == 0 ? 1u : 0u) : tw[k]) % HFP;
+      o[k >> 2] |= v << (8 * (k & 3));
+    }
+    if (i + 16 <= a.out_len) {
+      *reinterpret_cast<uint4*>(a.out + i) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if (i + k < a.out_len) a.out[i + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
+    }
+  }
+}
+
+// three slices of t(x) into the commitment arena in one launch (poly_slice, src/plonk.h:513-519)
+struct Copy3 {
+  const uint8_t* src[3];
+  uint8_t* dst[3];
+  uint64_t len[3];
+};
+__global__ __launch_bounds__(256) void copy3_kernel(Copy3 c) {
+  const int s = blockIdx.y;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < c.len[s]; i += (uint64_t)gridDim.x * blockDim.x)
+    c.dst[s][i] = c.src[s][i];
+}
+
 // ------------------------------------------------------------------ poly_eval (batched)
 // Horner of src/poly.h:265-272 == sum c_i x^i mod 17; x^i = x^(i mod 16) for x != 0.
 constexpr int EV_MAX = 12;
@@ -649,6 +710,57 @@ struct Bump {
   }
 };
 
+LcArgs make_lc(std::initializer_list<std::pair<const uint8_t*, uint64_t>> terms, std::initializer_list<int> slots,
+               int c0, int c1, int scale, int twist, uint8_t* out, uint64_t out_len) {
+  LcArgs a{};
+  int t = 0;
+  for (const auto& pr : terms) {
+    if (t < LC_MAX) { a.p[t] = pr.first; a.len[t] = pr.second; }
+    t++;
+  }
+  int s = 0;
+  for (int sl : slots) {
+    if (s < LC_MAX) a.slot[s] = sl;
+    s++;
+  }
+  a.nt = t == s && t <= LC_MAX ? t : -1;
+  a.c0 = c0;
+  a.c1 = c1;
+  a.scale = scale;
+  a.twist = twist;
+  a.out = out;
+  a.out_len = out_len;
+  return a;
+}
+
+// independent lincombs: one launch when all are 16-byte aligned, else one by one
+int lincomb_batch(plk_prover* P, std::initializer_list<LcArgs> list) {
+  LcBatch b{};
+  int n = 0;
+  bool vec = true;
+  uint64_t mx = 1;
+  for (const LcArgs& a : list) {
+    if (a.nt < 0 || n >= LCB_MAX) { plk_set_error("lincomb_batch: bad terms or more than %d", LCB_MAX); return PLK_ERR_ARG; }
+    b.a[n++] = a;
+    vec = vec && ((uintptr_t)a.out % 16) == 0;
+    for (int i = 0; i < a.nt; i++) vec = vec && ((uintptr_t)a.p[i] % 16) == 0;
+    mx = std::max<uint64_t>(mx, a.out_len);
+  }
+  if (!vec) {
+    for (int i = 0; i < n; i++) {
+      const uint64_t blocks = std::min<uint64_t>((b.a[i].out_len + 255) / 256, 2048);
+      hipLaunchKernelGGL(lincomb_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, b.a[i],
+                         P->d_S);
+    }
+  } else {
+    const uint64_t blocks = std::min<uint64_t>((mx + 4095) / 4096, 2048);
+    hipLaunchKernelGGL(lincomb16_batch_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1), n), dim3(256), 0, P->st, b,
+                       P->d_S);
+  }
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
 int lincomb(plk_prover* P, std::initializer_list<std::pair<const uint8_t*, uint64_t>> terms,
             std::initializer_list<int> slots, int c0, int c1, int scale, int twist, uint8_t* out, uint64_t out_len) {
   LcArgs a{};
@@ -704,7 +816,8 @@ int pmul(plk_prover* P, const uint8_t* a, uint64_t la, const uint8_t* b, uint64_
 
 // divide num (upper-bound length nl) by Z_H; q gets ltx bytes
 int divide_zh(plk_prover* P, const uint8_t* num, uint64_t nl, uint8_t* q, uint64_t ql, uint32_t* flag) {
-  PLK_HIP(hipMemsetAsync(q, 0, ql, P->st));
+  // the binomial kernel writes every q[j < ql] whenever nl > m (one chain per residue)
+  if (P->zh_kind != 0 || nl <= P->zh_len - 1) PLK_HIP(hipMemsetAsync(q, 0, ql, P->st));
   if (P->zh_kind == 0) {
     const uint64_t m = P->zh_len - 1;
     hipLaunchKernelGGL(divide_binomial_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, P->st, num, nl, m,
@@ -769,7 +882,10 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   const Lens L = lens_for(P->n, P->zh_len);
   const uint64_t n = P->n;
   // commitments: a b c z t_lo t_mid t_hi w_z w_zw
-  P->cmax = std::max(std::max(L.la, L.lzx), std::max(std::max(n + 2, L.ltx), std::max(L.lwq, L.lwo)));
+  // committed lengths: a b c z (la, lzx), t_lo / t_mid / t_hi (poly_slice of t_x at part = n + 2:
+  // <= part, <= part, ltx - 2 part), w_z, w_zw (lwq, lwo) -- t_x itself is never committed
+  const uint64_t lthi = L.ltx > 2 * (n + 2) ? L.ltx - 2 * (n + 2) : 1;
+  P->cmax = std::max(std::max(L.la, L.lzx), std::max(std::max<uint64_t>(n + 2, lthi), std::max(L.lwq, L.lwo)));
   P->cstride = (P->cmax + 15) & ~(size_t)15;
   // poly_mul workspace: the largest batch of round 3 (rounds()), or a single product
   size_t ws = 0;
@@ -897,7 +1013,8 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   PLK_HIP(hipMemcpyAsync(P->d_S, S, NSLOT, hipMemcpyHostToDevice, P->st));
   // status: stage-A words (gate/copy/acc) are owned by the circuit path; reset the rest
   PLK_HIP(hipMemsetAsync(P->d_stat, 0, 4 * ST_GATE, P->st));
-  PLK_HIP(hipMemsetAsync(P->arena, 0, 9 * P->cstride, P->st));
+  // (the commitment arena needs no clearing: it is zeroed at plk_prover_create and every proof
+  // writes the same upper-bound ranges of its 9 slots, so the bytes past them stay zero)
   uint8_t* const cA = P->arena;
   uint8_t* const cB = cA + P->cstride;
   uint8_t* const cC = cB + P->cstride;
@@ -914,23 +1031,24 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   RC(pmul(P, dS + P_BLA, 2, P->d_zh, L.lz, P->blA));
   RC(pmul(P, dS + P_BLB, 2, P->d_zh, L.lz, P->blB));
   RC(pmul(P, dS + P_BLC, 2, P->d_zh, L.lz, P->blC));
-  RC(lincomb(P, {{P->blA, L.lz + 1}, {FA, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cA, L.la));
-  RC(lincomb(P, {{P->blB, L.lz + 1}, {FB, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cB, L.la));
-  RC(lincomb(P, {{P->blC, L.lz + 1}, {FC, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cC, L.la));
+  RC(lincomb_batch(P, {make_lc({{P->blA, L.lz + 1}, {FA, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cA, L.la),
+                        make_lc({{P->blB, L.lz + 1}, {FB, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cB, L.la),
+                        make_lc({{P->blC, L.lz + 1}, {FC, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cC, L.la)}));
   // ---- round 2: z_x = (b9 + b8 x + b7 x^2) Z_H + acc_x  (1 poly_mul)
   RC(pmul(P, dS + P_BLZ, 3, P->d_zh, L.lz, P->zB));
   RC(lincomb(P, {{P->zB, L.lz + 2}, {ACC, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cZ, L.lzx));
   // ---- round 3: t(x) numerator (12 poly_mul), src/plonk.h:386-503.  The linear factors
   // first, then the 12 products in three batches of independent ones (one launch per NTT pass
   // for a whole batch): 7 first-level products, the 3 products of those, the last 2.
-  RC(lincomb(P, {{cA, L.la}}, {S_ONE}, S_GAMMA, S_BETA, S_ALPHA, -1, P->A2, L.la));   // alpha (a + gamma + beta x)
-  RC(lincomb(P, {{cB, L.la}}, {S_ONE}, S_GAMMA, S_BK1, S_ONE, -1, P->B2, L.la));      // b + gamma + beta k1 x
-  RC(lincomb(P, {{cC, L.la}}, {S_ONE}, S_GAMMA, S_BK2, S_ONE, -1, P->C2, L.la));      // c + gamma + beta k2 x
-  RC(lincomb(P, {{cA, L.la}, {S1, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ALPHA, -1, P->A3, L.la));
-  RC(lincomb(P, {{cB, L.la}, {S2, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ONE, -1, P->B3, L.la));
-  RC(lincomb(P, {{cC, L.la}, {S3, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ONE, -1, P->C3, L.la));
-  RC(lincomb(P, {{cZ, L.lzx}}, {S_ONE}, -1, -1, S_ONE, S_OMEGA, P->ZW, L.lzw));       // z(omega x)
-  RC(lincomb(P, {{cZ, L.lzx}}, {S_ONE}, S_NEG1, -1, S_ALPHA2, -1, P->Z1, L.lz1));     // alpha^2 (z - 1)
+  RC(lincomb_batch(P, {
+      make_lc({{cA, L.la}}, {S_ONE}, S_GAMMA, S_BETA, S_ALPHA, -1, P->A2, L.la),   // alpha (a + gamma + beta x)
+      make_lc({{cB, L.la}}, {S_ONE}, S_GAMMA, S_BK1, S_ONE, -1, P->B2, L.la),      // b + gamma + beta k1 x
+      make_lc({{cC, L.la}}, {S_ONE}, S_GAMMA, S_BK2, S_ONE, -1, P->C2, L.la),      // c + gamma + beta k2 x
+      make_lc({{cA, L.la}, {S1, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ALPHA, -1, P->A3, L.la),
+      make_lc({{cB, L.la}, {S2, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ONE, -1, P->B3, L.la),
+      make_lc({{cC, L.la}, {S3, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ONE, -1, P->C3, L.la),
+      make_lc({{cZ, L.lzx}}, {S_ONE}, -1, -1, S_ONE, S_OMEGA, P->ZW, L.lzw),       // z(omega x)
+      make_lc({{cZ, L.lzx}}, {S_ONE}, S_NEG1, -1, S_ALPHA2, -1, P->Z1, L.lz1)}));  // alpha^2 (z - 1)
   {
     const PlkPolyMulJob g1[] = {{cA, L.la, cB, L.la, P->AB},      {cA, L.la, QL, n, P->AQL},
                                 {cB, L.la, QR, n, P->BQR},        {cC, L.la, QO, n, P->CQO},
@@ -952,9 +1070,13 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   const uint64_t part = n + 2;
   const uint64_t lmid = L.ltx > part ? std::min<uint64_t>(part, L.ltx - part) : 0;
   const uint64_t lhi = L.ltx > 2 * part ? L.ltx - 2 * part : 0;
-  PLK_HIP(hipMemcpyAsync(cTlo, P->TX, std::min<uint64_t>(part, L.ltx), hipMemcpyDeviceToDevice, P->st));
-  if (lmid) PLK_HIP(hipMemcpyAsync(cTmid, P->TX + part, lmid, hipMemcpyDeviceToDevice, P->st));
-  if (lhi) PLK_HIP(hipMemcpyAsync(cThi, P->TX + 2 * part, lhi, hipMemcpyDeviceToDevice, P->st));
+  {
+    const Copy3 c{{P->TX, P->TX + part, P->TX + 2 * part}, {cTlo, cTmid, cThi},
+                  {std::min<uint64_t>(part, L.ltx), lmid, lhi}};
+    const uint64_t blocks = std::min<uint64_t>((c.len[0] + 255) / 256, 2048);
+    hipLaunchKernelGGL(copy3_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1), 3), dim3(256), 0, P->st, c);
+    PLK_HIP(hipGetLastError());
+  }
   // ---- round 4: evaluations at z (src/plonk.h:527-533) and r(x)
   RC(evals(P, {{cA, L.la, S_Z, S_AZ}, {cB, L.la, S_Z, S_BZ}, {cC, L.la, S_Z, S_CZ}, {S1, n, S_Z, S_S1Z},
                {S2, n, S_Z, S_S2Z}, {P->TX, L.ltx, S_Z, S_TZ}, {P->ZW, L.lzw, S_Z, S_ZWZ}, {L1, n, S_Z, S_L1Z}}));
@@ -987,7 +1109,7 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   }
   // ---- the 9 commitments: one batched MSM over the arena (srs_eval_at_s, src/srs.h:53-68)
   const uint64_t nm = std::min<uint64_t>(P->cmax, P->srs_len);
-  PLK_HIP(hipMemsetAsync(P->d_res, 0, 9 * sizeof(PlkMsmResult), P->st));
+  // (the 9 result records are zeroed at plk_prover_create and every launch leaves them re-armed)
   if (!P->srs_irregular) {
     RC(plk_msm_batch_launch(P->d_srs, 0, P->arena, P->cstride, nm, 9, P->d_res, P->st));
   } else {
