@@ -341,6 +341,17 @@ def main():
             "GB_s": round(MSM_BYTES_PER_POINT * n * B8 / (avg8 * 1e-3) / 1e9, 1),
             "note": "8 MSMs per launch (the prover's commitments are 9 per launch)"}
         line["components"] = comp
+    if world > 1 and not args.no_components:
+        # C5 at N GPUs: replicas only (the prover's NTT work stays on one GPU) --
+        # every rank proves its own 2^20-gate instance at the same time; slowest rank reported
+        pc = prove_component(torch, hip, dev, 20, reps=3)
+        t = torch.tensor([pc["ms"]], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if rank == 0:
+            line.setdefault("components", {})["prove_2^20_gates_replicas"] = {
+                "gpus": world, "ms_slowest_rank": round(float(t.item()), 3),
+                "proofs_per_s": round(world / (float(t.item()) * 1e-3), 1),
+                "note": "one independent proof per GPU concurrently, no exchange"}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
