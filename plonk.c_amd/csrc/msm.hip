@@ -375,11 +375,19 @@ int plk_msm_upload_tables(const uint32_t* ytab, const uint8_t* exp4, const uint8
   return PLK_OK;
 }
 
-// Launch geometry.  Big MSMs use 512-thread blocks, two per CU (two 64 KB tables, 16
-// waves); small ones 256-thread blocks so they still spread over many CUs.  A batch shares
-// the chip: <= 512 blocks in total, so each block loops over its MSM's groups instead of
-// paying table fill + finish per 16 KB.  G (groups in flight per thread and iteration) is
-// the largest power of two <= min(2, groups per thread) (G = 4 measured slower).
+// Launch geometry.  Big MSMs use 512-thread blocks (two 64 KB tables per CU, 16 waves);
+// small ones 256-thread blocks so they still spread over many CUs.  Blocks per MSM:
+//   * at least enough to fill the chip once (512 resident blocks shared by the batch), at
+//     most one 16-point group per thread;
+//   * and no fewer than one block per 2 groups per thread (32 points, 64 KB of input per
+//     512-thread block -- the size of its LDS table).
+// For large batches the second bound wins and the launch runs many rounds of short blocks:
+// the chip then sweeps a few MSMs at a time instead of every block of one resident round
+// striding through all of them, and blocks that finish early take more work.  Measured at
+// 40 x 2^22 points per launch: 480 blocks 120 us, 10240 blocks 105 us (6.4 TB/s);
+// at 8 x 2^22: 25.3 -> 24.9 us; one MSM: unchanged (tools/msm_layout_lab.hip).
+// G (groups in flight per thread and iteration) is 1: with <= 2 groups per thread two
+// iterations of one group measured faster than one of two.
 // Overridable for tuning with PLK_MSM_THREADS / PLK_MSM_MAX_BLOCKS / PLK_MSM_G.
 namespace {
 int env_int(const char* name) {
@@ -398,15 +406,17 @@ void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* gpt
   const uint64_t groups = n >> 4;
   int th = groups >= 64ull * 1024 ? 512 : 256;
   if (env_threads == 256 || env_threads == 512 || env_threads == 1024) th = env_threads;
-  // two 64 KB tables per CU: 512 resident blocks fill the chip once
-  uint64_t cap = env_blocks > 0 ? (uint64_t)env_blocks : 512;
-  if (batch > 1) cap = cap / (uint64_t)batch > 1 ? cap / (uint64_t)batch : 1;
-  uint64_t b = (groups + th - 1) / th;
-  if (b > cap) b = cap;
+  uint64_t fill = env_blocks > 0 ? (uint64_t)env_blocks : 512;           // resident blocks
+  fill = fill / (uint64_t)batch > 1 ? fill / (uint64_t)batch : 1;
+  const uint64_t one_per_thread = (groups + th - 1) / th;
+  const uint64_t two_per_thread = (groups + 2 * (uint64_t)th - 1) / (2 * (uint64_t)th);
+  uint64_t b = fill < one_per_thread ? fill : one_per_thread;
+  if (env_blocks <= 0 && two_per_thread > b) b = two_per_thread;
   if (b < 1) b = 1;
+  if (b > 8ull * 65535ull) b = 8ull * 65535ull;   // the finish's per-shard ticket field is 16 bits
   const uint64_t per_thread = groups / (b * (uint64_t)th);
   int g = 1;
-  const int gmax = (env_g == 1 || env_g == 2 || env_g == 4) ? env_g : 2;
+  const int gmax = (env_g == 1 || env_g == 2 || env_g == 4) ? env_g : 1;
   while (g < gmax && (uint64_t)(2 * g) <= per_thread) g *= 2;
   *threads = th;
   *blocks = (int)b;
