@@ -46,7 +46,7 @@ namespace {
 #define PLK_NTT_RC13 3         // register bits per thread of the 2^13-tile center kernel
 #endif
 #ifndef PLK_NTT_CW13
-#define PLK_NTT_CW13 1         // waves per SIMD it must fit (tuning)
+#define PLK_NTT_CW13 8         // min waves per SIMD (launch bound): 8 = two 1024-thread blocks per CU
 #endif
 constexpr int wt_rc(int TB) { return TB == 13 ? PLK_NTT_RC13 : PLK_NTT_R12; }
 constexpr int wt_ntc(int TB) { return 1 << (TB - wt_rc(TB)); }
@@ -78,36 +78,61 @@ struct WTw {
 };
 
 // Field policies.  FBB: BabyBear, values fully reduced in [0, p).  F29: p = 7 2^26 + 1, values
-// lazy in [0, 2p) (plk_device.h): DIF butterfly 7 VALU instead of 10, DIT 9 instead of 11.
+// lazy below 4p (forward) / 8p (inverse) -- bounds in the comments of F29.
+//   dif(u, x, w, red)  : u, x <- u + x, (u - x) w;  red = u's inputs may both be >= 2p
+//   dit(u, x, w, red)  : u, x <- u + x w, u - x w;  red = u's input may be >= 6p
+//   pmul(a, b)         : pointwise product of two forward outputs
+//   colf(cl, ch)       : column factor cl * ch, fully reduced (< p)
 struct FBB {
   static constexpr int ADIC = bb::TWO_ADICITY;
-  __device__ static __forceinline__ void dif(uint32_t& u, uint32_t& x, uint32_t w) {
+  __device__ static __forceinline__ void dif(uint32_t& u, uint32_t& x, uint32_t w, bool) {
     const uint32_t a = u, b = x;
     u = bb::madd(a, b);
     x = bb::mmul(bb::msub_lazy(a, b), w);
   }
-  __device__ static __forceinline__ void dit(uint32_t& u, uint32_t& x, uint32_t w) {
+  __device__ static __forceinline__ void dit(uint32_t& u, uint32_t& x, uint32_t w, bool) {
     const uint32_t xw = bb::mmul(x, w), a = u;
     u = bb::madd(a, xw);
     x = bb::msub(a, xw);
   }
   __device__ static __forceinline__ uint32_t mul(uint32_t a, uint32_t b) { return bb::mmul(a, b); }
+  __device__ static __forceinline__ uint32_t pmul(uint32_t a, uint32_t b) { return bb::mmul(a, b); }
+  __device__ static __forceinline__ uint32_t colf(uint32_t cl, uint32_t ch) { return bb::mmul(cl, ch); }
   __device__ static __forceinline__ uint32_t from_byte(uint32_t b) { return bb::mmul(b % 17u, bb::R2); }
   __device__ static __forceinline__ uint32_t out17(uint32_t v, uint32_t ninv) { return bb::mmul(v, ninv) % 17u; }
 };
+// F29 bounds.  Montgomery REDC of t < p 2^32 lands in [0, 2p); so a product of ANY u32 with a
+// twiddle w < p is < 2p, and so is the DIF difference term t = a w + b (p - w) (= (a - b) w
+// mod p, no subtraction, for any u32 a, b: t <= max(a, b) p).  Forward: every value < 4p;
+// x outputs < 2p, so a sum of two x outputs is < 4p as it stands and only a sum of two u
+// outputs (< 8p) is reduced (one sub + min); which it is is the element's previous stage bit,
+// known at compile time inside a round (the first stage of a round reduces).  Inverse: every
+// value < 8p; outputs are a + x w and a + 2p - x w with x w < 2p, so they exceed the a operand's
+// bound by 2p and the a operand is reduced (< 8p -> < 4p) when its bound reaches 8p.
 struct F29 {
   static constexpr int ADIC = f29::TWO_ADICITY;
-  __device__ static __forceinline__ void dif(uint32_t& u, uint32_t& x, uint32_t w) {
-    const uint32_t a = u, b = x;                 // a, b < 2p
-    u = f29::red2(a + b);                        // < 4p -> < 2p
-    x = f29::mmul(a + f29::P2 - b, w);           // (0, 4p) x [0, p) -> [0, 2p)
+  __device__ static __forceinline__ uint32_t red4(uint32_t x) {   // [0, 8p) -> [0, 4p)
+    const uint32_t y = x - 2 * f29::P2;
+    return y < x ? y : x;
   }
-  __device__ static __forceinline__ void dit(uint32_t& u, uint32_t& x, uint32_t w) {
-    const uint32_t xw = f29::mmul(x, w), a = u;  // [0, 2p)
-    u = f29::red2(a + xw);
-    x = f29::red2(a + f29::P2 - xw);
+  __device__ static __forceinline__ void dif(uint32_t& u, uint32_t& x, uint32_t w, bool red) {
+    const uint32_t a = u, b = x;                 // < 4p
+    const uint64_t t = (uint64_t)a * w + (uint64_t)b * (f29::P - w);
+    const uint32_t m = (uint32_t)t * f29::PINV;
+    x = (uint32_t)((t + (uint64_t)m * f29::P) >> 32);   // < 2p
+    const uint32_t s = a + b;                    // < 8p (< 4p when both are x outputs)
+    u = red ? red4(s) : s;
+  }
+  __device__ static __forceinline__ void dit(uint32_t& u, uint32_t& x, uint32_t w, bool red) {
+    const uint32_t xw = f29::mmul(x, w);         // any u32 x: [0, 2p)
+    const uint32_t a = red ? red4(u) : u;        // a < 6p (unreduced) or < 4p
+    u = a + xw;                                  // < a's bound + 2p <= 8p
+    x = a + f29::P2 - xw;
   }
   __device__ static __forceinline__ uint32_t mul(uint32_t a, uint32_t b) { return f29::mmul(a, b); }
+  // a, b < 4p: reduce one below 2p so that a b < p 2^32
+  __device__ static __forceinline__ uint32_t pmul(uint32_t a, uint32_t b) { return f29::mmul(a, f29::red2(b)); }
+  __device__ static __forceinline__ uint32_t colf(uint32_t cl, uint32_t ch) { return f29::red1(f29::mmul(cl, ch)); }
   __device__ static __forceinline__ uint32_t from_byte(uint32_t b) { return f29::mmul(b % 17u, f29::R2); }
   __device__ static __forceinline__ uint32_t out17(uint32_t v, uint32_t ninv) {
     return f29::red1(f29::mmul(v, ninv)) % 17u;
@@ -172,8 +197,13 @@ struct Eng {
         // ds_read offset.  (A padded W13 table read at W13[rr << (12 - s)] halved the LDS but
         // needed ~4 VALU of address math per butterfly.)
         const uint32_t w = Tsm[(1u << s) + rr];
-        if (!INV) F::dif(v[k], v[k | (1 << q)], w);
-        else F::dit(v[k], v[k | (1 << q)], w);
+        // lazy-reduction flags (F29), compile-time after unrolling: DIF reduces u when the
+        // pair were u outputs of the previous stage (its bit q+1 of k is 0; unknown for a
+        // round's first stage); DIT reduces the a operand on the round's even stages (bound
+        // 8p assumed on entry, +2p per stage)
+        const bool red = INV ? (i % 2 == 0) : (i == 0 || !((k >> (q + 1)) & 1));
+        if (!INV) F::dif(v[k], v[k | (1 << q)], w, red);
+        else F::dit(v[k], v[k | (1 << q)], w, red);
       }
     }
   }
@@ -289,7 +319,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WJobs jobs, 
   for (int k = 0; k < G::E; k++) {
     const uint32_t e = bf + ((uint32_t)k << LF);
     uint32_t x = v[k];
-    if (G::HIGH) x = F::mul(x, F::mul(cl[k], ch[k]));
+    if (G::HIGH) x = F::mul(x, F::colf(cl[k], ch[k]));
     d[G::index(p, tile, e)] = x;
   }
 }
@@ -326,7 +356,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   load_pass_tw<M, G::NT>(Tsm, tw.small);
   if (G::HIGH) {
 #pragma unroll
-    for (int k = 0; k < G::E; k++) v[k] = F::mul(v[k], F::mul(cl[k], ch[k]));
+    for (int k = 0; k < G::E; k++) v[k] = F::mul(v[k], F::colf(cl[k], ch[k]));
   }
   __syncthreads();
   G::template pass<true>(v, tid, bufs, 0, Tsm);
@@ -335,25 +365,32 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
 #pragma unroll
   for (int k = 0; k < G::E; k++) {
     const uint64_t idx = G::index(p, tile, bf + ((uint32_t)k << LF));
-    if (!TO_U8) d[idx] = v[k];
-    else if (idx < out_len) out8[idx] = (uint8_t)F::out17(v[k], ninv);
+    if (!TO_U8) {
+      d[idx] = v[k];
+    } else {
+      // poly_mul runs its inverse with the FORWARD roots (no inverse table in LDS): that
+      // yields N c[-idx mod N], so the coefficient lands at the negated position
+      const uint64_t j = ((1ull << p.k) - idx) & ((1ull << p.k) - 1);
+      if (j < out_len) out8[j] = (uint8_t)F::out17(v[k], ninv);
+    }
   }
 }
 
 // Center of poly_mul: last forward pass (lo = 0) of a and b, pointwise product, first
 // inverse pass, all in registers of one block; result written over a.  The last DIF round
 // and the first DIT round both have local bits [0, R), so no exchange sits in between.
-// Stage twiddles: the forward and inverse tables T in LDS (2 x 2^TB words).
+// Stage twiddles: ONE table T in LDS (2^TB words): the inverse runs with the forward roots
+// (the DIT of the forward DFT; the final pass negates output positions, wt_inv_kernel), which
+// halves the block's LDS so that two blocks fit a CU.
 template <int TB, int R, class F>
 __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_center_kernel(WPass p, WJobs jobs,
-                                                                                                     WTw twf, WTw twi) {
+                                                                                                     WTw twf) {
   using G = Eng<TB, R, TB, F>;
   static_assert(G::NT == wt_ntc(TB), "tile block size");
   static_assert(G::lbq(G::NR - 1, false) == 0 && G::lbq(0, true) == 0, "center mapping");
-  __shared__ uint32_t Tlds[2 << TB];
+  __shared__ uint32_t Tlds[1 << TB];
   __shared__ uint32_t bufs[(G::DBUF ? 2 : 1) * G::BUF];
   const uint32_t* Tf = Tlds;
-  const uint32_t* Ti = Tlds + (1 << TB);
   uint32_t* d0 = jobs.j[blockIdx.y].A;
   const uint32_t* d1 = jobs.j[blockIdx.y].B;
   const uint32_t tid = threadIdx.x;
@@ -368,13 +405,12 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
     vb[k] = d1[idx];
   }
   load_pass_tw<TB, G::NT>(Tlds, twf.small);
-  load_pass_tw<TB, G::NT>(Tlds + (1 << TB), twi.small);
   __syncthreads();
   G::template pass<false>(va, tid, bufs, 0, Tf);
   G::template pass<false>(vb, tid, bufs, G::XCH, Tf);
 #pragma unroll
-  for (int k = 0; k < G::E; k++) va[k] = F::mul(va[k], vb[k]);
-  G::template pass<true>(va, tid, bufs, 2 * G::XCH, Ti);
+  for (int k = 0; k < G::E; k++) va[k] = F::pmul(va[k], vb[k]);
+  G::template pass<true>(va, tid, bufs, 2 * G::XCH, Tf);
   constexpr int LF = G::lbq(G::NR - 1, true);
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, true);
 #pragma unroll
@@ -482,7 +518,7 @@ int inv_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipS
 template <int TB, class F>
 int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t st) {
   const PlkTwTables t = F::ADIC == f29::TWO_ADICITY ? plk_ntt_tables29() : plk_ntt_tables();
-  const WTw twf = to_wtw(t, false), twi = to_wtw(t, true);
+  const WTw twf = to_wtw(t, false);   // forward roots for the inverse too (wt_center_kernel)
   int Ms[4];
   const int np = wave_plan(k, TB, Ms);
   int lo[4];
@@ -494,13 +530,12 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
     if (rc) return rc;
   }
   const uint32_t tiles = (uint32_t)((1ull << k) >> TB);
-  hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F>), dim3(tiles, nj), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, jobs, twf,
-                     twi);
+  hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F>), dim3(tiles, nj), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, jobs, twf);
   PLK_HIP(hipGetLastError());
   for (int i = np - 2; i >= 0; i--) {
     const WPass p{k, lo[i]};
-    rc = i == 0 ? inv_m<TB, true, F>(Ms[i], p, jobs, nj, twi, ninv, st)
-                : inv_m<TB, false, F>(Ms[i], p, jobs, nj, twi, 0u, st);
+    rc = i == 0 ? inv_m<TB, true, F>(Ms[i], p, jobs, nj, twf, ninv, st)
+                : inv_m<TB, false, F>(Ms[i], p, jobs, nj, twf, 0u, st);
     if (rc) return rc;
   }
   return PLK_OK;
