@@ -514,14 +514,31 @@ __global__ void scalars_r5_kernel(uint8_t* S) {
   S[S_W0] = (uint8_t)(c % HFP);
 }
 
+// The scalar file (challenges, constants, blinding scalars) travels as a kernel argument, and
+// the same launch clears status words [st0, st1): no pageable host->device copy (each of those
+// stalls the host ~20 us) before the first compute kernel.
+struct SlotFile {
+  uint8_t b[NSLOT];
+};
+__global__ void scalars_init_kernel(SlotFile f, uint8_t* __restrict__ S, uint32_t* __restrict__ stat, int st0,
+                                    int st1) {
+  const int t = threadIdx.x;
+  if (t < NSLOT) S[t] = f.b[t];
+  if (t >= st0 && t < st1) stat[t] = 0;
+}
+
 // 9 commitments (4-byte records from msm_finalize_kernel) + 7 evaluations -> PROOF
 // (src/plonk.h:24-41: 9 x G1 {x, y, infinite}, then a_z b_z c_z s1_z s2_z r_z z_omega_z)
+// The proof bytes and the status words go straight to mapped pinned host memory (`host`:
+// 64 proof bytes, then NSTAT words), so the call's end is one stream synchronize and no
+// device->host copies.
 __global__ void proof_pack_kernel(const uint8_t* __restrict__ g4, const uint8_t* __restrict__ S,
-                                  uint8_t* __restrict__ proof) {
+                                  const uint32_t* __restrict__ stat, uint8_t* __restrict__ host) {
   const int t = threadIdx.x;
-  if (t < 27) proof[t] = g4[4 * (t / 3) + t % 3];
+  if (t < 27) host[t] = g4[4 * (t / 3) + t % 3];
   const int ev[7] = {S_AZ, S_BZ, S_CZ, S_S1Z, S_S2Z, S_RZ, S_ZWZ};
-  if (t >= 27 && t < 34) proof[t] = S[ev[t - 27]];
+  if (t >= 27 && t < 34) host[t] = S[ev[t - 27]];
+  if (t < NSTAT) ((uint32_t*)(host + 64))[t] = stat[t];
 }
 
 // ------------------------------------------------------------------ stage A (circuit)
@@ -644,7 +661,6 @@ struct plk_prover {
   uint32_t* d_bsum = nullptr;      // scan block sums
   PlkMsmResult* d_res = nullptr;   // 9 MSM records
   uint8_t* d_g4 = nullptr;         // 9 x 4 bytes
-  uint8_t* d_proof = nullptr;
   uint8_t* arena = nullptr;        // [9][cstride] committed polynomials
   size_t cstride = 0, cmax = 0;
   uint8_t* d_polys[13] = {};       // stage-A outputs (circuit path)
@@ -657,10 +673,9 @@ struct plk_prover {
   void* work = nullptr;
   size_t work_bytes = 0;
   hipStream_t st = nullptr;
-  // host staging of async uploads (alive until the call's final stream synchronize)
-  uint8_t hS[NSLOT];
-  uint8_t hS0[NSLOT];
-  uint8_t h_om;
+  // mapped pinned host memory: 64 proof bytes + NSTAT status words (proof_pack_kernel)
+  uint8_t* h_res = nullptr;
+  uint8_t* d_res_host = nullptr;   // its device address
 };
 
 namespace {
@@ -904,7 +919,7 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
                o_hinv = B.take(P->have_circuit_tables ? n * n + 16 : 16), o_S = B.take(NSLOT),
                o_stat = B.take(4 * NSTAT), o_part = B.take(4 * EV_MAX * EV_BLOCKS),
                o_bsum = B.take(4 * ((L.lw + SCAN_B - 1) / SCAN_B + 2) + 4 * ((L.lzz + SCAN_B) / SCAN_B + 2)),
-               o_res = B.take(9 * sizeof(PlkMsmResult)), o_g4 = B.take(64), o_proof = B.take(64),
+               o_res = B.take(9 * sizeof(PlkMsmResult)), o_g4 = B.take(64),
                o_arena = B.take(9 * P->cstride);
   size_t o_polys[13];
   for (int i = 0; i < 13; i++) o_polys[i] = B.take(n + 16);
@@ -925,10 +940,16 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
     delete P;
     return PLK_ERR_NOMEM;
   }
+  if (hipHostMalloc((void**)&P->h_res, 64 + 4 * NSTAT, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&P->d_res_host, P->h_res, 0) != hipSuccess) {
+    plk_set_error("plk_prover_create: hipHostMalloc of the result buffer failed");
+    plk_prover_destroy(P);
+    return PLK_ERR_NOMEM;
+  }
   uint8_t* m = P->mem;
   P->d_srs = m + o_srs; P->d_zh = m + o_zh; P->d_h3 = m + o_h3; P->d_hinv = m + o_hinv; P->d_S = m + o_S;
   P->d_stat = (uint32_t*)(m + o_stat); P->d_part = (uint32_t*)(m + o_part); P->d_bsum = (uint32_t*)(m + o_bsum);
-  P->d_res = (PlkMsmResult*)(m + o_res); P->d_g4 = m + o_g4; P->d_proof = m + o_proof; P->arena = m + o_arena;
+  P->d_res = (PlkMsmResult*)(m + o_res); P->d_g4 = m + o_g4; P->arena = m + o_arena;
   for (int i = 0; i < 13; i++) P->d_polys[i] = m + o_polys[i];
   P->d_cir = m + o_cir; P->d_vals = m + o_vals; P->d_outs = (uint8_t**)(m + o_outs);
   for (size_t i = 0; i < sizeof(iv) / sizeof(iv[0]); i++) *iv[i].p = m + o_iv[i];
@@ -975,6 +996,7 @@ void plk_prover_destroy(plk_prover_t* P) {
   if (!P) return;
   if (P->st) (void)hipStreamSynchronize(P->st);
   (void)hipFree(P->mem);
+  if (P->h_res) (void)hipHostFree(P->h_res);
   if (P->st) (void)hipStreamDestroy(P->st);
   delete P;
 }
@@ -993,8 +1015,8 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   const uint8_t *FA = pl[0], *FB = pl[1], *FC = pl[2], *QO = pl[3], *QM = pl[4], *QL = pl[5], *QR = pl[6],
                 *QC = pl[7], *S1 = pl[8], *S2 = pl[9], *S3 = pl[10], *ACC = pl[11], *L1 = pl[12];
   // scalar file: challenges, constants and host-derivable powers (src/plonk.h:237-247)
-  uint8_t* S = P->hS;
-  memset(S, 0, NSLOT);
+  SlotFile sf{};
+  uint8_t* S = sf.b;
   const uint32_t al = chal[0] % HFP, be = chal[1] % HFP, ga = chal[2] % HFP, z = chal[3] % HFP, v = chal[4] % HFP;
   S[S_ZERO] = 0; S[S_ONE] = 1; S[S_NEG1] = 16;
   S[S_ALPHA] = al; S[S_BETA] = be; S[S_GAMMA] = ga; S[S_Z] = z; S[S_V] = v;
@@ -1010,9 +1032,9 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   S[P_BLB] = rnd[3] % HFP; S[P_BLB + 1] = rnd[2] % HFP;
   S[P_BLC] = rnd[5] % HFP; S[P_BLC + 1] = rnd[4] % HFP;
   S[P_BLZ] = rnd[8] % HFP; S[P_BLZ + 1] = rnd[7] % HFP; S[P_BLZ + 2] = rnd[6] % HFP;
-  PLK_HIP(hipMemcpyAsync(P->d_S, S, NSLOT, hipMemcpyHostToDevice, P->st));
   // status: stage-A words (gate/copy/acc) are owned by the circuit path; reset the rest
-  PLK_HIP(hipMemsetAsync(P->d_stat, 0, 4 * ST_GATE, P->st));
+  hipLaunchKernelGGL(scalars_init_kernel, dim3(1), dim3(NSLOT), 0, P->st, sf, P->d_S, P->d_stat, 0, (int)ST_GATE);
+  PLK_HIP(hipGetLastError());
   // (the commitment arena needs no clearing: it is zeroed at plk_prover_create and every proof
   // writes the same upper-bound ranges of its 9 slots, so the bytes past them stay zero)
   uint8_t* const cA = P->arena;
@@ -1117,7 +1139,7 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   }
   RC(plk_msm_finalize_launch((const uint32_t*)((const uint8_t*)P->d_res + offsetof(PlkMsmResult, log)), 9,
                              (int)(sizeof(PlkMsmResult) / 4), P->d_g4, P->st));
-  hipLaunchKernelGGL(proof_pack_kernel, dim3(1), dim3(64), 0, P->st, P->d_g4, P->d_S, P->d_proof);
+  hipLaunchKernelGGL(proof_pack_kernel, dim3(1), dim3(64), 0, P->st, P->d_g4, P->d_S, P->d_stat, P->d_res_host);
   PLK_HIP(hipGetLastError());
 #undef RC
   return PLK_OK;
@@ -1144,14 +1166,12 @@ int check_status(const plk_prover* P, const uint32_t* st, int strict, int circui
 }
 
 int finish(plk_prover* P, int strict, int circuit, uint8_t proof[34]) {
-  uint8_t hp[64];
+  PLK_HIP(hipStreamSynchronize(P->st));   // proof_pack_kernel wrote P->h_res (mapped pinned)
   uint32_t hs[NSTAT];
-  PLK_HIP(hipMemcpyAsync(hp, P->d_proof, 64, hipMemcpyDeviceToHost, P->st));
-  PLK_HIP(hipMemcpyAsync(hs, P->d_stat, sizeof hs, hipMemcpyDeviceToHost, P->st));
-  PLK_HIP(hipStreamSynchronize(P->st));
+  memcpy(hs, P->h_res + 64, sizeof hs);
   const int rc = check_status(P, hs, strict, circuit);
   if (rc) return rc;
-  if (proof) memcpy(proof, hp, 34);
+  if (proof) memcpy(proof, P->h_res, 34);
   return PLK_OK;
 }
 
@@ -1190,14 +1210,16 @@ int plk_prover_prove(plk_prover_t* P, const plk_circuit_t* c, const uint8_t chal
     if (!(i >= 5 * n && i < 11 * n)) h[i] %= HFP;   // HF values (hf_new reduces), copies stay raw
   PLK_HIP(hipMemcpyAsync(P->d_cir, h.data(), h.size(), hipMemcpyHostToDevice, P->st));
   // challenges are needed by the grand product before rounds() uploads the scalar file
-  uint8_t* S0 = P->hS0;
-  memset(S0, 0, NSLOT);
+  SlotFile sf0{};
+  uint8_t* S0 = sf0.b;
   S0[S_ONE] = 1; S0[S_NEG1] = 16;
   S0[S_ALPHA] = chal[0] % HFP; S0[S_BETA] = chal[1] % HFP; S0[S_GAMMA] = chal[2] % HFP;
   S0[S_Z] = chal[3] % HFP; S0[S_V] = chal[4] % HFP;
   S0[S_OMEGA] = 4; S0[S_K1] = 2; S0[S_K2] = 3;
-  PLK_HIP(hipMemcpyAsync(P->d_S, S0, NSLOT, hipMemcpyHostToDevice, P->st));
-  PLK_HIP(hipMemsetAsync(P->d_stat + ST_GATE, 0, 4 * (NSTAT - ST_GATE), P->st));
+  S0[S_ACCW + 1] = h_pow(4, n);   // x = omega^n for the acc_x(omega^n) == 1 check below
+  hipLaunchKernelGGL(scalars_init_kernel, dim3(1), dim3(NSLOT), 0, P->st, sf0, P->d_S, P->d_stat, (int)ST_GATE,
+                     (int)NSTAT);
+  PLK_HIP(hipGetLastError());
   // stage A: checks + sigma, 11 interpolations, grand product, acc_x and L1(x)
   for (int i = 0; i < 13; i++) PLK_HIP(hipMemsetAsync(P->d_polys[i], 0, n, P->st));
   hipLaunchKernelGGL(circuit_check_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, P->st, P->d_cir, n,
@@ -1220,8 +1242,6 @@ int plk_prover_prove(plk_prover_t* P, const plk_circuit_t* c, const uint8_t chal
   PLK_HIP(hipGetLastError());
   // acc_x(omega^n) must be 1 (src/plonk.h:366-368): evaluate into the status word
   {
-    P->h_om = h_pow(4, n);
-    PLK_HIP(hipMemcpyAsync(P->d_S + S_ACCW + 1, &P->h_om, 1, hipMemcpyHostToDevice, P->st));   // x slot
     EvArgs a{};
     a.p[0] = P->d_polys[11];
     a.len[0] = n;
