@@ -154,12 +154,15 @@ struct Eng {
   static constexpr int XCH = NR - 1;            // exchanges per pass
   static constexpr int NBUF = XCH == 0 ? 0 : (XCH > 1 && DBUF ? 2 : 1);
 
-  // DIF rounds take chunks of <= R stage bits from the top, DIT rounds from the bottom.
-  static constexpr int s_hi(int q, bool inv) {
-    return inv ? (R * q + R - 1 > M - 1 ? M - 1 : R * q + R - 1) : M - 1 - R * q;
-  }
+  // DIF rounds take chunks of <= R stage bits from the top (the short chunk last), DIT rounds
+  // from the bottom with the short chunk FIRST: either way the first and last rounds of a pass
+  // hold R full bits ending at the pass's top or starting at 0, so the column mapping applies
+  // to the global loads and stores (a short last DIT round put consecutive threads on
+  // different rows: byte stores 2^lo apart, twice the pass time at 2^21).
+  static constexpr int s_hi(int q, bool inv) { return inv ? M - 1 - R * (NR - 1 - q) : M - 1 - R * q; }
   static constexpr int s_lo(int q, bool inv) {
-    return inv ? R * q : (M - 1 - R * q - (R - 1) < 0 ? 0 : M - 1 - R * q - (R - 1));
+    return inv ? (M - R * (NR - q) < 0 ? 0 : M - R * (NR - q))
+               : (M - 1 - R * q - (R - 1) < 0 ? 0 : M - 1 - R * q - (R - 1));
   }
   static constexpr int lbq(int q, bool inv) { return s_lo(q, inv) < TB - R ? s_lo(q, inv) : TB - R; }
   // first/last round of a high-bit pass: the low thread bits index the columns, so
