@@ -42,7 +42,7 @@ enum Slot : int {
   // evaluations (round 4)
   S_AZ = 32, S_BZ, S_CZ, S_S1Z, S_S2Z, S_TZ, S_ZWZ, S_L1Z, S_RZ, S_ACCW,
   // derived from evaluations
-  S_AB = 48, S_R24, S_BZW, S_R3, S_W0, S_NEGZWZ,
+  S_AB = 48, S_R24, S_BZW, S_R3, S_W0, S_NEGZWZ, S_R3B,
   // small constant polynomials (blinding factors), 4-byte aligned
   P_BLA = 64, P_BLB = 68, P_BLC = 72, P_BLZ = 76,
   NSLOT = 128
@@ -235,7 +235,9 @@ __global__ __launch_bounds__(256) void copy3_kernel(Copy3 c) {
 // ------------------------------------------------------------------ poly_eval (batched)
 // Horner of src/poly.h:265-272 == sum c_i x^i mod 17; x^i = x^(i mod 16) for x != 0.
 constexpr int EV_MAX = 12;
-constexpr int EV_BLOCKS = 256;
+constexpr int EV_BLOCKS = 64;
+constexpr int TICK_STRIDE = 32;   // one 128-byte line per arrival word
+enum EvPost : int { EV_POST_NONE = 0, EV_POST_ACC = 1, EV_POST_R4 = 4, EV_POST_R5 = 5 };
 struct EvArgs {
   const uint8_t* p[EV_MAX];
   uint64_t len[EV_MAX];
@@ -243,10 +245,19 @@ struct EvArgs {
   int out[EV_MAX];
   int vec[EV_MAX];   // pointer 16-byte aligned: uint4 loads
   int ne;
+  int post;          // scalar program the last block runs (EvPost)
 };
 
-__global__ __launch_bounds__(256) void eval_partial_kernel(EvArgs a, const uint8_t* __restrict__ S,
-                                                           uint32_t* __restrict__ part) {
+__device__ void scalars_r4(uint8_t* S);
+__device__ void scalars_r5(uint8_t* S);
+
+// One launch per batch of evaluations: blockIdx.y = evaluation, EV_BLOCKS blocks each.  Every
+// block publishes a partial sum and takes a ticket on its evaluation's arrival word; the last
+// block of an evaluation sums the partials into S[out], re-arms the word and takes a ticket on
+// the top word; the last of those runs the round's scalar program (which reads the new
+// evaluations) -- the partial / final / scalar kernels of a three-launch chain in one.
+__global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict__ S, uint32_t* __restrict__ part,
+                                                   uint32_t* __restrict__ tick, uint32_t* __restrict__ stat) {
   const int e = blockIdx.y;
   const uint32_t x = S[a.xslot[e]];
   uint32_t pw[16];
@@ -285,15 +296,22 @@ __global__ __launch_bounds__(256) void eval_partial_kernel(EvArgs a, const uint8
     if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
     __syncthreads();
   }
-  if (threadIdx.x == 0) part[e * EV_BLOCKS + blockIdx.x] = red[0] % HFP;
-}
-
-__global__ void eval_final_kernel(EvArgs a, const uint32_t* __restrict__ part, uint8_t* __restrict__ S) {
-  const int e = threadIdx.x;
-  if (e >= a.ne) return;
-  uint32_t s = 0;
-  for (int b = 0; b < EV_BLOCKS; b++) s += part[e * EV_BLOCKS + b];
-  S[a.out[e]] = (uint8_t)(s % HFP);
+  if (threadIdx.x != 0) return;
+  part[e * EV_BLOCKS + blockIdx.x] = red[0] % HFP;
+  __threadfence();                                        // release the partial
+  if (atomicAdd(&tick[e * TICK_STRIDE], 1u) != gridDim.x - 1) return;
+  __threadfence();                                        // acquire every partial
+  uint32_t sum = 0;
+  for (int b = 0; b < (int)gridDim.x; b++) sum += part[e * EV_BLOCKS + b];
+  S[a.out[e]] = (uint8_t)(sum % HFP);
+  tick[e * TICK_STRIDE] = 0;                              // re-armed for the next launch
+  __threadfence();
+  if (atomicAdd(&tick[EV_MAX * TICK_STRIDE], 1u) != (uint32_t)a.ne - 1) return;
+  __threadfence();
+  tick[EV_MAX * TICK_STRIDE] = 0;
+  if (a.post == EV_POST_R4) scalars_r4(S);
+  if (a.post == EV_POST_R5) scalars_r5(S);
+  if (a.post == EV_POST_ACC) stat[ST_ACC] = S[S_ACCW];   // acc_x(omega^n), src/plonk.h:366-368
 }
 
 // ------------------------------------------------------------------ poly_divide
@@ -309,8 +327,23 @@ __global__ __launch_bounds__(256) void divide_binomial_kernel(const uint8_t* __r
   const uint32_t li = hinv(lead);
   const uint32_t nc = hneg(c);
   uint32_t prev = 0;   // q[j + m]
-  if (r < m && nl > m && r < ql) {
-    uint64_t j = r + ((ql - 1 - r) / m) * m;   // top of the chain
+  const uint64_t cnt = (r < m && nl > m && r < ql) ? (ql - 1 - r) / m + 1 : 0;   // chain length
+  if (cnt <= 8) {
+    // the prover's chains are ~4 long: issue every load of the chain first, then walk it
+    // (a load per step inside the loop serialised one memory latency per step)
+    uint32_t w[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) w[t] = (uint64_t)t < cnt ? num[r + (cnt - 1 - t) * m + m] : 0u;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      if ((uint64_t)t < cnt) {
+        const uint32_t v = (w[t] + nc * prev) % HFP * li % HFP;
+        q[r + (cnt - 1 - t) * m] = (uint8_t)v;
+        prev = v;
+      }
+    }
+  } else {
+    uint64_t j = r + (cnt - 1) * m;   // top of the chain
     for (;;) {
       const uint32_t v = (num[j + m] + nc * prev) % HFP * li % HFP;
       q[j] = (uint8_t)v;
@@ -331,11 +364,27 @@ __global__ __launch_bounds__(256) void divide_binomial_kernel(const uint8_t* __r
 // The prover only divides by x - z and x - z omega (d1 = 1).  Three-phase suffix scan over
 // 4096-element blocks.
 constexpr int SCAN_T = 256, SCAN_E = 16, SCAN_B = SCAN_T * SCAN_E;
+// Round 5's two divisions (by x - z and by x - z omega) are independent: one launch per phase
+// for both (blockIdx.y / the carry block = the division).
+struct LinDiv {
+  const uint8_t* num;
+  uint64_t nl;
+  int aslot;
+  int nb;              // scan blocks
+  uint8_t* q;
+  uint32_t* flag;
+  uint32_t* bsum;
+};
+struct LinDivs {
+  LinDiv d[2];
+};
 
-__global__ __launch_bounds__(SCAN_T) void lin_scan_sums_kernel(const uint8_t* __restrict__ num, uint64_t nl,
-                                                                const uint8_t* __restrict__ S, int aslot,
-                                                                uint32_t* __restrict__ bsum) {
-  const uint32_t a = S[aslot];
+__global__ __launch_bounds__(SCAN_T) void lin_scan_sums_kernel(LinDivs L, const uint8_t* __restrict__ S) {
+  const LinDiv& D = L.d[blockIdx.y];
+  if ((int)blockIdx.x >= D.nb) return;
+  const uint8_t* num = D.num;
+  const uint64_t nl = D.nl;
+  const uint32_t a = S[D.aslot];
   uint32_t pw[16];
   pw[0] = 1;
 #pragma unroll
@@ -354,11 +403,13 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_sums_kernel(const uint8_t* __
     if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
     __syncthreads();
   }
-  if (threadIdx.x == 0) bsum[blockIdx.x] = red[0] % HFP;
+  if (threadIdx.x == 0) D.bsum[blockIdx.x] = red[0] % HFP;
 }
 
-// exclusive suffix sums of the block sums (one block)
-__global__ __launch_bounds__(1024) void lin_scan_carry_kernel(uint32_t* __restrict__ bsum, int nb) {
+// exclusive suffix sums of the block sums (one block per division)
+__global__ __launch_bounds__(1024) void lin_scan_carry_kernel(LinDivs L) {
+  uint32_t* bsum = L.d[blockIdx.x].bsum;
+  const int nb = L.d[blockIdx.x].nb;
   __shared__ uint32_t t[1024];
   uint32_t carry = 0;
   for (int hi = nb; hi > 0; hi -= 1024) {
@@ -382,11 +433,13 @@ __global__ __launch_bounds__(1024) void lin_scan_carry_kernel(uint32_t* __restri
 }
 
 // divisor x - a (d1 = 1, d0 = -a): q[j] = a^-(j+1) sum_{i>j} num[i] a^i, rem = num[0] + a q[0]
-__global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(const uint8_t* __restrict__ num, uint64_t nl,
-                                                                 const uint8_t* __restrict__ S, int aslot,
-                                                                 const uint32_t* __restrict__ carry,
-                                                                 uint8_t* __restrict__ q, uint32_t* rem_flag) {
-  const uint32_t a = S[aslot];
+__global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(LinDivs L, const uint8_t* __restrict__ S) {
+  const LinDiv& D = L.d[blockIdx.y];
+  if ((int)blockIdx.x >= D.nb) return;
+  const uint8_t* num = D.num;
+  const uint64_t nl = D.nl;
+  uint8_t* q = D.q;
+  const uint32_t a = S[D.aslot];
   uint32_t pw[16], ipw[16];
   pw[0] = ipw[0] = 1;
   const uint32_t ai = hinv(a);
@@ -412,7 +465,7 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(const uint8_t* _
     __syncthreads();
   }
   // sum of w over elements after this thread's chunk
-  uint32_t run = ((int)threadIdx.x + 1 < SCAN_T ? t[threadIdx.x + 1] : 0u) + carry[blockIdx.x];
+  uint32_t run = ((int)threadIdx.x + 1 < SCAN_T ? t[threadIdx.x + 1] : 0u) + D.bsum[blockIdx.x];
   const uint64_t ql = nl - 1;
 #pragma unroll
   for (int k = SCAN_E - 1; k >= 0; k--) {
@@ -424,7 +477,7 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(const uint8_t* _
       q[j] = (uint8_t)v;
       if (j == 0) {
         const uint32_t r0 = (num[0] + a * v) % HFP;
-        if (r0) atomicOr(rem_flag, 1u);
+        if (r0) atomicOr(D.flag, 1u);
       }
     }
     run += w[k];
@@ -482,7 +535,7 @@ __global__ __launch_bounds__(256) void trim_many_kernel(TrimArgs a, uint32_t* __
 }
 
 // ------------------------------------------------------------------ scalar programs
-__global__ void scalars_r4_kernel(uint8_t* S) {
+__device__ void scalars_r4(uint8_t* S) {
   const uint32_t al = S[S_ALPHA], be = S[S_BETA], ga = S[S_GAMMA], z = S[S_Z];
   const uint32_t az = S[S_AZ], bz = S[S_BZ], cz = S[S_CZ], s1 = S[S_S1Z], s2 = S[S_S2Z];
   const uint32_t zw = S[S_ZWZ], l1 = S[S_L1Z];
@@ -499,10 +552,11 @@ __global__ void scalars_r4_kernel(uint8_t* S) {
   S[S_BZW] = (uint8_t)(be * zw % HFP);
   const uint32_t y1 = (az + be * s1 + ga) % HFP, y2 = (bz + be * s2 + ga) % HFP;
   S[S_R3] = (uint8_t)(y1 * y2 % HFP * al % HFP);
+  S[S_R3B] = (uint8_t)(S[S_R3] * S[S_BZW] % HFP);   // r_3 scale times the s_sigma_3 factor
   S[S_NEGZWZ] = (uint8_t)hneg(zw);
 }
 
-__global__ void scalars_r5_kernel(uint8_t* S) {
+__device__ void scalars_r5(uint8_t* S) {
   // constant term of w_z(x), src/plonk.h:584-603
   uint32_t c = hneg(S[S_TZ]);
   c += S[S_V] * hneg(S[S_RZ]);
@@ -527,15 +581,15 @@ __global__ void scalars_init_kernel(SlotFile f, uint8_t* __restrict__ S, uint32_
   if (t >= st0 && t < st1) stat[t] = 0;
 }
 
-// 9 commitments (4-byte records from msm_finalize_kernel) + 7 evaluations -> PROOF
+// 9 commitments (the points in the MSM result records) + 7 evaluations -> PROOF
 // (src/plonk.h:24-41: 9 x G1 {x, y, infinite}, then a_z b_z c_z s1_z s2_z r_z z_omega_z)
 // The proof bytes and the status words go straight to mapped pinned host memory (`host`:
 // 64 proof bytes, then NSTAT words), so the call's end is one stream synchronize and no
 // device->host copies.
-__global__ void proof_pack_kernel(const uint8_t* __restrict__ g4, const uint8_t* __restrict__ S,
+__global__ void proof_pack_kernel(const PlkMsmResult* __restrict__ res, const uint8_t* __restrict__ S,
                                   const uint32_t* __restrict__ stat, uint8_t* __restrict__ host) {
   const int t = threadIdx.x;
-  if (t < 27) host[t] = g4[4 * (t / 3) + t % 3];
+  if (t < 27) host[t] = res[t / 3].g1[t % 3];
   const int ev[7] = {S_AZ, S_BZ, S_CZ, S_S1Z, S_S2Z, S_RZ, S_ZWZ};
   if (t >= 27 && t < 34) host[t] = S[ev[t - 27]];
   if (t < NSTAT) ((uint32_t*)(host + 64))[t] = stat[t];
@@ -658,9 +712,9 @@ struct plk_prover {
   uint8_t* d_S = nullptr;          // scalar file
   uint32_t* d_stat = nullptr;      // status words
   uint32_t* d_part = nullptr;      // eval partials
+  uint32_t* d_tick = nullptr;      // eval arrival words (zeroed at create, re-armed by eval_kernel)
   uint32_t* d_bsum = nullptr;      // scan block sums
   PlkMsmResult* d_res = nullptr;   // 9 MSM records
-  uint8_t* d_g4 = nullptr;         // 9 x 4 bytes
   uint8_t* arena = nullptr;        // [9][cstride] committed polynomials
   size_t cstride = 0, cmax = 0;
   uint8_t* d_polys[13] = {};       // stage-A outputs (circuit path)
@@ -669,7 +723,7 @@ struct plk_prover {
   uint8_t** d_outs = nullptr;      // device array of the 13 poly pointers
   // intermediates
   uint8_t *blA, *blB, *blC, *zB, *AB, *ABQM, *AQL, *BQR, *CQO, *A2, *B2, *C2, *T2a, *T2b, *T2, *A3, *B3, *C3, *ZW,
-      *T3a, *T3b, *T3, *Z1, *T4, *NUM, *TX, *RX, *S3S, *P3, *W, *ZZ, *REMT, *ACCV, *E0;
+      *T3a, *T3b, *T3, *Z1, *T4, *NUM, *TX, *RX, *P3, *W, *ZZ, *REMT, *ACCV, *E0;
   void* work = nullptr;
   size_t work_bytes = 0;
   hipStream_t st = nullptr;
@@ -806,7 +860,7 @@ int lincomb(plk_prover* P, std::initializer_list<std::pair<const uint8_t*, uint6
   return PLK_OK;
 }
 
-int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64_t, int, int>> ev) {
+int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64_t, int, int>> ev, int post) {
   EvArgs a{};
   int e = 0;
   for (const auto& t : ev) {
@@ -818,9 +872,9 @@ int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64
     e++;
   }
   a.ne = e;
-  hipLaunchKernelGGL(eval_partial_kernel, dim3(EV_BLOCKS, e), dim3(256), 0, P->st, a, P->d_S, P->d_part);
-  PLK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(eval_final_kernel, dim3(1), dim3(64), 0, P->st, a, P->d_part, P->d_S);
+  a.post = post;
+  hipLaunchKernelGGL(eval_kernel, dim3(EV_BLOCKS, e), dim3(256), 0, P->st, a, P->d_S, P->d_part, P->d_tick,
+                     P->d_stat);
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }
@@ -846,21 +900,35 @@ int divide_zh(plk_prover* P, const uint8_t* num, uint64_t nl, uint8_t* q, uint64
   return PLK_OK;
 }
 
-// divide num by x - S[aslot]; q gets nl - 1 bytes
-int divide_linear(plk_prover* P, const uint8_t* num, uint64_t nl, int aslot, uint8_t* q, uint32_t* flag) {
-  if (nl < 2) {   // quotient [0]; remainder = num (checked by trim)
-    PLK_HIP(hipMemsetAsync(q, 0, 1, P->st));
-    return PLK_OK;
+// divide num_i by x - S[aslot_i] (i < nd <= 2); q_i gets nl_i - 1 bytes
+struct LinDivReq {
+  const uint8_t* num;
+  uint64_t nl;
+  int aslot;
+  uint8_t* q;
+  uint32_t* flag;
+};
+int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs) {
+  LinDivs L{};
+  int nd = 0, nbmax = 0;
+  uint32_t* bs = P->d_bsum;
+  for (const LinDivReq& r : reqs) {
+    if (r.nl < 2) {   // quotient [0]; remainder = num (checked by trim)
+      PLK_HIP(hipMemsetAsync(r.q, 0, 1, P->st));
+      continue;
+    }
+    const int nb = (int)((r.nl + SCAN_B - 1) / SCAN_B);
+    L.d[nd++] = LinDiv{r.num, r.nl, r.aslot, nb, r.q, r.flag, bs};
+    bs += nb + 2;
+    nbmax = std::max(nbmax, nb);
   }
-  const uint64_t nb = (nl + SCAN_B - 1) / SCAN_B;
-  hipLaunchKernelGGL(lin_scan_sums_kernel, dim3((unsigned)nb), dim3(SCAN_T), 0, P->st, num, nl, P->d_S, aslot,
-                     P->d_bsum);
+  if (!nd) return PLK_OK;
+  hipLaunchKernelGGL(lin_scan_sums_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, L, P->d_S);
   PLK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(lin_scan_carry_kernel, dim3(1), dim3(1024), 0, P->st, P->d_bsum, (int)nb);
+  hipLaunchKernelGGL(lin_scan_carry_kernel, dim3(nd), dim3(1024), 0, P->st, L);
   PLK_HIP(hipGetLastError());
   // denominators poly_new({-z, 1}) and ({-z omega, 1}), src/plonk.h:604-613
-  hipLaunchKernelGGL(lin_scan_apply_kernel, dim3((unsigned)nb), dim3(SCAN_T), 0, P->st, num, nl, P->d_S, aslot,
-                     P->d_bsum, q, flag);
+  hipLaunchKernelGGL(lin_scan_apply_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, L, P->d_S);
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }
@@ -906,7 +974,8 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   size_t ws = 0;
   const uint64_t shapes[][2] = {{2, L.lz}, {3, L.lz}, {L.lzx, n}};
   for (const auto& s : shapes) ws = std::max(ws, plk_poly_mul_workspace_bytes(s[0], s[1]));
-  const uint64_t g1[][2] = {{L.la, L.la}, {L.la, n}, {L.la, n}, {L.la, n}, {L.la, L.la}, {L.la, L.la}, {L.lz1, n}};
+  const uint64_t g1[][2] = {{L.la, L.la}, {L.la, n}, {L.la, n}, {L.la, n}, {L.la, L.la}, {L.la, L.la}, {L.lz1, n},
+                              {L.lzx, n}};
   const uint64_t g2[][2] = {{L.lab, n}, {L.l2a, L.la}, {L.l2a, L.la}};
   const uint64_t g3[][2] = {{L.l2b, L.lzx}, {L.l2b, L.lzw}};
   size_t w1 = 0, w2 = 0, w3 = 0;
@@ -917,9 +986,9 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   Bump B;
   const size_t o_srs = B.take(3 * P->srs_len + 16), o_zh = B.take(zl + 16), o_h3 = B.take(3 * n + 16),
                o_hinv = B.take(P->have_circuit_tables ? n * n + 16 : 16), o_S = B.take(NSLOT),
-               o_stat = B.take(4 * NSTAT), o_part = B.take(4 * EV_MAX * EV_BLOCKS),
+               o_stat = B.take(4 * NSTAT), o_part = B.take(4 * EV_MAX * EV_BLOCKS), o_tick = B.take(4 * TICK_STRIDE * (EV_MAX + 1)),
                o_bsum = B.take(4 * ((L.lw + SCAN_B - 1) / SCAN_B + 2) + 4 * ((L.lzz + SCAN_B) / SCAN_B + 2)),
-               o_res = B.take(9 * sizeof(PlkMsmResult)), o_g4 = B.take(64),
+               o_res = B.take(9 * sizeof(PlkMsmResult)),
                o_arena = B.take(9 * P->cstride);
   size_t o_polys[13];
   for (int i = 0; i < 13; i++) o_polys[i] = B.take(n + 16);
@@ -929,7 +998,7 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
       {&P->ABQM, L.labqm}, {&P->AQL, L.lq1}, {&P->BQR, L.lq1}, {&P->CQO, L.lq1}, {&P->A2, L.la}, {&P->B2, L.la},
       {&P->C2, L.la}, {&P->T2a, L.l2a}, {&P->T2b, L.l2b}, {&P->T2, L.l2}, {&P->A3, L.la}, {&P->B3, L.la},
       {&P->C3, L.la}, {&P->ZW, L.lzw}, {&P->T3a, L.l2a}, {&P->T3b, L.l2b}, {&P->T3, L.l3}, {&P->Z1, L.lz1},
-      {&P->T4, L.lt4}, {&P->NUM, L.lnum}, {&P->TX, L.ltx}, {&P->RX, L.lrx}, {&P->S3S, n}, {&P->P3, L.lr3},
+      {&P->T4, L.lt4}, {&P->NUM, L.lnum}, {&P->TX, L.ltx}, {&P->RX, L.lrx}, {&P->P3, L.lr3},
       {&P->W, L.lw}, {&P->ZZ, L.lzz}, {&P->REMT, L.lnum}, {&P->ACCV, n}, {&P->E0, n}};
   size_t o_iv[sizeof(iv) / sizeof(iv[0])];
   for (size_t i = 0; i < sizeof(iv) / sizeof(iv[0]); i++) o_iv[i] = B.take(iv[i].len + 16);
@@ -948,8 +1017,8 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   }
   uint8_t* m = P->mem;
   P->d_srs = m + o_srs; P->d_zh = m + o_zh; P->d_h3 = m + o_h3; P->d_hinv = m + o_hinv; P->d_S = m + o_S;
-  P->d_stat = (uint32_t*)(m + o_stat); P->d_part = (uint32_t*)(m + o_part); P->d_bsum = (uint32_t*)(m + o_bsum);
-  P->d_res = (PlkMsmResult*)(m + o_res); P->d_g4 = m + o_g4; P->arena = m + o_arena;
+  P->d_stat = (uint32_t*)(m + o_stat); P->d_part = (uint32_t*)(m + o_part); P->d_tick = (uint32_t*)(m + o_tick); P->d_bsum = (uint32_t*)(m + o_bsum);
+  P->d_res = (PlkMsmResult*)(m + o_res); P->arena = m + o_arena;
   for (int i = 0; i < 13; i++) P->d_polys[i] = m + o_polys[i];
   P->d_cir = m + o_cir; P->d_vals = m + o_vals; P->d_outs = (uint8_t**)(m + o_outs);
   for (size_t i = 0; i < sizeof(iv) / sizeof(iv[0]); i++) *iv[i].p = m + o_iv[i];
@@ -1075,8 +1144,12 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     const PlkPolyMulJob g1[] = {{cA, L.la, cB, L.la, P->AB},      {cA, L.la, QL, n, P->AQL},
                                 {cB, L.la, QR, n, P->BQR},        {cC, L.la, QO, n, P->CQO},
                                 {P->A2, L.la, P->B2, L.la, P->T2a}, {P->A3, L.la, P->B3, L.la, P->T3a},
-                                {P->Z1, L.lz1, L1, n, P->T4}};
-    RC(plk_poly_mul_batch_launch(g1, 7, P->work, P->work_bytes, P->st));
+                                {P->Z1, L.lz1, L1, n, P->T4},
+                                // the 17th poly_mul, z_x s_sigma_3 (src/plonk.h:560), as z_x * s3:
+                                // its scalar beta z_omega_z (a round-4 value) moves into r(x)'s
+                                // lincomb (S_R3B), so the product joins this batch
+                                {cZ, L.lzx, S3, n, P->P3}};
+    RC(plk_poly_mul_batch_launch(g1, 8, P->work, P->work_bytes, P->st));
     const PlkPolyMulJob g2[] = {{P->AB, L.lab, QM, n, P->ABQM}, {P->T2a, L.l2a, P->C2, L.la, P->T2b},
                                 {P->T3a, L.l2a, P->C3, L.la, P->T3b}};
     RC(plk_poly_mul_batch_launch(g2, 3, P->work, P->work_bytes, P->st));
@@ -1101,24 +1174,21 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   }
   // ---- round 4: evaluations at z (src/plonk.h:527-533) and r(x)
   RC(evals(P, {{cA, L.la, S_Z, S_AZ}, {cB, L.la, S_Z, S_BZ}, {cC, L.la, S_Z, S_CZ}, {S1, n, S_Z, S_S1Z},
-               {S2, n, S_Z, S_S2Z}, {P->TX, L.ltx, S_Z, S_TZ}, {P->ZW, L.lzw, S_Z, S_ZWZ}, {L1, n, S_Z, S_L1Z}}));
-  hipLaunchKernelGGL(scalars_r4_kernel, dim3(1), dim3(1), 0, P->st, P->d_S);
-  PLK_HIP(hipGetLastError());
-  RC(lincomb(P, {{S3, n}}, {S_BZW}, -1, -1, S_ONE, -1, P->S3S, n));   // s_sigma_3 * beta z_omega_z
-  RC(pmul(P, cZ, L.lzx, P->S3S, n, P->P3));                          // the 17th poly_mul
+               {S2, n, S_Z, S_S2Z}, {P->TX, L.ltx, S_Z, S_TZ}, {P->ZW, L.lzw, S_Z, S_ZWZ}, {L1, n, S_Z, S_L1Z}},
+           EV_POST_R4));
+  // r(x) = ... + r3 (z_x (s_sigma_3 beta z_omega_z)) = ... + (r3 beta z_omega_z) (z_x s_sigma_3)
   RC(lincomb(P, {{QM, n}, {QL, n}, {QR, n}, {QO, n}, {cZ, L.lzx}, {P->P3, L.lr3}},
-             {S_AB, S_AZ, S_BZ, S_CZ, S_R24, S_R3}, -1, -1, S_ONE, -1, P->RX, L.lrx));
-  RC(evals(P, {{P->RX, L.lrx, S_Z, S_RZ}}));
+             {S_AB, S_AZ, S_BZ, S_CZ, S_R24, S_R3B}, -1, -1, S_ONE, -1, P->RX, L.lrx));
+  RC(evals(P, {{P->RX, L.lrx, S_Z, S_RZ}}, EV_POST_R5));   // + round 5's scalar program (w_z constant)
   // ---- round 5: opening polynomials (src/plonk.h:580-621)
-  hipLaunchKernelGGL(scalars_r5_kernel, dim3(1), dim3(1), 0, P->st, P->d_S);
-  PLK_HIP(hipGetLastError());
-  RC(lincomb(P,
-             {{cTlo, std::min<uint64_t>(part, L.ltx)}, {cTmid, lmid}, {cThi, lhi}, {P->RX, L.lrx}, {cA, L.la},
-              {cB, L.la}, {cC, L.la}, {S1, n}, {S2, n}},
-             {S_ONE, S_ZN2, S_Z2N4, S_V, S_V2, S_V3, S_V4, S_V5, S_V6}, S_W0, -1, S_ONE, -1, P->W, L.lw));
-  RC(divide_linear(P, P->W, L.lw, S_Z, cWz, P->d_stat + ST_REM_W1));
-  RC(lincomb(P, {{cZ, L.lzx}}, {S_ONE}, S_NEGZWZ, -1, S_ONE, -1, P->ZZ, L.lzz));
-  RC(divide_linear(P, P->ZZ, L.lzz, S_ZOMEGA, cWzw, P->d_stat + ST_REM_W2));
+  // w_z numerator and z(x) - z_omega_z, then both divisions, each pair in one launch per phase
+  RC(lincomb_batch(P, {make_lc({{cTlo, std::min<uint64_t>(part, L.ltx)}, {cTmid, lmid}, {cThi, lhi}, {P->RX, L.lrx},
+                                {cA, L.la}, {cB, L.la}, {cC, L.la}, {S1, n}, {S2, n}},
+                               {S_ONE, S_ZN2, S_Z2N4, S_V, S_V2, S_V3, S_V4, S_V5, S_V6}, S_W0, -1, S_ONE, -1, P->W,
+                               L.lw),
+                       make_lc({{cZ, L.lzx}}, {S_ONE}, S_NEGZWZ, -1, S_ONE, -1, P->ZZ, L.lzz)}));
+  RC(divide_linear(P, {{P->W, L.lw, S_Z, cWz, P->d_stat + ST_REM_W1},
+                       {P->ZZ, L.lzz, S_ZOMEGA, cWzw, P->d_stat + ST_REM_W2}}));
   // ---- trimmed lengths for the reference's exits
   {
     TrimArgs t{};
@@ -1137,9 +1207,8 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   } else {
     for (int i = 0; i < 9; i++) RC(plk_msm_serial_launch(P->d_srs, P->arena + i * P->cstride, nm, P->d_res + i, P->st));
   }
-  RC(plk_msm_finalize_launch((const uint32_t*)((const uint8_t*)P->d_res + offsetof(PlkMsmResult, log)), 9,
-                             (int)(sizeof(PlkMsmResult) / 4), P->d_g4, P->st));
-  hipLaunchKernelGGL(proof_pack_kernel, dim3(1), dim3(64), 0, P->st, P->d_g4, P->d_S, P->d_stat, P->d_res_host);
+  // (each record's finishing block already wrote its point: no finalize launch)
+  hipLaunchKernelGGL(proof_pack_kernel, dim3(1), dim3(64), 0, P->st, P->d_res, P->d_S, P->d_stat, P->d_res_host);
   PLK_HIP(hipGetLastError());
 #undef RC
   return PLK_OK;
@@ -1240,19 +1309,12 @@ int plk_prover_prove(plk_prover_t* P, const plk_circuit_t* c, const uint8_t chal
   hipLaunchKernelGGL(interpolate_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, P->st, P->d_hinv, n,
                      P->E0, 1, P->d_outs + 12);
   PLK_HIP(hipGetLastError());
-  // acc_x(omega^n) must be 1 (src/plonk.h:366-368): evaluate into the status word
+  // acc_x(omega^n) must be 1 (src/plonk.h:366-368): evaluated straight into its status word
   {
-    EvArgs a{};
-    a.p[0] = P->d_polys[11];
-    a.len[0] = n;
-    a.xslot[0] = S_ACCW + 1;
-    a.out[0] = S_ACCW;
-    a.ne = 1;
-    hipLaunchKernelGGL(eval_partial_kernel, dim3(EV_BLOCKS, 1), dim3(256), 0, P->st, a, P->d_S, P->d_part);
-    hipLaunchKernelGGL(eval_final_kernel, dim3(1), dim3(64), 0, P->st, a, P->d_part, P->d_S);
-    PLK_HIP(hipGetLastError());
-    PLK_HIP(hipMemcpyAsync(P->d_stat + ST_ACC, P->d_S + S_ACCW, 1, hipMemcpyDeviceToDevice, P->st));
+    const int erc = evals(P, {{P->d_polys[11], n, S_ACCW + 1, S_ACCW}}, EV_POST_ACC);
+    if (erc) { (void)hipStreamSynchronize(P->st); return erc; }
   }
+
   const uint8_t* pl[13];
   for (int i = 0; i < 13; i++) pl[i] = P->d_polys[i];
   int rc = rounds(P, pl, chal, rand9);
