@@ -171,6 +171,80 @@ __global__ __launch_bounds__(256) void lincomb16_kernel(LcArgs a, const uint8_t*
   }
 }
 
+// store 16 packed coefficients at out[i..i+16) clipped to len (out 16-byte aligned)
+__device__ __forceinline__ void store16(uint8_t* out, uint64_t len, uint64_t i, const uint32_t (&o)[4]) {
+  if (i + 16 <= len) {
+    *reinterpret_cast<uint4*>(out + i) = make_uint4(o[0], o[1], o[2], o[3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      if (i + k < len) out[i + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
+  }
+}
+
+// Rounds 1-3 preparation in ONE launch (every step is elementwise up to a shift of 2):
+//   a_x = (b2 + b1 x) Z_H + f_a, b_x, c_x (src/plonk.h:280-296), z_x = (b9 + b8 x + b7 x^2) Z_H
+//   + acc_x (:371-377), then round 3's linear factors alpha (a + beta x + gamma), b + beta k1 x +
+//   gamma, c + beta k2 x + gamma, alpha (a + beta s1 + gamma), b + beta s2 + gamma, c + beta s3 +
+//   gamma, z(omega x), alpha^2 (z - 1) (:409-489).  Same bytes as the 4 blinding poly_muls and 3
+//   lincomb launches it replaces (the first kernels of a proof are host-launch bound).
+struct PrepArgs {
+  const uint8_t *zh, *fa, *fb, *fc, *acc, *s1, *s2, *s3;
+  uint64_t lz, n, la, lzx;
+  uint8_t *cA, *cB, *cC, *cZ, *A2, *B2, *C2, *A3, *B3, *C3, *ZW, *Z1;
+};
+__global__ __launch_bounds__(256) void prep_kernel(PrepArgs a, const uint8_t* __restrict__ S) {
+  const uint32_t al = S[S_ALPHA], be = S[S_BETA], ga = S[S_GAMMA], bk1 = S[S_BK1], bk2 = S[S_BK2];
+  const uint32_t al2 = S[S_ALPHA2], om = S[S_OMEGA];
+  const uint32_t ba0 = S[P_BLA], ba1 = S[P_BLA + 1], bb0 = S[P_BLB], bb1 = S[P_BLB + 1], bc0 = S[P_BLC],
+                 bc1 = S[P_BLC + 1], bz0 = S[P_BLZ], bz1 = S[P_BLZ + 1], bz2 = S[P_BLZ + 2];
+  uint32_t tw[16];   // omega^k; omega^i = 1 for i = 0 mod 16 (omega != 0)
+  tw[0] = 1;
+#pragma unroll
+  for (int k = 1; k < 16; k++) tw[k] = tw[k - 1] * om % HFP;
+  const uint64_t top = a.la > a.lzx ? a.la : a.lzx;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; i < top; i += stride) {
+    uint32_t z[18];   // z[k + 2] = Z_H[i + k] mod 17, k = -2 .. 15 (zero outside [0, lz))
+    {
+      uint32_t w[4];
+      load16(a.zh, a.lz, i, w);
+#pragma unroll
+      for (int k = 0; k < 16; k++) z[k + 2] = ((w[k >> 2] >> (8 * (k & 3))) & 0xFFu) % HFP;
+      z[0] = (i >= 2 && i - 2 < a.lz) ? a.zh[i - 2] % HFP : 0u;
+      z[1] = (i >= 1 && i - 1 < a.lz) ? a.zh[i - 1] % HFP : 0u;
+    }
+    uint32_t fa[4], fb[4], fc[4], fz[4], f1[4], f2[4], f3[4];
+    load16(a.fa, a.n, i, fa); load16(a.fb, a.n, i, fb); load16(a.fc, a.n, i, fc); load16(a.acc, a.n, i, fz);
+    load16(a.s1, a.n, i, f1); load16(a.s2, a.n, i, f2); load16(a.s3, a.n, i, f3);
+    uint32_t oA[4] = {}, oB[4] = {}, oC[4] = {}, oZ[4] = {}, oA2[4] = {}, oB2[4] = {}, oC2[4] = {}, oA3[4] = {},
+             oB3[4] = {}, oC3[4] = {}, oZW[4] = {}, oZ1[4] = {};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int wd = k >> 2, sh = 8 * (k & 3);
+      auto byte = [&](const uint32_t (&f)[4]) { return (f[wd] >> sh) & 0xFFu; };
+      const uint32_t c0 = (i + k == 0), c1 = (i + k == 1);
+      const uint32_t va = (ba0 * z[k + 2] + ba1 * z[k + 1] + byte(fa)) % HFP;
+      const uint32_t vb = (bb0 * z[k + 2] + bb1 * z[k + 1] + byte(fb)) % HFP;
+      const uint32_t vc = (bc0 * z[k + 2] + bc1 * z[k + 1] + byte(fc)) % HFP;
+      const uint32_t vz = (bz0 * z[k + 2] + bz1 * z[k + 1] + bz2 * z[k] + byte(fz)) % HFP;
+      oA[wd] |= va << sh; oB[wd] |= vb << sh; oC[wd] |= vc << sh; oZ[wd] |= vz << sh;
+      oA2[wd] |= (va + c0 * ga + c1 * be) % HFP * al % HFP << sh;
+      oB2[wd] |= (vb + c0 * ga + c1 * bk1) % HFP << sh;
+      oC2[wd] |= (vc + c0 * ga + c1 * bk2) % HFP << sh;
+      oA3[wd] |= (va + be * byte(f1) + c0 * ga) % HFP * al % HFP << sh;
+      oB3[wd] |= (vb + be * byte(f2) + c0 * ga) % HFP << sh;
+      oC3[wd] |= (vc + be * byte(f3) + c0 * ga) % HFP << sh;
+      oZW[wd] |= vz * (om == 0 ? c0 : tw[k]) % HFP << sh;
+      oZ1[wd] |= (vz + c0 * 16u) % HFP * al2 % HFP << sh;
+    }
+    store16(a.cA, a.la, i, oA); store16(a.cB, a.la, i, oB); store16(a.cC, a.la, i, oC);
+    store16(a.A2, a.la, i, oA2); store16(a.B2, a.la, i, oB2); store16(a.C2, a.la, i, oC2);
+    store16(a.A3, a.la, i, oA3); store16(a.B3, a.la, i, oB3); store16(a.C3, a.la, i, oC3);
+    store16(a.cZ, a.lzx, i, oZ); store16(a.ZW, a.lzx, i, oZW); store16(a.Z1, a.lzx, i, oZ1);
+  }
+}
+
 // several independent lincombs in one launch (blockIdx.y = which), all 16-byte aligned
 constexpr int LCB_MAX = 8;
 struct LcBatch {
@@ -234,8 +308,8 @@ __global__ __launch_bounds__(256) void copy3_kernel(Copy3 c) {
 
 // ------------------------------------------------------------------ poly_eval (batched)
 // Horner of src/poly.h:265-272 == sum c_i x^i mod 17; x^i = x^(i mod 16) for x != 0.
-constexpr int EV_MAX = 12;
-constexpr int EV_BLOCKS = 64;
+constexpr int EV_MAX = 12;   // 5-bit values of all of them fit the top arrival word (bits 0-59)
+constexpr int EV_BLOCKS = 256;
 constexpr int TICK_STRIDE = 32;   // one 128-byte line per arrival word
 enum EvPost : int { EV_POST_NONE = 0, EV_POST_ACC = 1, EV_POST_R4 = 4, EV_POST_R5 = 5 };
 struct EvArgs {
@@ -252,12 +326,12 @@ __device__ void scalars_r4(uint8_t* S);
 __device__ void scalars_r5(uint8_t* S);
 
 // One launch per batch of evaluations: blockIdx.y = evaluation, EV_BLOCKS blocks each.  Every
-// block publishes a partial sum and takes a ticket on its evaluation's arrival word; the last
-// block of an evaluation sums the partials into S[out], re-arms the word and takes a ticket on
-// the top word; the last of those runs the round's scalar program (which reads the new
-// evaluations) -- the partial / final / scalar kernels of a three-launch chain in one.
-__global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict__ S, uint32_t* __restrict__ part,
-                                                   uint32_t* __restrict__ tick, uint32_t* __restrict__ stat) {
+// block adds its partial sum with a ticket to its evaluation's arrival word; the last block of
+// an evaluation adds the finished value with a ticket to the top word; the last of those writes
+// every S[out] and runs the round's scalar program -- the partial / final / scalar kernels of a
+// three-launch chain in one.
+__global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict__ S, uint32_t* __restrict__ tick,
+                                                   uint32_t* __restrict__ stat) {
   const int e = blockIdx.y;
   const uint32_t x = S[a.xslot[e]];
   uint32_t pw[16];
@@ -297,18 +371,21 @@ __global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict
     __syncthreads();
   }
   if (threadIdx.x != 0) return;
-  part[e * EV_BLOCKS + blockIdx.x] = red[0] % HFP;
-  __threadfence();                                        // release the partial
-  if (atomicAdd(&tick[e * TICK_STRIDE], 1u) != gridDim.x - 1) return;
-  __threadfence();                                        // acquire every partial
-  uint32_t sum = 0;
-  for (int b = 0; b < (int)gridDim.x; b++) sum += part[e * EV_BLOCKS + b];
-  S[a.out[e]] = (uint8_t)(sum % HFP);
-  tick[e * TICK_STRIDE] = 0;                              // re-armed for the next launch
-  __threadfence();
-  if (atomicAdd(&tick[EV_MAX * TICK_STRIDE], 1u) != (uint32_t)a.ne - 1) return;
-  __threadfence();
-  tick[EV_MAX * TICK_STRIDE] = 0;
+  // the partial travels inside the atomic (no fence: a device-scope release per block costs an
+  // L2 writeback each, 2048 of them took 60 us): row word = sum | arrivals << 32; the row's
+  // last block adds its value (5 bits at 5 e) into the top word, arrivals at bit 60
+  const uint32_t mine = red[0] % HFP;
+  unsigned long long* row = reinterpret_cast<unsigned long long*>(tick) + e * (TICK_STRIDE / 2);
+  const unsigned long long old = atomicAdd(row, (unsigned long long)mine | (1ull << 32));
+  if ((uint32_t)(old >> 32) != gridDim.x - 1) return;
+  *row = 0;                                               // re-armed for the next launch
+  const unsigned long long v = ((uint32_t)old + mine) % HFP;
+  unsigned long long* topw = reinterpret_cast<unsigned long long*>(tick) + EV_MAX * (TICK_STRIDE / 2);
+  const unsigned long long told = atomicAdd(topw, (v << (5 * e)) | (1ull << 60));
+  if ((int)(told >> 60) != a.ne - 1) return;
+  *topw = 0;
+  const unsigned long long all = told + ((v << (5 * e)) | (1ull << 60));
+  for (int r = 0; r < a.ne; r++) S[a.out[r]] = (uint8_t)((all >> (5 * r)) & 31u);
   if (a.post == EV_POST_R4) scalars_r4(S);
   if (a.post == EV_POST_R5) scalars_r5(S);
   if (a.post == EV_POST_ACC) stat[ST_ACC] = S[S_ACCW];   // acc_x(omega^n), src/plonk.h:366-368
@@ -357,6 +434,74 @@ __global__ __launch_bounds__(256) void divide_binomial_kernel(const uint8_t* __r
   // (same-address atomics from every wave serialise in one L2 channel)
   if (__syncthreads_or(rv != 0) && threadIdx.x == 0 && __hip_atomic_load(rem_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
     atomicOr(rem_flag, 1u);
+}
+
+// The same with 4 consecutive residues per thread (m % 4 == 0, num / q 4-byte aligned): one
+// dword per chain element, loaded before the chains are walked.  Lanes of a residue whose chain
+// is one shorter than its word's first residue skip the word's top element (and do not store it).
+// cq, cr: ql - 1 = cq m + cr (host-side), so a chain has cq + 1 elements for r <= cr and cq
+// after (no 64-bit division on the device: a software routine of ~100 instructions per call)
+__global__ __launch_bounds__(256) void divide_binomial4_kernel(const uint8_t* __restrict__ num, uint64_t nl,
+                                                               uint64_t m, uint32_t lead, uint32_t c,
+                                                               uint8_t* __restrict__ q, uint64_t ql, uint64_t cq,
+                                                               uint64_t cr, uint8_t* __restrict__ rem_part) {
+  const uint64_t r0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const uint32_t li = hinv(lead);
+  const uint32_t nc = hneg(c);
+  auto chain = [&](uint64_t r) -> uint64_t { return (r < m && nl > m && r < ql) ? (r <= cr ? cq + 1 : cq) : 0; };
+  const uint64_t cnt0 = chain(r0);   // the longest of the 4 (chain length falls with r)
+  uint32_t rv = 0;
+  if (cnt0 <= 8) {
+    uint32_t w[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      w[k] = (uint64_t)k < cnt0 ? *reinterpret_cast<const uint32_t*>(num + r0 + (cnt0 - 1 - k) * m + m) : 0u;
+    uint32_t prev[4] = {0, 0, 0, 0}, skip[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) skip[b] = (uint32_t)(cnt0 - chain(r0 + b));   // 0 or 1 (or cnt0 past the end)
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if ((uint64_t)k < cnt0) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          if ((uint32_t)k >= skip[b]) {
+            const uint32_t v = (((w[k] >> (8 * b)) & 0xFFu) + nc * prev[b]) % HFP * li % HFP;
+            prev[b] = v;
+            o |= v << (8 * b);
+          }
+        }
+        uint8_t* dst = q + r0 + (cnt0 - 1 - k) * m;
+        if (skip[0] == 0 && skip[3] == 0) *reinterpret_cast<uint32_t*>(dst) = o;
+        else
+#pragma unroll
+          for (int b = 0; b < 4; b++)
+            if ((uint32_t)k >= skip[b]) dst[b] = (uint8_t)(o >> (8 * b));
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint64_t r = r0 + b;
+      if (r < m && r < nl && (num[r] + nc * prev[b]) % HFP) rv = 1;   // prev = q[r] (0 if none)
+    }
+  } else {
+    for (int b = 0; b < 4; b++) {
+      const uint64_t r = r0 + b;
+      const uint64_t cnt = chain(r);
+      uint32_t prev = 0;
+      for (uint64_t t = 0; t < cnt; t++) {
+        const uint64_t j = r + (cnt - 1 - t) * m;
+        const uint32_t v = (num[j + m] + nc * prev) % HFP * li % HFP;
+        q[j] = (uint8_t)v;
+        prev = v;
+      }
+      if (r < m && r < nl && (num[r] + nc * prev) % HFP) rv = 1;
+    }
+  }
+  // one vote byte per block (trim_many_kernel ORs them into the status word): the blocks run
+  // together, so a "skip if already set" atomic would still serialise ~1000 same-address ORs
+  const int vote = __syncthreads_or(rv != 0);
+  if (threadIdx.x == 0) rem_part[blockIdx.x] = vote ? 1 : 0;
 }
 
 // (b) divisor d1 x + d0: the long division gives q[j] = b num[j+1] + a q[j+1] with
@@ -508,10 +653,12 @@ __global__ __launch_bounds__(256) void divide_general_kernel(const uint8_t* __re
 
 // ------------------------------------------------------------------ trimmed lengths
 // one block per buffer: index + 1 of the last non-zero byte, at least 1 (src/poly.h:20-24)
+// dst | TRIM_ANY: write 1 to the word if any byte is non-zero (a flag), leave it otherwise
+constexpr int TRIM_ANY = 1 << 16;
 struct TrimArgs {
-  const uint8_t* p[10];
-  uint64_t len[10];
-  int dst[10];
+  const uint8_t* p[11];
+  uint64_t len[11];
+  int dst[11];
 };
 __global__ __launch_bounds__(256) void trim_many_kernel(TrimArgs a, uint32_t* __restrict__ stat) {
   const uint8_t* p = a.p[blockIdx.x];
@@ -531,7 +678,13 @@ __global__ __launch_bounds__(256) void trim_many_kernel(TrimArgs a, uint32_t* __
     if (b) break;
     hi = lo;
   }
-  if (threadIdx.x == 0) stat[a.dst[blockIdx.x]] = best ? best : 1u;
+  if (threadIdx.x != 0) return;
+  const int d = a.dst[blockIdx.x];
+  if (d & TRIM_ANY) {
+    if (best) stat[d & ~TRIM_ANY] = 1u;
+  } else {
+    stat[d] = best ? best : 1u;
+  }
 }
 
 // ------------------------------------------------------------------ scalar programs
@@ -711,8 +864,9 @@ struct plk_prover {
   uint8_t *d_srs = nullptr, *d_zh = nullptr, *d_h3 = nullptr, *d_hinv = nullptr;
   uint8_t* d_S = nullptr;          // scalar file
   uint32_t* d_stat = nullptr;      // status words
-  uint32_t* d_part = nullptr;      // eval partials
   uint32_t* d_tick = nullptr;      // eval arrival words (zeroed at create, re-armed by eval_kernel)
+  uint8_t* d_rem = nullptr;        // Z_H division: one remainder vote per block
+  uint64_t rem_blocks = 0;
   uint32_t* d_bsum = nullptr;      // scan block sums
   PlkMsmResult* d_res = nullptr;   // 9 MSM records
   uint8_t* arena = nullptr;        // [9][cstride] committed polynomials
@@ -873,8 +1027,7 @@ int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64
   }
   a.ne = e;
   a.post = post;
-  hipLaunchKernelGGL(eval_kernel, dim3(EV_BLOCKS, e), dim3(256), 0, P->st, a, P->d_S, P->d_part, P->d_tick,
-                     P->d_stat);
+  hipLaunchKernelGGL(eval_kernel, dim3(EV_BLOCKS, e), dim3(256), 0, P->st, a, P->d_S, P->d_tick, P->d_stat);
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }
@@ -887,10 +1040,18 @@ int pmul(plk_prover* P, const uint8_t* a, uint64_t la, const uint8_t* b, uint64_
 int divide_zh(plk_prover* P, const uint8_t* num, uint64_t nl, uint8_t* q, uint64_t ql, uint32_t* flag) {
   // the binomial kernel writes every q[j < ql] whenever nl > m (one chain per residue)
   if (P->zh_kind != 0 || nl <= P->zh_len - 1) PLK_HIP(hipMemsetAsync(q, 0, ql, P->st));
+  P->rem_blocks = 0;
   if (P->zh_kind == 0) {
     const uint64_t m = P->zh_len - 1;
-    hipLaunchKernelGGL(divide_binomial_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, P->st, num, nl, m,
-                       P->zh_lead, P->zh_c, q, ql, flag);
+    if (m % 4 == 0 && (uintptr_t)num % 4 == 0 && (uintptr_t)q % 4 == 0 && flag == P->d_stat + ST_REM_T) {
+      const uint64_t nb = (m / 4 + 255) / 256;
+      hipLaunchKernelGGL(divide_binomial4_kernel, dim3((unsigned)nb), dim3(256), 0, P->st, num, nl, m, P->zh_lead,
+                         P->zh_c, q, ql, ql ? (ql - 1) / m : 0, ql ? (ql - 1) % m : 0, P->d_rem);
+      P->rem_blocks = nb;   // trim_many_kernel folds the votes into *flag (ST_REM_T)
+    } else {
+      hipLaunchKernelGGL(divide_binomial_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, P->st, num, nl, m,
+                         P->zh_lead, P->zh_c, q, ql, flag);
+    }
   } else {
     if (nl > (1u << 20)) { plk_set_error("poly_divide: non-binomial Z_H with %llu coefficients", (unsigned long long)nl); return PLK_ERR_RANGE; }
     hipLaunchKernelGGL(divide_general_kernel, dim3(1), dim3(256), 0, P->st, num, nl, P->d_zh, (uint64_t)P->zh_len,
@@ -986,7 +1147,8 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   Bump B;
   const size_t o_srs = B.take(3 * P->srs_len + 16), o_zh = B.take(zl + 16), o_h3 = B.take(3 * n + 16),
                o_hinv = B.take(P->have_circuit_tables ? n * n + 16 : 16), o_S = B.take(NSLOT),
-               o_stat = B.take(4 * NSTAT), o_part = B.take(4 * EV_MAX * EV_BLOCKS), o_tick = B.take(4 * TICK_STRIDE * (EV_MAX + 1)),
+               o_stat = B.take(4 * NSTAT), o_tick = B.take(4 * TICK_STRIDE * (EV_MAX + 1)),
+               o_rem = B.take(P->zh_len / 1024 + 64),
                o_bsum = B.take(4 * ((L.lw + SCAN_B - 1) / SCAN_B + 2) + 4 * ((L.lzz + SCAN_B) / SCAN_B + 2)),
                o_res = B.take(9 * sizeof(PlkMsmResult)),
                o_arena = B.take(9 * P->cstride);
@@ -1017,7 +1179,7 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   }
   uint8_t* m = P->mem;
   P->d_srs = m + o_srs; P->d_zh = m + o_zh; P->d_h3 = m + o_h3; P->d_hinv = m + o_hinv; P->d_S = m + o_S;
-  P->d_stat = (uint32_t*)(m + o_stat); P->d_part = (uint32_t*)(m + o_part); P->d_tick = (uint32_t*)(m + o_tick); P->d_bsum = (uint32_t*)(m + o_bsum);
+  P->d_stat = (uint32_t*)(m + o_stat); P->d_tick = (uint32_t*)(m + o_tick); P->d_rem = m + o_rem; P->d_bsum = (uint32_t*)(m + o_bsum);
   P->d_res = (PlkMsmResult*)(m + o_res); P->arena = m + o_arena;
   for (int i = 0; i < 13; i++) P->d_polys[i] = m + o_polys[i];
   P->d_cir = m + o_cir; P->d_vals = m + o_vals; P->d_outs = (uint8_t**)(m + o_outs);
@@ -1118,28 +1280,40 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   const uint8_t* dS = P->d_S;
   int rc;
 #define RC(x) do { if ((rc = (x))) return rc; } while (0)
-  // ---- round 1: a_x = (b2 + b1 x) Z_H + f_a, ...  (3 poly_mul)
-  RC(pmul(P, dS + P_BLA, 2, P->d_zh, L.lz, P->blA));
-  RC(pmul(P, dS + P_BLB, 2, P->d_zh, L.lz, P->blB));
-  RC(pmul(P, dS + P_BLC, 2, P->d_zh, L.lz, P->blC));
-  RC(lincomb_batch(P, {make_lc({{P->blA, L.lz + 1}, {FA, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cA, L.la),
-                        make_lc({{P->blB, L.lz + 1}, {FB, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cB, L.la),
-                        make_lc({{P->blC, L.lz + 1}, {FC, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cC, L.la)}));
-  // ---- round 2: z_x = (b9 + b8 x + b7 x^2) Z_H + acc_x  (1 poly_mul)
-  RC(pmul(P, dS + P_BLZ, 3, P->d_zh, L.lz, P->zB));
-  RC(lincomb(P, {{P->zB, L.lz + 2}, {ACC, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cZ, L.lzx));
-  // ---- round 3: t(x) numerator (12 poly_mul), src/plonk.h:386-503.  The linear factors
-  // first, then the 12 products in three batches of independent ones (one launch per NTT pass
-  // for a whole batch): 7 first-level products, the 3 products of those, the last 2.
-  RC(lincomb_batch(P, {
-      make_lc({{cA, L.la}}, {S_ONE}, S_GAMMA, S_BETA, S_ALPHA, -1, P->A2, L.la),   // alpha (a + gamma + beta x)
-      make_lc({{cB, L.la}}, {S_ONE}, S_GAMMA, S_BK1, S_ONE, -1, P->B2, L.la),      // b + gamma + beta k1 x
-      make_lc({{cC, L.la}}, {S_ONE}, S_GAMMA, S_BK2, S_ONE, -1, P->C2, L.la),      // c + gamma + beta k2 x
-      make_lc({{cA, L.la}, {S1, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ALPHA, -1, P->A3, L.la),
-      make_lc({{cB, L.la}, {S2, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ONE, -1, P->B3, L.la),
-      make_lc({{cC, L.la}, {S3, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ONE, -1, P->C3, L.la),
-      make_lc({{cZ, L.lzx}}, {S_ONE}, -1, -1, S_ONE, S_OMEGA, P->ZW, L.lzw),       // z(omega x)
-      make_lc({{cZ, L.lzx}}, {S_ONE}, S_NEG1, -1, S_ALPHA2, -1, P->Z1, L.lz1)}));  // alpha^2 (z - 1)
+  // ---- rounds 1-2 (a_x b_x c_x z_x) and round 3's linear factors, src/plonk.h:280-489
+  const uint8_t* ins[8] = {P->d_zh, FA, FB, FC, ACC, S1, S2, S3};
+  bool aligned = true;
+  for (const uint8_t* q : ins) aligned = aligned && ((uintptr_t)q % 16) == 0;
+  if (aligned && L.la <= L.lzx && L.lzx <= L.la + 1) {
+    const PrepArgs pa{P->d_zh, FA, FB, FC, ACC, S1, S2, S3, L.lz, n, L.la, L.lzx,
+                      cA, cB, cC, cZ, P->A2, P->B2, P->C2, P->A3, P->B3, P->C3, P->ZW, P->Z1};
+    const uint64_t blocks = std::min<uint64_t>((L.lzx + 4095) / 4096, 2048);
+    hipLaunchKernelGGL(prep_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, pa, dS);
+    PLK_HIP(hipGetLastError());
+  } else {
+    // ---- round 1: a_x = (b2 + b1 x) Z_H + f_a, ...  (3 poly_mul)
+    RC(pmul(P, dS + P_BLA, 2, P->d_zh, L.lz, P->blA));
+    RC(pmul(P, dS + P_BLB, 2, P->d_zh, L.lz, P->blB));
+    RC(pmul(P, dS + P_BLC, 2, P->d_zh, L.lz, P->blC));
+    RC(lincomb_batch(P, {make_lc({{P->blA, L.lz + 1}, {FA, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cA, L.la),
+                          make_lc({{P->blB, L.lz + 1}, {FB, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cB, L.la),
+                          make_lc({{P->blC, L.lz + 1}, {FC, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cC, L.la)}));
+    // ---- round 2: z_x = (b9 + b8 x + b7 x^2) Z_H + acc_x  (1 poly_mul)
+    RC(pmul(P, dS + P_BLZ, 3, P->d_zh, L.lz, P->zB));
+    RC(lincomb(P, {{P->zB, L.lz + 2}, {ACC, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cZ, L.lzx));
+    // ---- round 3: t(x) numerator (12 poly_mul), src/plonk.h:386-503.  The linear factors
+    // first, then the 12 products in three batches of independent ones (one launch per NTT pass
+    // for a whole batch): 7 first-level products, the 3 products of those, the last 2.
+    RC(lincomb_batch(P, {
+        make_lc({{cA, L.la}}, {S_ONE}, S_GAMMA, S_BETA, S_ALPHA, -1, P->A2, L.la),   // alpha (a + gamma + beta x)
+        make_lc({{cB, L.la}}, {S_ONE}, S_GAMMA, S_BK1, S_ONE, -1, P->B2, L.la),      // b + gamma + beta k1 x
+        make_lc({{cC, L.la}}, {S_ONE}, S_GAMMA, S_BK2, S_ONE, -1, P->C2, L.la),      // c + gamma + beta k2 x
+        make_lc({{cA, L.la}, {S1, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ALPHA, -1, P->A3, L.la),
+        make_lc({{cB, L.la}, {S2, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ONE, -1, P->B3, L.la),
+        make_lc({{cC, L.la}, {S3, n}}, {S_ONE, S_BETA}, S_GAMMA, -1, S_ONE, -1, P->C3, L.la),
+        make_lc({{cZ, L.lzx}}, {S_ONE}, -1, -1, S_ONE, S_OMEGA, P->ZW, L.lzw),       // z(omega x)
+        make_lc({{cZ, L.lzx}}, {S_ONE}, S_NEG1, -1, S_ALPHA2, -1, P->Z1, L.lz1)}));  // alpha^2 (z - 1)
+  }
   {
     const PlkPolyMulJob g1[] = {{cA, L.la, cB, L.la, P->AB},      {cA, L.la, QL, n, P->AQL},
                                 {cB, L.la, QR, n, P->BQR},        {cC, L.la, QO, n, P->CQO},
@@ -1196,7 +1370,9 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     const uint64_t ub[9] = {L.la, L.la, L.la, L.lzx, std::min<uint64_t>(part, L.ltx), lmid, lhi, L.lwq, L.lwo};
     for (int i = 0; i < 9; i++) { t.p[i] = cps[i]; t.len[i] = std::max<uint64_t>(ub[i], 1); t.dst[i] = ST_LEN0 + i; }
     t.p[9] = P->TX; t.len[9] = L.ltx; t.dst[9] = ST_TXLEN;
-    hipLaunchKernelGGL(trim_many_kernel, dim3(10), dim3(256), 0, P->st, t, P->d_stat);
+    int nt = 10;
+    if (P->rem_blocks) { t.p[10] = P->d_rem; t.len[10] = P->rem_blocks; t.dst[10] = ST_REM_T | TRIM_ANY; nt = 11; }
+    hipLaunchKernelGGL(trim_many_kernel, dim3(nt), dim3(256), 0, P->st, t, P->d_stat);
     PLK_HIP(hipGetLastError());
   }
   // ---- the 9 commitments: one batched MSM over the arena (srs_eval_at_s, src/srs.h:53-68)
