@@ -541,7 +541,7 @@ int plk_ntt_init_tables(void) {
   if ((rc = up(&g_tw.d_small_f, sf)) || (rc = up(&g_tw.d_small_i, si)) || (rc = up(&g_tw.d_lo_f, lf)) ||
       (rc = up(&g_tw.d_hi_f, hf)) || (rc = up(&g_tw.d_lo_i, li)) || (rc = up(&g_tw.d_hi_i, hi_)))
     return rc;
-  return PLK_OK;
+  return plk_wave_init_coltabs();
 }
 
 void plk_ntt_free_tables(void) {
@@ -551,6 +551,7 @@ void plk_ntt_free_tables(void) {
   (void)hipFree(g_tw29.d_hi_f); (void)hipFree(g_tw29.d_lo_i); (void)hipFree(g_tw29.d_hi_i);
   g_tw29.d_small_f = g_tw29.d_small_i = g_tw29.d_lo_f = g_tw29.d_hi_f = g_tw29.d_lo_i = g_tw29.d_hi_i = nullptr;
   g_tw = TwHost{};
+  plk_wave_free_coltabs();
 }
 
 static int log2_ceil(uint64_t v) {

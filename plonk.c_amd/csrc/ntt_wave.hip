@@ -75,6 +75,8 @@ struct WTw {
   const uint32_t* small;   // T[2^j + r] = w_{2^(j+1)}^r (Montgomery), 2^PLK_NTT_SMALL_LOG entries
   const uint32_t* lo;      // w_{2^ADIC}^i, i < 4096 (ADIC = the field's 2-adicity)
   const uint32_t* hi;      // w_{2^ADIC}^(4096 i)
+  const uint32_t* col;     // forward roots, 2-pass plans: the high pass's column factor of the
+                           // element at global index i, fully reduced (nullptr: none)
 };
 
 // Field policies.  FBB: BabyBear, values fully reduced in [0, p).  F29: p = 7 2^26 + 1, values
@@ -280,7 +282,9 @@ __device__ __forceinline__ void load_pass_tw(uint32_t* Tsm, const uint32_t* smal
 
 // Forward (DIF) pass over ARR (1 or 2) arrays of each job (blockIdx.y = job * ARR + array),
 // u32 in place, or the first pass reading bytes (zero padded, reduced mod 17, to Montgomery).
-template <int TB, int R, int M, bool FROM_U8, int ARR, class F>
+// COLT: the column factors come from tw.col (one word per element, indexed like the data)
+// instead of lo * hi (two words and a multiply per element).
+template <int TB, int R, int M, bool FROM_U8, int ARR, class F, bool COLT = false>
 __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WJobs jobs, WTw tw) {
   using G = Eng<TB, R, M, F>;
   static_assert(G::NT == wt_nt(TB), "tile block size");
@@ -306,13 +310,17 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WJobs jobs, 
   // column factor table words of the elements this thread stores (HIGH passes)
   constexpr int LF = G::lbq(G::NR - 1, false);
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, false);
-  uint32_t cl[G::HIGH ? G::E : 1], ch[G::HIGH ? G::E : 1];
+  uint32_t cl[G::HIGH ? G::E : 1], ch[G::HIGH && !COLT ? G::E : 1];
   if (G::HIGH) {
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
-      const uint32_t ex = G::col_exp(p, tile, bf + ((uint32_t)k << LF));
-      cl[k] = tw.lo[ex & 4095u];
-      ch[k] = tw.hi[ex >> 12];
+      if constexpr (COLT) {
+        cl[k] = tw.col[G::index(p, tile, bf + ((uint32_t)k << LF))];
+      } else {
+        const uint32_t ex = G::col_exp(p, tile, bf + ((uint32_t)k << LF));
+        cl[k] = tw.lo[ex & 4095u];
+        ch[k] = tw.hi[ex >> 12];
+      }
     }
   }
   load_pass_tw<M, G::NT>(Tsm, tw.small);
@@ -322,14 +330,15 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WJobs jobs, 
   for (int k = 0; k < G::E; k++) {
     const uint32_t e = bf + ((uint32_t)k << LF);
     uint32_t x = v[k];
-    if (G::HIGH) x = F::mul(x, F::colf(cl[k], ch[k]));
+    if constexpr (G::HIGH && COLT) x = F::mul(x, cl[k]);
+    else if constexpr (G::HIGH) x = F::mul(x, F::colf(cl[k], ch[k]));
     d[G::index(p, tile, e)] = x;
   }
 }
 
 // Inverse (DIT) pass, u32 in place; the final pass (TO_U8) scales by N^-1 (normal form,
 // which also leaves Montgomery form), reduces mod 17 and writes bytes for idx < out_len.
-template <int TB, int R, int M, bool TO_U8, class F>
+template <int TB, int R, int M, bool TO_U8, class F, bool COLT = false>
 __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, WTw tw, uint32_t ninv) {
   using G = Eng<TB, R, M, F>;
   static_assert(G::NT == wt_nt(TB), "tile block size");
@@ -345,21 +354,29 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   const uint32_t b0 = G::template base_q<0>(tid, true);
   constexpr int L0 = G::lbq(0, true);
   uint32_t v[G::E];
-  uint32_t cl[G::HIGH ? G::E : 1], ch[G::HIGH ? G::E : 1];
+  uint32_t cl[G::HIGH ? G::E : 1], ch[G::HIGH && !COLT ? G::E : 1];
 #pragma unroll
   for (int k = 0; k < G::E; k++) {
     const uint32_t e = b0 + ((uint32_t)k << L0);
-    v[k] = d[G::index(p, tile, e)];
+    const uint64_t idx = G::index(p, tile, e);
+    v[k] = d[idx];
     if (G::HIGH) {
-      const uint32_t ex = G::col_exp(p, tile, e);   // tw = inverse roots
-      cl[k] = tw.lo[ex & 4095u];
-      ch[k] = tw.hi[ex >> 12];
+      if constexpr (COLT) {
+        cl[k] = tw.col[idx];
+      } else {
+        const uint32_t ex = G::col_exp(p, tile, e);   // roots of tw (inverse or forward)
+        cl[k] = tw.lo[ex & 4095u];
+        ch[k] = tw.hi[ex >> 12];
+      }
     }
   }
   load_pass_tw<M, G::NT>(Tsm, tw.small);
   if (G::HIGH) {
 #pragma unroll
-    for (int k = 0; k < G::E; k++) v[k] = F::mul(v[k], F::colf(cl[k], ch[k]));
+    for (int k = 0; k < G::E; k++) {
+      if constexpr (COLT) v[k] = F::mul(v[k], cl[k]);
+      else v[k] = F::mul(v[k], F::colf(cl[k], ch[k]));
+    }
   }
   __syncthreads();
   G::template pass<true>(v, tid, bufs, 0, Tsm);
@@ -420,6 +437,19 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
   for (int k = 0; k < G::E; k++) d0[G::index(p, tile, bf + ((uint32_t)k << LF))] = va[k];
 }
 
+// Column-factor table of a 2-pass plan (lo = TB, M = k - TB): entry i = the high pass's factor
+// of the element at global index i = r 2^lo + L, w_{2^k}^(L bitrev_M(r)), fully reduced.
+template <int TB, class F>
+__global__ __launch_bounds__(256) void coltab_kernel(uint32_t* __restrict__ out, int k, WTw tw) {
+  const uint64_t idx = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (1ull << k)) return;
+  const int M = k - TB;
+  const uint32_t L = (uint32_t)(idx & ((1u << TB) - 1)), r = (uint32_t)(idx >> TB);
+  const uint32_t f = M ? __brev(r) >> (32 - M) : 0u;
+  const uint32_t ex = (L * f) << (F::ADIC - k);
+  out[idx] = F::colf(tw.lo[ex & 4095u], tw.hi[ex >> 12]);
+}
+
 // ------------------------------------------------------------------------------ host side
 namespace {
 
@@ -444,20 +474,49 @@ int wave_plan(int k, int TB, int* Ms) {
   return n;
 }
 
+// column tables [field][k] (field 0 BabyBear, 1 F29) for the 2-pass plans, k = 13 .. 23
+constexpr int COLT_MIN_K = 13, COLT_MAX_K = 23;
+uint32_t* g_col[2][COLT_MAX_K + 1] = {};
+
 WTw to_wtw(const PlkTwTables& t, bool inv) {
-  return inv ? WTw{t.small_i, t.lo_i, t.hi_i} : WTw{t.small_f, t.lo_f, t.hi_f};
+  return inv ? WTw{t.small_i, t.lo_i, t.hi_i, nullptr} : WTw{t.small_f, t.lo_f, t.hi_f, nullptr};
+}
+// forward roots of field F with the column table of a 2^k transform (when built)
+template <class F>
+WTw fwd_wtw(int k) {
+  const bool f29 = F::ADIC == f29::TWO_ADICITY;
+  WTw w = to_wtw(f29 ? plk_ntt_tables29() : plk_ntt_tables(), false);
+  w.col = (k >= COLT_MIN_K && k <= COLT_MAX_K) ? g_col[f29 ? 1 : 0][k] : nullptr;
+  return w;
 }
 
+// the table path applies to the pass whose bits reach the top (lo + M = k): a plan's first
+// forward and last inverse pass; byte-input forward / byte-output inverse or single-array
+// forward passes are the only ones instantiated with it
 template <int TB, int M, bool U8, int ARR, class F>
 void launch_fwd(WPass p, const WJobs& jobs, int nj, WTw tw, hipStream_t st) {
   constexpr int R = wt_r(TB);
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB);
+  if constexpr (M < TB && (U8 || ARR == 1)) {
+    if (tw.col && p.lo + M == p.k) {
+      hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, ARR, F, true>), dim3(tiles, ARR * nj), dim3(wt_nt(TB)), 0, st, p,
+                         jobs, tw);
+      return;
+    }
+  }
   hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, ARR, F>), dim3(tiles, ARR * nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw);
 }
 template <int TB, int M, bool U8, class F>
 void launch_inv(WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipStream_t st) {
   constexpr int R = wt_r(TB);
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB);
+  if constexpr (M < TB && U8) {
+    if (tw.col && p.lo + M == p.k) {
+      hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8, F, true>), dim3(tiles, nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw,
+                         ninv);
+      return;
+    }
+  }
   hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8, F>), dim3(tiles, nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw, ninv);
 }
 
@@ -520,8 +579,7 @@ int inv_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipS
 
 template <int TB, class F>
 int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t st) {
-  const PlkTwTables t = F::ADIC == f29::TWO_ADICITY ? plk_ntt_tables29() : plk_ntt_tables();
-  const WTw twf = to_wtw(t, false);   // forward roots for the inverse too (wt_center_kernel)
+  const WTw twf = fwd_wtw<F>(k);   // forward roots for the inverse too (wt_center_kernel)
   int Ms[4];
   const int np = wave_plan(k, TB, Ms);
   int lo[4];
@@ -555,7 +613,7 @@ int wave_ntt_t(const WJobs& jobs, int nj, int k, int inverse, hipStream_t st) {
     const int i = inverse ? np - 1 - s : s;
     const WPass p{k, lo[i]};
     const int rc = inverse ? inv_m<TB, false, FBB>(Ms[i], p, jobs, nj, to_wtw(t, true), 0u, st)
-                           : fwd_m<TB, false, 1, FBB>(Ms[i], p, jobs, nj, to_wtw(t, false), st);
+                           : fwd_m<TB, false, 1, FBB>(Ms[i], p, jobs, nj, fwd_wtw<FBB>(k), st);
     if (rc) return rc;
   }
   return PLK_OK;
@@ -564,6 +622,37 @@ int wave_ntt_t(const WJobs& jobs, int nj, int k, int inverse, hipStream_t st) {
 }  // namespace
 
 bool plk_wave_ntt_supported(int k) { return k > 12 && k <= bb::TWO_ADICITY; }
+
+namespace {
+template <class F>
+int build_coltabs(int fi) {
+  for (int k = COLT_MIN_K; k <= COLT_MAX_K; k++) {
+    if (g_col[fi][k]) continue;
+    PLK_HIP(hipMalloc((void**)&g_col[fi][k], 4ull << k));
+    const WTw tw = to_wtw(fi ? plk_ntt_tables29() : plk_ntt_tables(), false);
+    const unsigned blocks = (unsigned)((1ull << k) / 256);
+    if (tile_bits(k) == 13) hipLaunchKernelGGL((coltab_kernel<13, F>), dim3(blocks), dim3(256), 0, 0, g_col[fi][k], k, tw);
+    else hipLaunchKernelGGL((coltab_kernel<12, F>), dim3(blocks), dim3(256), 0, 0, g_col[fi][k], k, tw);
+    PLK_HIP(hipGetLastError());
+  }
+  return PLK_OK;
+}
+}  // namespace
+
+// 2 x 64 MB of column tables (BabyBear and F29, 2^13 .. 2^23 points), built on the device
+int plk_wave_init_coltabs(void) {
+  int rc = build_coltabs<FBB>(0);
+  if (!rc) rc = build_coltabs<F29>(1);
+  if (!rc) PLK_HIP(hipDeviceSynchronize());
+  return rc;
+}
+void plk_wave_free_coltabs(void) {
+  for (auto& f : g_col)
+    for (auto& t : f) {
+      (void)hipFree(t);
+      t = nullptr;
+    }
+}
 
 int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, int field, uint32_t ninv, hipStream_t st) {
   for (int j0 = 0; j0 < nj; j0 += WT_MAX_JOBS) {

@@ -77,3 +77,5 @@ bool plk_wave_ntt_supported(int k);
 // ninv = 2^-k mod p in normal form for that field
 int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, int field, uint32_t ninv, hipStream_t st);
 int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st);
+int plk_wave_init_coltabs(void);    // after plk_ntt_init_tables' root tables
+void plk_wave_free_coltabs(void);
