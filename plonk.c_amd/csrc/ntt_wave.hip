@@ -30,6 +30,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 #ifndef PLK_NTT_DIAG
 #define PLK_NTT_DIAG 0        // tuning builds only: bit 0 skips the butterflies, bit 1 the LDS exchanges
 #endif
@@ -404,37 +406,47 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
 // halves the block's LDS so that two blocks fit a CU.
 template <int TB, int R, class F>
 __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_center_kernel(WPass p, WJobs jobs,
-                                                                                                     WTw twf) {
+                                                                                                     WTw twf,
+                                                                                                     uint32_t nitems_jobs) {
   using G = Eng<TB, R, TB, F>;
   static_assert(G::NT == wt_ntc(TB), "tile block size");
   static_assert(G::lbq(G::NR - 1, false) == 0 && G::lbq(0, true) == 0, "center mapping");
   __shared__ uint32_t Tlds[1 << TB];
   __shared__ uint32_t bufs[(G::DBUF ? 2 : 1) * G::BUF];
   const uint32_t* Tf = Tlds;
-  uint32_t* d0 = jobs.j[blockIdx.y].A;
-  const uint32_t* d1 = jobs.j[blockIdx.y].B;
   const uint32_t tid = threadIdx.x;
-  const uint32_t tile = block_tile();
   const uint32_t b0 = G::template base_q<0>(tid, false);
   constexpr int L0 = G::lbq(0, false);
-  uint32_t va[G::E], vb[G::E];
-#pragma unroll
-  for (int k = 0; k < G::E; k++) {
-    const uint64_t idx = G::index(p, tile, b0 + ((uint32_t)k << L0));
-    va[k] = d0[idx];
-    vb[k] = d1[idx];
-  }
-  load_pass_tw<TB, G::NT>(Tlds, twf.small);
-  __syncthreads();
-  G::template pass<false>(va, tid, bufs, 0, Tf);
-  G::template pass<false>(vb, tid, bufs, G::XCH, Tf);
-#pragma unroll
-  for (int k = 0; k < G::E; k++) va[k] = F::pmul(va[k], vb[k]);
-  G::template pass<true>(va, tid, bufs, 2 * G::XCH, Tf);
   constexpr int LF = G::lbq(G::NR - 1, true);
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, true);
+  // persistent: the grid (<= 2 blocks per CU) walks the batch's (job, tile) items, so the
+  // 2^TB-word twiddle table is loaded once per block instead of once per tile
+  const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB), items = tiles * nitems_jobs;
+  bool first = true;
+  for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+    const uint32_t job = it / tiles, tile = it - job * tiles;
+    uint32_t* d0 = jobs.j[job].A;
+    const uint32_t* d1 = jobs.j[job].B;
+    uint32_t va[G::E], vb[G::E];
 #pragma unroll
-  for (int k = 0; k < G::E; k++) d0[G::index(p, tile, bf + ((uint32_t)k << LF))] = va[k];
+    for (int k = 0; k < G::E; k++) {
+      const uint64_t idx = G::index(p, tile, b0 + ((uint32_t)k << L0));
+      va[k] = d0[idx];
+      vb[k] = d1[idx];
+    }
+    if (first) {
+      load_pass_tw<TB, G::NT>(Tlds, twf.small);
+      first = false;
+    }
+    __syncthreads();
+    G::template pass<false>(va, tid, bufs, 0, Tf);
+    G::template pass<false>(vb, tid, bufs, G::XCH, Tf);
+#pragma unroll
+    for (int k = 0; k < G::E; k++) va[k] = F::pmul(va[k], vb[k]);
+    G::template pass<true>(va, tid, bufs, 2 * G::XCH, Tf);
+#pragma unroll
+    for (int k = 0; k < G::E; k++) d0[G::index(p, tile, bf + ((uint32_t)k << LF))] = va[k];
+  }
 }
 
 // Column-factor table of a 2-pass plan (lo = TB, M = k - TB): entry i = the high pass's factor
@@ -461,6 +473,19 @@ int tile_bits(int k) {
     min_k = e ? atoi(e) : 21;
   }
   return k >= min_k ? 13 : 12;
+}
+
+// resident blocks of the persistent center kernel: 2 per CU (PLK_NTT_CENTER_BLOCKS overrides)
+uint32_t center_blocks() {
+  static uint32_t nb = 0;
+  if (!nb) {
+    const char* e = getenv("PLK_NTT_CENTER_BLOCKS");
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    nb = e ? (uint32_t)atoi(e) : 2u * (uint32_t)cus;
+    if (!nb) nb = 512;
+  }
+  return nb;
 }
 
 // passes of a 2^k transform, high bits first: the bits above the TB-bit lo = 0 pass in
@@ -591,7 +616,9 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
     if (rc) return rc;
   }
   const uint32_t tiles = (uint32_t)((1ull << k) >> TB);
-  hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F>), dim3(tiles, nj), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, jobs, twf);
+  const uint32_t grid = std::min<uint32_t>(tiles * nj, center_blocks());
+  hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F>), dim3(grid), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, jobs, twf,
+                     (uint32_t)nj);
   PLK_HIP(hipGetLastError());
   for (int i = np - 2; i >= 0; i--) {
     const WPass p{k, lo[i]};
