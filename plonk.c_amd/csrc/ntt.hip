@@ -364,8 +364,9 @@ __global__ __launch_bounds__(256) void polymul_direct_kernel(const uint8_t* lg, 
 
 // Batched tails of split products (one launch for a whole product group, blockIdx.y = job):
 // out[i] += sum_{j < lt} t[j] g[i - base - j] for i in [base, rl), out[i] for i >= ntt_len not
-// yet written (taken as 0).  16 outputs per thread: o0 = i0 - base is a multiple of 16, so the
-// g window [o0 - 16, o0 + 16) is two aligned uint4 loads when g is 16-byte aligned and in range.
+// yet written (taken as 0).  16 outputs per thread, chunks aligned to the OUTPUT (one uint4
+// read-modify-write); the 32-byte g window is funnel-shifted out of three aligned uint4 loads
+// and each output is four v_dot4_u32_u8 of the reversed t against the window's bytes.
 struct TailJob {
   const uint8_t* g;
   uint64_t lg;
@@ -379,41 +380,110 @@ struct TailJobs {
   TailJob j[TAIL_MAX_JOBS];
 };
 
+__device__ __forceinline__ uint32_t mod17_small(uint32_t a) {   // a < 2^13
+  const uint32_t q = (a * 61681u) >> 20;
+  return a - 17u * q;
+}
+// any byte of x above 16 (false positives only next to bytes >= 0x80)
+__device__ __forceinline__ bool bytes_over16(uint32_t x) { return (((x + 0x6F6F6F6Fu) | x) & 0x80808080u) != 0; }
+__device__ __forceinline__ uint32_t bytes_mod17(uint32_t x) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++) r |= (((x >> (8 * b)) & 0xFFu) % 17u) << (8 * b);
+  return r;
+}
+
 __global__ __launch_bounds__(256) void polymul_tail_batch_kernel(TailJobs J) {
   const TailJob& jb = J.j[blockIdx.y];
-  uint32_t T[16];
+  uint32_t Tr[4] = {0, 0, 0, 0};   // byte j' = t[15 - j'] mod 17
 #pragma unroll
-  for (int j = 0; j < 16; j++) T[j] = j < jb.lt ? jb.t[j] % 17u : 0u;
-  const bool al = ((uintptr_t)jb.g % 16) == 0;
+  for (int j = 0; j < 16; j++) {
+    const uint32_t v = j < jb.lt ? jb.t[j] % 17u : 0u;
+    Tr[(15 - j) >> 2] |= v << (8 * ((15 - j) & 3));
+  }
   const uint64_t span = jb.rl - jb.base;
-  for (uint64_t o0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; o0 < span;
-       o0 += (uint64_t)gridDim.x * blockDim.x * 16) {
-    uint32_t win[32];   // g[o0 - 16 + q], 0 outside [0, lg)
-    if (al && o0 >= 16 && o0 + 16 <= jb.lg) {
-      const uint4 a = *reinterpret_cast<const uint4*>(jb.g + o0 - 16);
-      const uint4 b = *reinterpret_cast<const uint4*>(jb.g + o0);
-      const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint8_t* const ob = jb.out8 + jb.base;
+  const int64_t d = (int64_t)((uintptr_t)ob & 15);     // chunk c: outputs o in [16c - d, 16c - d + 16)
+  const int64_t s = (int64_t)((1 - d) & 15);           // window start mod 16
+  const bool galign = ((uintptr_t)jb.g & 15) == 0;
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 16 * c < span + d;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const int64_t o0 = (int64_t)(16 * c) - d;
+    const int64_t ws = o0 - 15;                        // window bytes g[ws + q], q < 32
+    uint32_t W[8];
+    const int64_t A = ws - s;                          // 16-byte aligned
+    if (galign && A >= 0 && (uint64_t)(A + 48) <= jb.lg) {
+      uint32_t L[12];
 #pragma unroll
-      for (int q = 0; q < 32; q++) win[q] = (w[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+      for (int v = 0; v < 3; v++) {
+        const uint4 q = *reinterpret_cast<const uint4*>(jb.g + A + 16 * v);
+        L[4 * v] = q.x; L[4 * v + 1] = q.y; L[4 * v + 2] = q.z; L[4 * v + 3] = q.w;
+      }
+      const uint32_t r = (uint32_t)(s & 3);
+      switch (s >> 2) {   // uniform
+#define PLK_TAIL_W(Q)                                                                          \
+  case Q:                                                                                     \
+    _Pragma("unroll") for (int m = 0; m < 8; m++) W[m] = __builtin_amdgcn_alignbyte(L[Q + m + 1], L[Q + m], r); \
+    break;
+        PLK_TAIL_W(0) PLK_TAIL_W(1) PLK_TAIL_W(2) PLK_TAIL_W(3)
+#undef PLK_TAIL_W
+      }
     } else {
 #pragma unroll
-      for (int q = 0; q < 32; q++) {
-        const int64_t o = (int64_t)o0 - 16 + q;
-        win[q] = (o >= 0 && (uint64_t)o < jb.lg) ? jb.g[o] : 0u;
+      for (int m = 0; m < 8; m++) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const int64_t o = ws + 4 * m + b;
+          if (o >= 0 && (uint64_t)o < jb.lg) w |= (uint32_t)jb.g[o] << (8 * b);
+        }
+        W[m] = w;
       }
     }
+    bool big = false;
+#pragma unroll
+    for (int m = 0; m < 8; m++) big |= bytes_over16(W[m]);
+    if (big) {
+#pragma unroll
+      for (int m = 0; m < 8; m++) W[m] = bytes_mod17(W[m]);
+    }
+    // current outputs (0 where not yet written by the transform)
+    uint32_t cur[4] = {0, 0, 0, 0};
+    const bool full = o0 >= 0 && (uint64_t)(o0 + 16) <= span;
+    if (full && jb.base + (uint64_t)o0 + 16 <= jb.ntt_len) {
+      const uint4 q = *reinterpret_cast<const uint4*>(ob + o0);
+      cur[0] = q.x; cur[1] = q.y; cur[2] = q.z; cur[3] = q.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const int64_t o = o0 + k;
+        if (o >= 0 && (uint64_t)o < span && jb.base + (uint64_t)o < jb.ntt_len)
+          cur[k >> 2] |= (uint32_t)ob[o] << (8 * (k & 3));
+      }
+    }
+    uint32_t res[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-      const uint64_t i = jb.base + o0 + k;
-      if (o0 + k >= span) break;
-      uint32_t acc = i < jb.ntt_len ? jb.out8[i] : 0u;
+      uint32_t acc = (cur[k >> 2] >> (8 * (k & 3))) & 0xFFu;
 #pragma unroll
-      for (int j = 0; j < 16; j++) acc += T[j] * (win[16 + k - j] % 17u);
-      jb.out8[i] = (uint8_t)(acc % 17u);
+      for (int m = 0; m < 4; m++) {
+        const int i = (k >> 2) + m;
+        const uint32_t wd = (k & 3) ? __builtin_amdgcn_alignbyte(W[i + 1], W[i], k & 3) : W[i];
+        acc = __builtin_amdgcn_udot4(Tr[m], wd, acc, false);
+      }
+      res[k >> 2] |= mod17_small(acc) << (8 * (k & 3));
+    }
+    if (full) {
+      *reinterpret_cast<uint4*>(ob + o0) = make_uint4(res[0], res[1], res[2], res[3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const int64_t o = o0 + k;
+        if (o >= 0 && (uint64_t)o < span) ob[o] = (uint8_t)(res[k >> 2] >> (8 * (k & 3)));
+      }
     }
   }
 }
-
 
 // ------------------------------------------------------------------------------ host side
 namespace {

@@ -84,6 +84,25 @@ def test_rounds_shape_vs_oracle(hip, oracle, n, seed):
         ref.rounds(polys, chal, rnd, strict=True)
 
 
+def test_rounds_unaligned_inputs(hip, oracle):
+    """Polynomials at odd device addresses: the rounds 1-3 preparation falls back from the fused
+    16-byte kernel (prep_kernel) to the blinding poly_muls + lincombs; same bytes as the oracle."""
+    n = 1000
+    polys, chal, rnd, zh, pts = _synthetic(n, 4, 2 * n + 8)   # the n = 1000 case above (no reference exit)
+    ref = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes())
+    want = ref.rounds(polys, chal, rnd, strict=False)
+    pr = hip.Prover(n, zh, pts)
+    backing = [torch.zeros(n + 16, dtype=torch.uint8, device="cuda") for _ in polys]
+    dev = []
+    for b, p in zip(backing, polys):
+        b[3:3 + n] = torch.from_numpy(p).to("cuda")
+        dev.append(b[3:3 + n])
+    assert all(t.data_ptr() % 16 == 3 for t in dev)
+    assert pr.rounds_dev(dev, chal, rnd, strict=False).hex() == want.hex()
+    aligned = [torch.from_numpy(p).to("cuda") for p in polys]
+    assert pr.rounds_dev(aligned, chal, rnd, strict=False).hex() == want.hex()
+
+
 def test_rounds_general_divisor(hip, oracle):
     """Z_H that is not x^m + c (H not a subgroup, e.g. n = 3): general long division path."""
     n = 3
