@@ -171,17 +171,6 @@ __global__ __launch_bounds__(256) void lincomb16_kernel(LcArgs a, const uint8_t*
   }
 }
 
-// store 16 packed coefficients at out[i..i+16) clipped to len (out 16-byte aligned)
-__device__ __forceinline__ void store16(uint8_t* out, uint64_t len, uint64_t i, const uint32_t (&o)[4]) {
-  if (i + 16 <= len) {
-    *reinterpret_cast<uint4*>(out + i) = make_uint4(o[0], o[1], o[2], o[3]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      if (i + k < len) out[i + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
-  }
-}
-
 // Rounds 1-3 preparation in ONE launch (every step is elementwise up to a shift of 2):
 //   a_x = (b2 + b1 x) Z_H + f_a, b_x, c_x (src/plonk.h:280-296), z_x = (b9 + b8 x + b7 x^2) Z_H
 //   + acc_x (:371-377), then round 3's linear factors alpha (a + beta x + gamma), b + beta k1 x +
@@ -193,55 +182,77 @@ struct PrepArgs {
   uint64_t lz, n, la, lzx;
   uint8_t *cA, *cB, *cC, *cZ, *A2, *B2, *C2, *A3, *B3, *C3, *ZW, *Z1;
 };
+// 4 coefficients per thread (dword loads / stores): a 2^20-gate proof has 2^18 threads, four
+// waves per SIMD to overlap the loads (16 per thread left one wave per SIMD: 18 us)
+__device__ __forceinline__ uint32_t load4(const uint8_t* p, uint64_t len, uint64_t i) {
+  if (i + 4 <= len) return *reinterpret_cast<const uint32_t*>(p + i);
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (i + k < len) w |= (uint32_t)p[i + k] << (8 * k);
+  return w;
+}
+__device__ __forceinline__ void store4(uint8_t* out, uint64_t len, uint64_t i, uint32_t w) {
+  if (i + 4 <= len) {
+    *reinterpret_cast<uint32_t*>(out + i) = w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (i + k < len) out[i + k] = (uint8_t)(w >> (8 * k));
+  }
+}
 __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a, const uint8_t* __restrict__ S) {
   const uint32_t al = S[S_ALPHA], be = S[S_BETA], ga = S[S_GAMMA], bk1 = S[S_BK1], bk2 = S[S_BK2];
   const uint32_t al2 = S[S_ALPHA2], om = S[S_OMEGA];
   const uint32_t ba0 = S[P_BLA], ba1 = S[P_BLA + 1], bb0 = S[P_BLB], bb1 = S[P_BLB + 1], bc0 = S[P_BLC],
                  bc1 = S[P_BLC + 1], bz0 = S[P_BLZ], bz1 = S[P_BLZ + 1], bz2 = S[P_BLZ + 2];
-  uint32_t tw[16];   // omega^k; omega^i = 1 for i = 0 mod 16 (omega != 0)
-  tw[0] = 1;
-#pragma unroll
-  for (int k = 1; k < 16; k++) tw[k] = tw[k - 1] * om % HFP;
+  uint32_t tw[4];   // omega^(i + k) for this thread's 4 coefficients
   const uint64_t top = a.la > a.lzx ? a.la : a.lzx;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
-  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; i < top; i += stride) {
-    uint32_t z[18];   // z[k + 2] = Z_H[i + k] mod 17, k = -2 .. 15 (zero outside [0, lz))
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < top; i += stride) {
+    // omega^i, i mod 16 (omega^16 = 1 for omega != 0)
     {
-      uint32_t w[4];
-      load16(a.zh, a.lz, i, w);
+      uint32_t x = 1, b = om, e = (uint32_t)(i & 15);
+      while (e) { if (e & 1) x = x * b % HFP; b = b * b % HFP; e >>= 1; }
+      tw[0] = x;
 #pragma unroll
-      for (int k = 0; k < 16; k++) z[k + 2] = ((w[k >> 2] >> (8 * (k & 3))) & 0xFFu) % HFP;
+      for (int k = 1; k < 4; k++) tw[k] = tw[k - 1] * om % HFP;
+    }
+    uint32_t z[6];   // z[k + 2] = Z_H[i + k] mod 17, k = -2 .. 3 (zero outside [0, lz))
+    {
+      const uint32_t w = load4(a.zh, a.lz, i);
+#pragma unroll
+      for (int k = 0; k < 4; k++) z[k + 2] = ((w >> (8 * k)) & 0xFFu) % HFP;
       z[0] = (i >= 2 && i - 2 < a.lz) ? a.zh[i - 2] % HFP : 0u;
       z[1] = (i >= 1 && i - 1 < a.lz) ? a.zh[i - 1] % HFP : 0u;
     }
-    uint32_t fa[4], fb[4], fc[4], fz[4], f1[4], f2[4], f3[4];
-    load16(a.fa, a.n, i, fa); load16(a.fb, a.n, i, fb); load16(a.fc, a.n, i, fc); load16(a.acc, a.n, i, fz);
-    load16(a.s1, a.n, i, f1); load16(a.s2, a.n, i, f2); load16(a.s3, a.n, i, f3);
-    uint32_t oA[4] = {}, oB[4] = {}, oC[4] = {}, oZ[4] = {}, oA2[4] = {}, oB2[4] = {}, oC2[4] = {}, oA3[4] = {},
-             oB3[4] = {}, oC3[4] = {}, oZW[4] = {}, oZ1[4] = {};
+    const uint32_t fa = load4(a.fa, a.n, i), fb = load4(a.fb, a.n, i), fc = load4(a.fc, a.n, i),
+                   fz = load4(a.acc, a.n, i), f1 = load4(a.s1, a.n, i), f2 = load4(a.s2, a.n, i),
+                   f3 = load4(a.s3, a.n, i);
+    uint32_t oA = 0, oB = 0, oC = 0, oZ = 0, oA2 = 0, oB2 = 0, oC2 = 0, oA3 = 0, oB3 = 0, oC3 = 0, oZW = 0, oZ1 = 0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const int wd = k >> 2, sh = 8 * (k & 3);
-      auto byte = [&](const uint32_t (&f)[4]) { return (f[wd] >> sh) & 0xFFu; };
+    for (int k = 0; k < 4; k++) {
+      const int sh = 8 * k;
+      auto byte = [&](uint32_t f) { return (f >> sh) & 0xFFu; };
       const uint32_t c0 = (i + k == 0), c1 = (i + k == 1);
       const uint32_t va = (ba0 * z[k + 2] + ba1 * z[k + 1] + byte(fa)) % HFP;
       const uint32_t vb = (bb0 * z[k + 2] + bb1 * z[k + 1] + byte(fb)) % HFP;
       const uint32_t vc = (bc0 * z[k + 2] + bc1 * z[k + 1] + byte(fc)) % HFP;
       const uint32_t vz = (bz0 * z[k + 2] + bz1 * z[k + 1] + bz2 * z[k] + byte(fz)) % HFP;
-      oA[wd] |= va << sh; oB[wd] |= vb << sh; oC[wd] |= vc << sh; oZ[wd] |= vz << sh;
-      oA2[wd] |= (va + c0 * ga + c1 * be) % HFP * al % HFP << sh;
-      oB2[wd] |= (vb + c0 * ga + c1 * bk1) % HFP << sh;
-      oC2[wd] |= (vc + c0 * ga + c1 * bk2) % HFP << sh;
-      oA3[wd] |= (va + be * byte(f1) + c0 * ga) % HFP * al % HFP << sh;
-      oB3[wd] |= (vb + be * byte(f2) + c0 * ga) % HFP << sh;
-      oC3[wd] |= (vc + be * byte(f3) + c0 * ga) % HFP << sh;
-      oZW[wd] |= vz * (om == 0 ? c0 : tw[k]) % HFP << sh;
-      oZ1[wd] |= (vz + c0 * 16u) % HFP * al2 % HFP << sh;
+      oA |= va << sh; oB |= vb << sh; oC |= vc << sh; oZ |= vz << sh;
+      oA2 |= (va + c0 * ga + c1 * be) % HFP * al % HFP << sh;
+      oB2 |= (vb + c0 * ga + c1 * bk1) % HFP << sh;
+      oC2 |= (vc + c0 * ga + c1 * bk2) % HFP << sh;
+      oA3 |= (va + be * byte(f1) + c0 * ga) % HFP * al % HFP << sh;
+      oB3 |= (vb + be * byte(f2) + c0 * ga) % HFP << sh;
+      oC3 |= (vc + be * byte(f3) + c0 * ga) % HFP << sh;
+      oZW |= vz * (om == 0 ? c0 : tw[k]) % HFP << sh;
+      oZ1 |= (vz + c0 * 16u) % HFP * al2 % HFP << sh;
     }
-    store16(a.cA, a.la, i, oA); store16(a.cB, a.la, i, oB); store16(a.cC, a.la, i, oC);
-    store16(a.A2, a.la, i, oA2); store16(a.B2, a.la, i, oB2); store16(a.C2, a.la, i, oC2);
-    store16(a.A3, a.la, i, oA3); store16(a.B3, a.la, i, oB3); store16(a.C3, a.la, i, oC3);
-    store16(a.cZ, a.lzx, i, oZ); store16(a.ZW, a.lzx, i, oZW); store16(a.Z1, a.lzx, i, oZ1);
+    store4(a.cA, a.la, i, oA); store4(a.cB, a.la, i, oB); store4(a.cC, a.la, i, oC);
+    store4(a.A2, a.la, i, oA2); store4(a.B2, a.la, i, oB2); store4(a.C2, a.la, i, oC2);
+    store4(a.A3, a.la, i, oA3); store4(a.B3, a.la, i, oB3); store4(a.C3, a.la, i, oC3);
+    store4(a.cZ, a.lzx, i, oZ); store4(a.ZW, a.lzx, i, oZW); store4(a.Z1, a.lzx, i, oZ1);
   }
 }
 
@@ -1287,7 +1298,7 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   if (aligned && L.la <= L.lzx && L.lzx <= L.la + 1) {
     const PrepArgs pa{P->d_zh, FA, FB, FC, ACC, S1, S2, S3, L.lz, n, L.la, L.lzx,
                       cA, cB, cC, cZ, P->A2, P->B2, P->C2, P->A3, P->B3, P->C3, P->ZW, P->Z1};
-    const uint64_t blocks = std::min<uint64_t>((L.lzx + 4095) / 4096, 2048);
+    const uint64_t blocks = std::min<uint64_t>((L.lzx + 1023) / 1024, 4096);
     hipLaunchKernelGGL(prep_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, pa, dS);
     PLK_HIP(hipGetLastError());
   } else {
