@@ -515,6 +515,102 @@ __global__ __launch_bounds__(256) void divide_binomial4_kernel(const uint8_t* __
   if (threadIdx.x == 0) rem_part[blockIdx.x] = vote ? 1 : 0;
 }
 
+// t(x) in one launch: the numerator lincomb (src/plonk.h:494-503) evaluated per chain element
+// (no numerator buffer: its dwords come straight from the 8 product / q_c terms), the Z_H
+// division of divide_binomial4_kernel, and the t_lo / t_mid / t_hi slices (src/plonk.h:513-519)
+// written into the commitment arena next to t(x) itself.
+struct Slices3 {
+  uint8_t* dst[3];
+  uint64_t len[3];
+  uint64_t part;
+};
+// NT terms, branch-free: every load is issued (a position past a term's length reads the term's
+// first dword and is masked), so the chain's loads go out together -- loads under divergent
+// branches each waited for vmcnt(0).  Terms are 4-byte aligned and readable up to their length
+// rounded up to 4 (checked on the host).
+template <int NT>
+__device__ __forceinline__ uint32_t lc_word(const LcArgs& a, const uint32_t (&cf)[LC_MAX], uint32_t sc, uint32_t c0,
+                                            uint32_t c1, uint64_t x) {   // x = 0 mod 4
+  uint32_t acc[4] = {x == 0 ? c0 : 0u, x == 0 ? c1 : 0u, 0u, 0u};
+#pragma unroll
+  for (int t = 0; t < NT; t++) {
+    const uint64_t len = a.len[t];
+    const bool in = x < len;
+    const uint32_t wv = *reinterpret_cast<const uint32_t*>(a.p[t] + (in ? x : 0));
+    const uint32_t mask = x + 4 <= len ? 0xFFFFFFFFu : (in ? (1u << (8 * (uint32_t)(len - x))) - 1u : 0u);
+    const uint32_t w = wv & mask;
+#pragma unroll
+    for (int b = 0; b < 4; b++) acc[b] += cf[t] * ((w >> (8 * b)) & 0xFFu);
+  }
+  uint32_t o = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++) o |= (acc[b] % HFP * sc % HFP) << (8 * b);
+  return o;
+}
+template <int NT, int KMAX>
+__global__ __launch_bounds__(256) void numdiv_kernel(LcArgs a, const uint8_t* __restrict__ S, uint64_t m, uint32_t lead,
+                                                     uint32_t c, uint8_t* __restrict__ q, uint64_t ql, uint64_t cq,
+                                                     uint64_t cr, Slices3 sl, uint8_t* __restrict__ rem_part) {
+  uint32_t cf[LC_MAX];
+#pragma unroll
+  for (int t = 0; t < LC_MAX; t++) cf[t] = t < NT ? S[a.slot[t]] : 0u;
+  const uint32_t sc = S[a.scale];
+  const uint32_t c0 = a.c0 >= 0 ? S[a.c0] : 0u, c1 = a.c1 >= 0 ? S[a.c1] : 0u;
+  const uint64_t nl = a.out_len;
+  const uint64_t r0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const uint32_t li = hinv(lead);
+  const uint32_t nc = hneg(c);
+  auto chain = [&](uint64_t r) -> uint64_t { return (r < m && nl > m && r < ql) ? (r <= cr ? cq + 1 : cq) : 0; };
+  const uint64_t cnt0 = chain(r0);
+  uint32_t w[KMAX];   // chains are at most KMAX = cq + 1 long (host): no branch around the loads
+#pragma unroll
+  for (int k = 0; k < KMAX; k++) {
+    const uint64_t x = (uint64_t)k < cnt0 ? r0 + (cnt0 - 1 - k) * m + m : 0;   // shorter chains: drop
+    const uint32_t v = lc_word<NT>(a, cf, sc, c0, c1, x);
+    w[k] = (uint64_t)k < cnt0 ? v : 0u;
+  }
+  const uint32_t wr = lc_word<NT>(a, cf, sc, c0, c1, r0 < m ? r0 : 0);   // num[r0 .. r0+3] (remainders)
+  uint32_t prev[4] = {0, 0, 0, 0}, skip[4];
+#pragma unroll
+  for (int b = 0; b < 4; b++) skip[b] = (uint32_t)(cnt0 - chain(r0 + b));
+#pragma unroll
+  for (int k = 0; k < KMAX; k++) {
+    if ((uint64_t)k < cnt0) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        if ((uint32_t)k >= skip[b]) {
+          const uint32_t v = (((w[k] >> (8 * b)) & 0xFFu) + nc * prev[b]) % HFP * li % HFP;
+          prev[b] = v;
+          o |= v << (8 * b);
+        }
+      }
+      const uint64_t j0 = r0 + (cnt0 - 1 - k) * m;
+      if (skip[0] == 0 && skip[3] == 0) *reinterpret_cast<uint32_t*>(q + j0) = o;
+      else
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+          if ((uint32_t)k >= skip[b]) q[j0 + b] = (uint8_t)(o >> (8 * b));
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        if ((uint32_t)k < skip[b]) continue;
+        const uint64_t j = j0 + b;
+        const int si = j < sl.part ? 0 : (j < 2 * sl.part ? 1 : 2);
+        const uint64_t off = j - (uint64_t)si * sl.part;
+        if (off < sl.len[si]) sl.dst[si][off] = (uint8_t)(o >> (8 * b));
+      }
+    }
+  }
+  uint32_t rv = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const uint64_t r = r0 + b;
+    if (r < m && r < nl && (((wr >> (8 * b)) & 0xFFu) + nc * prev[b]) % HFP) rv = 1;
+  }
+  const int vote = __syncthreads_or(rv != 0);
+  if (threadIdx.x == 0) rem_part[blockIdx.x] = vote ? 1 : 0;
+}
+
 // (b) divisor d1 x + d0: the long division gives q[j] = b num[j+1] + a q[j+1] with
 // a = -d0/d1, b = 1/d1, i.e. q[j] = b a^-(j+1) sum_{i>j} num[i] a^i  (a != 0; a^i = a^(i mod 16)).
 // The prover only divides by x - z and x - z omega (d1 = 1).  Three-phase suffix scan over
@@ -1341,16 +1437,35 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     const PlkPolyMulJob g3[] = {{P->T2b, L.l2b, cZ, L.lzx, P->T2}, {P->T3b, L.l2b, P->ZW, L.lzw, P->T3}};
     RC(plk_poly_mul_batch_launch(g3, 2, P->work, P->work_bytes, P->st));
   }
-  RC(lincomb(P,
-             {{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {P->BQR, L.lq1}, {P->CQO, L.lq1}, {QC, n}, {P->T2, L.l2},
-              {P->T3, L.l3}, {P->T4, L.lt4}},
-             {S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_NEG1, S_ONE}, -1, -1, S_ONE, -1, P->NUM, L.lnum));
-  RC(divide_zh(P, P->NUM, L.lnum, P->TX, L.ltx, P->d_stat + ST_REM_T));
-  // t_lo / t_mid / t_hi = poly_slice(t_x, ...) with part n + 2 (src/plonk.h:513-519)
+  // t(x) = numerator / Z_H; t_lo / t_mid / t_hi = poly_slice(t_x, ...) with part n + 2
+  // (src/plonk.h:494-519)
   const uint64_t part = n + 2;
   const uint64_t lmid = L.ltx > part ? std::min<uint64_t>(part, L.ltx - part) : 0;
   const uint64_t lhi = L.ltx > 2 * part ? L.ltx - 2 * part : 0;
-  {
+  const LcArgs num = make_lc({{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {P->BQR, L.lq1}, {P->CQO, L.lq1}, {QC, n},
+                              {P->T2, L.l2}, {P->T3, L.l3}, {P->T4, L.lt4}},
+                             {S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_NEG1, S_ONE}, -1, -1, S_ONE, -1, P->NUM,
+                             L.lnum);
+  // (q_c is the caller's buffer: n % 4 == 0 keeps its last dword inside it; the intermediates
+  // carry >= 16 bytes of padding)
+  bool fused = P->zh_kind == 0 && (P->zh_len - 1) % 4 == 0 && L.lnum > P->zh_len - 1 && num.nt == 8 &&
+               (uintptr_t)P->TX % 4 == 0 && n % 4 == 0 && (P->zh_len - 1) / 4 < (1ull << 31) && L.ltx / (P->zh_len - 1) < 8;
+  for (int t = 0; t < num.nt; t++) fused = fused && (uintptr_t)num.p[t] % 4 == 0;
+  if (fused) {
+    const uint64_t m = P->zh_len - 1, ql = L.ltx, nb = (m / 4 + 255) / 256;
+    const Slices3 sl{{cTlo, cTmid, cThi}, {std::min<uint64_t>(part, L.ltx), lmid, lhi}, part};
+    const uint64_t cq = ql ? (ql - 1) / m : 0, cr = ql ? (ql - 1) % m : 0;
+    if (cq + 1 <= 4)
+      hipLaunchKernelGGL((numdiv_kernel<8, 4>), dim3((unsigned)nb), dim3(256), 0, P->st, num, dS, m, P->zh_lead, P->zh_c,
+                         P->TX, ql, cq, cr, sl, P->d_rem);
+    else
+      hipLaunchKernelGGL((numdiv_kernel<8, 8>), dim3((unsigned)nb), dim3(256), 0, P->st, num, dS, m, P->zh_lead, P->zh_c,
+                         P->TX, ql, cq, cr, sl, P->d_rem);
+    PLK_HIP(hipGetLastError());
+    P->rem_blocks = nb;   // trim_many_kernel folds the votes into ST_REM_T
+  } else {
+    RC(lincomb_batch(P, {num}));
+    RC(divide_zh(P, P->NUM, L.lnum, P->TX, L.ltx, P->d_stat + ST_REM_T));
     const Copy3 c{{P->TX, P->TX + part, P->TX + 2 * part}, {cTlo, cTmid, cThi},
                   {std::min<uint64_t>(part, L.ltx), lmid, lhi}};
     const uint64_t blocks = std::min<uint64_t>((c.len[0] + 255) / 256, 2048);
