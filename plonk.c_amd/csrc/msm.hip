@@ -101,12 +101,23 @@ struct Group {
   uint4 q0, q1, q2, s;
 };
 
+#ifndef PLK_MSM_NT
+#define PLK_MSM_NT 0   // non-temporal (streaming) loads of the points and scalars (tuning)
+#endif
+typedef unsigned int plk_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld4(const uint4* p) {
+  if (PLK_MSM_NT) {
+    const plk_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const plk_u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return *p;
+}
 __device__ __forceinline__ Group load_group(const uint4* p4, const uint4* s4, uint64_t g) {
   Group r;
-  r.q0 = p4[3 * g + 0];
-  r.q1 = p4[3 * g + 1];
-  r.q2 = p4[3 * g + 2];
-  r.s = s4[g];
+  r.q0 = ld4(p4 + 3 * g + 0);
+  r.q1 = ld4(p4 + 3 * g + 1);
+  r.q2 = ld4(p4 + 3 * g + 2);
+  r.s = ld4(s4 + g);
   return r;
 }
 
