@@ -45,6 +45,10 @@ enum Slot : int {
   S_AB = 48, S_R24, S_BZW, S_R3, S_W0, S_NEGZWZ, S_R3B,
   // small constant polynomials (blinding factors), 4-byte aligned
   P_BLA = 64, P_BLB = 68, P_BLC = 72, P_BLZ = 76,
+  // evaluations at z of r(x)'s terms (r_z without materialising r(x) for it), and w_z(x)'s
+  // coefficients of those terms (v times r(x)'s scalars)
+  S_QMZ = 80, S_QLZ, S_QRZ, S_QOZ, S_ZXZ, S_P3Z,
+  S_VAB = 88, S_VAZ, S_VBZ, S_VCZ, S_VR24, S_VR3B,
   NSLOT = 128
 };
 
@@ -78,7 +82,7 @@ __device__ __forceinline__ uint32_t hinv(uint32_t a) { return hpow_d(a, HFP - 2)
 // out[i] = S[scale] * (sum_t S[slot_t] * p_t[i] + [i==0] S[c0] + [i==1] S[c1]) mod 17,
 // optionally times S[twist]^i.  Covers poly_add/sub/scale/add_hf chains (src/poly.h:67-104,
 // :179-197) and the z(omega x) twist (src/plonk.h:459-463).
-constexpr int LC_MAX = 10;
+constexpr int LC_MAX = 16;
 struct LcArgs {
   const uint8_t* p[LC_MAX];
   uint64_t len[LC_MAX];
@@ -319,10 +323,10 @@ __global__ __launch_bounds__(256) void copy3_kernel(Copy3 c) {
 
 // ------------------------------------------------------------------ poly_eval (batched)
 // Horner of src/poly.h:265-272 == sum c_i x^i mod 17; x^i = x^(i mod 16) for x != 0.
-constexpr int EV_MAX = 12;   // 5-bit values of all of them fit the top arrival word (bits 0-59)
+constexpr int EV_MAX = 16;
 constexpr int EV_BLOCKS = 256;
 constexpr int TICK_STRIDE = 32;   // one 128-byte line per arrival word
-enum EvPost : int { EV_POST_NONE = 0, EV_POST_ACC = 1, EV_POST_R4 = 4, EV_POST_R5 = 5 };
+enum EvPost : int { EV_POST_NONE = 0, EV_POST_ACC = 1, EV_POST_R4 = 4 };
 struct EvArgs {
   const uint8_t* p[EV_MAX];
   uint64_t len[EV_MAX];
@@ -383,22 +387,23 @@ __global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict
   }
   if (threadIdx.x != 0) return;
   // the partial travels inside the atomic (no fence: a device-scope release per block costs an
-  // L2 writeback each, 2048 of them took 60 us): row word = sum | arrivals << 32; the row's
-  // last block adds its value (5 bits at 5 e) into the top word, arrivals at bit 60
+  // L2 writeback each, 2048 of them took 60 us): row word = sum | arrivals << 32
   const uint32_t mine = red[0] % HFP;
   unsigned long long* row = reinterpret_cast<unsigned long long*>(tick) + e * (TICK_STRIDE / 2);
   const unsigned long long old = atomicAdd(row, (unsigned long long)mine | (1ull << 32));
   if ((uint32_t)(old >> 32) != gridDim.x - 1) return;
   *row = 0;                                               // re-armed for the next launch
-  const unsigned long long v = ((uint32_t)old + mine) % HFP;
-  unsigned long long* topw = reinterpret_cast<unsigned long long*>(tick) + EV_MAX * (TICK_STRIDE / 2);
-  const unsigned long long told = atomicAdd(topw, (v << (5 * e)) | (1ull << 60));
-  if ((int)(told >> 60) != a.ne - 1) return;
+  // the row's last block publishes the value: only these <= EV_MAX blocks fence
+  S[a.out[e]] = (uint8_t)(((uint32_t)old + mine) % HFP);
+  __threadfence();
+  uint32_t* topw = tick + EV_MAX * TICK_STRIDE;
+  if (atomicAdd(topw, 1u) != (uint32_t)a.ne - 1) return;
+  __threadfence();
   *topw = 0;
-  const unsigned long long all = told + ((v << (5 * e)) | (1ull << 60));
-  for (int r = 0; r < a.ne; r++) S[a.out[r]] = (uint8_t)((all >> (5 * r)) & 31u);
-  if (a.post == EV_POST_R4) scalars_r4(S);
-  if (a.post == EV_POST_R5) scalars_r5(S);
+  if (a.post == EV_POST_R4) {   // round 4's scalars (incl. r_z) and round 5's (w_z constant)
+    scalars_r4(S);
+    scalars_r5(S);
+  }
   if (a.post == EV_POST_ACC) stat[ST_ACC] = S[S_ACCW];   // acc_x(omega^n), src/plonk.h:366-368
 }
 
@@ -813,6 +818,16 @@ __device__ void scalars_r4(uint8_t* S) {
   const uint32_t y1 = (az + be * s1 + ga) % HFP, y2 = (bz + be * s2 + ga) % HFP;
   S[S_R3] = (uint8_t)(y1 * y2 % HFP * al % HFP);
   S[S_R3B] = (uint8_t)(S[S_R3] * S[S_BZW] % HFP);   // r_3 scale times the s_sigma_3 factor
+  // r_z = r(z) (src/plonk.h:571) from the evaluations of r(x)'s terms: evaluation is a ring
+  // homomorphism, so sum_i c_i p_i(z) = (sum_i c_i p_i)(z) mod 17
+  const uint32_t cs[6] = {S[S_AB], az, bz, cz, S[S_R24], S[S_R3B]};
+  const uint32_t ez[6] = {S[S_QMZ], S[S_QLZ], S[S_QRZ], S[S_QOZ], S[S_ZXZ], S[S_P3Z]};
+  uint32_t rz = 0;
+  for (int i = 0; i < 6; i++) {
+    rz += cs[i] * ez[i];
+    S[S_VAB + i] = (uint8_t)(S[S_V] * cs[i] % HFP);   // w_z(x) takes v r(x) term by term
+  }
+  S[S_RZ] = (uint8_t)(rz % HFP);
   S[S_NEGZWZ] = (uint8_t)hneg(zw);
 }
 
@@ -984,7 +999,7 @@ struct plk_prover {
   uint8_t** d_outs = nullptr;      // device array of the 13 poly pointers
   // intermediates
   uint8_t *blA, *blB, *blC, *zB, *AB, *ABQM, *AQL, *BQR, *CQO, *A2, *B2, *C2, *T2a, *T2b, *T2, *A3, *B3, *C3, *ZW,
-      *T3a, *T3b, *T3, *Z1, *T4, *NUM, *TX, *RX, *P3, *W, *ZZ, *REMT, *ACCV, *E0;
+      *T3a, *T3b, *T3, *Z1, *T4, *NUM, *TX, *P3, *W, *ZZ, *REMT, *ACCV, *E0;
   void* work = nullptr;
   size_t work_bytes = 0;
   hipStream_t st = nullptr;
@@ -1267,7 +1282,7 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
       {&P->ABQM, L.labqm}, {&P->AQL, L.lq1}, {&P->BQR, L.lq1}, {&P->CQO, L.lq1}, {&P->A2, L.la}, {&P->B2, L.la},
       {&P->C2, L.la}, {&P->T2a, L.l2a}, {&P->T2b, L.l2b}, {&P->T2, L.l2}, {&P->A3, L.la}, {&P->B3, L.la},
       {&P->C3, L.la}, {&P->ZW, L.lzw}, {&P->T3a, L.l2a}, {&P->T3b, L.l2b}, {&P->T3, L.l3}, {&P->Z1, L.lz1},
-      {&P->T4, L.lt4}, {&P->NUM, L.lnum}, {&P->TX, L.ltx}, {&P->RX, L.lrx}, {&P->P3, L.lr3},
+      {&P->T4, L.lt4}, {&P->NUM, L.lnum}, {&P->TX, L.ltx}, {&P->P3, L.lr3},
       {&P->W, L.lw}, {&P->ZZ, L.lzz}, {&P->REMT, L.lnum}, {&P->ACCV, n}, {&P->E0, n}};
   size_t o_iv[sizeof(iv) / sizeof(iv[0])];
   for (size_t i = 0; i < sizeof(iv) / sizeof(iv[0]); i++) o_iv[i] = B.take(iv[i].len + 16);
@@ -1473,19 +1488,23 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     PLK_HIP(hipGetLastError());
   }
   // ---- round 4: evaluations at z (src/plonk.h:527-533) and r(x)
+  // r(x) = ab q_m + a_z q_l + b_z q_r + c_z q_o + (r2 + r4) z_x + r3 z_x (s_sigma_3 beta z_omega_z)
+  // (src/plonk.h:536-571; the last product is z_x s_sigma_3 from round 3 times r3 beta z_omega_z).
+  // r(x) is never materialised: r_z comes from its terms' evaluations (scalars_r4) and w_z(x)
+  // takes v r(x) term by term.  One launch: the 14 evaluations + rounds 4/5 scalar programs.
   RC(evals(P, {{cA, L.la, S_Z, S_AZ}, {cB, L.la, S_Z, S_BZ}, {cC, L.la, S_Z, S_CZ}, {S1, n, S_Z, S_S1Z},
-               {S2, n, S_Z, S_S2Z}, {P->TX, L.ltx, S_Z, S_TZ}, {P->ZW, L.lzw, S_Z, S_ZWZ}, {L1, n, S_Z, S_L1Z}},
+               {S2, n, S_Z, S_S2Z}, {P->TX, L.ltx, S_Z, S_TZ}, {P->ZW, L.lzw, S_Z, S_ZWZ}, {L1, n, S_Z, S_L1Z},
+               {QM, n, S_Z, S_QMZ}, {QL, n, S_Z, S_QLZ}, {QR, n, S_Z, S_QRZ}, {QO, n, S_Z, S_QOZ},
+               {cZ, L.lzx, S_Z, S_ZXZ}, {P->P3, L.lr3, S_Z, S_P3Z}},
            EV_POST_R4));
-  // r(x) = ... + r3 (z_x (s_sigma_3 beta z_omega_z)) = ... + (r3 beta z_omega_z) (z_x s_sigma_3)
-  RC(lincomb(P, {{QM, n}, {QL, n}, {QR, n}, {QO, n}, {cZ, L.lzx}, {P->P3, L.lr3}},
-             {S_AB, S_AZ, S_BZ, S_CZ, S_R24, S_R3B}, -1, -1, S_ONE, -1, P->RX, L.lrx));
-  RC(evals(P, {{P->RX, L.lrx, S_Z, S_RZ}}, EV_POST_R5));   // + round 5's scalar program (w_z constant)
   // ---- round 5: opening polynomials (src/plonk.h:580-621)
   // w_z numerator and z(x) - z_omega_z, then both divisions, each pair in one launch per phase
-  RC(lincomb_batch(P, {make_lc({{cTlo, std::min<uint64_t>(part, L.ltx)}, {cTmid, lmid}, {cThi, lhi}, {P->RX, L.lrx},
-                                {cA, L.la}, {cB, L.la}, {cC, L.la}, {S1, n}, {S2, n}},
-                               {S_ONE, S_ZN2, S_Z2N4, S_V, S_V2, S_V3, S_V4, S_V5, S_V6}, S_W0, -1, S_ONE, -1, P->W,
-                               L.lw),
+  RC(lincomb_batch(P, {make_lc({{cTlo, std::min<uint64_t>(part, L.ltx)}, {cTmid, lmid}, {cThi, lhi}, {QM, n},
+                                {QL, n}, {QR, n}, {QO, n}, {cZ, L.lzx}, {P->P3, L.lr3}, {cA, L.la}, {cB, L.la},
+                                {cC, L.la}, {S1, n}, {S2, n}},
+                               {S_ONE, S_ZN2, S_Z2N4, S_VAB, S_VAZ, S_VBZ, S_VCZ, S_VR24, S_VR3B, S_V2, S_V3, S_V4,
+                                S_V5, S_V6},
+                               S_W0, -1, S_ONE, -1, P->W, L.lw),
                        make_lc({{cZ, L.lzx}}, {S_ONE}, S_NEGZWZ, -1, S_ONE, -1, P->ZZ, L.lzz)}));
   RC(divide_linear(P, {{P->W, L.lw, S_Z, cWz, P->d_stat + ST_REM_W1},
                        {P->ZZ, L.lzz, S_ZOMEGA, cWzw, P->d_stat + ST_REM_W2}}));
