@@ -618,8 +618,8 @@ __global__ __launch_bounds__(256) void numdiv_kernel(LcArgs a, const uint8_t* __
 
 // (b) divisor d1 x + d0: the long division gives q[j] = b num[j+1] + a q[j+1] with
 // a = -d0/d1, b = 1/d1, i.e. q[j] = b a^-(j+1) sum_{i>j} num[i] a^i  (a != 0; a^i = a^(i mod 16)).
-// The prover only divides by x - z and x - z omega (d1 = 1).  Three-phase suffix scan over
-// 4096-element blocks.
+// The prover only divides by x - z and x - z omega (d1 = 1).  Two-phase suffix scan over
+// 4096-element blocks: block aggregates, then each block reduces the aggregates after it itself.
 constexpr int SCAN_T = 256, SCAN_E = 16, SCAN_B = SCAN_T * SCAN_E;
 // Round 5's two divisions (by x - z and by x - z omega) are independent: one launch per phase
 // for both (blockIdx.y / the carry block = the division).
@@ -663,32 +663,6 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_sums_kernel(LinDivs L, const 
   if (threadIdx.x == 0) D.bsum[blockIdx.x] = red[0] % HFP;
 }
 
-// exclusive suffix sums of the block sums (one block per division)
-__global__ __launch_bounds__(1024) void lin_scan_carry_kernel(LinDivs L) {
-  uint32_t* bsum = L.d[blockIdx.x].bsum;
-  const int nb = L.d[blockIdx.x].nb;
-  __shared__ uint32_t t[1024];
-  uint32_t carry = 0;
-  for (int hi = nb; hi > 0; hi -= 1024) {
-    const int lo = hi - 1024 > 0 ? hi - 1024 : 0;
-    const int i = lo + (int)threadIdx.x;
-    const uint32_t v = i < hi ? bsum[i] : 0u;
-    t[threadIdx.x] = v;
-    __syncthreads();
-    // inclusive suffix scan (Hillis-Steele)
-    for (int s = 1; s < 1024; s <<= 1) {
-      const uint32_t add = (int)threadIdx.x + s < 1024 ? t[threadIdx.x + s] : 0u;
-      __syncthreads();
-      t[threadIdx.x] = (t[threadIdx.x] + add) % HFP;
-      __syncthreads();
-    }
-    if (i < hi) bsum[i] = (t[threadIdx.x] + HFP - v + carry) % HFP;   // exclusive + carry
-    const uint32_t tot = t[0];
-    __syncthreads();
-    carry = (carry + tot) % HFP;
-  }
-}
-
 // divisor x - a (d1 = 1, d0 = -a): q[j] = a^-(j+1) sum_{i>j} num[i] a^i, rem = num[0] + a q[0]
 __global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(LinDivs L, const uint8_t* __restrict__ S) {
   const LinDiv& D = L.d[blockIdx.y];
@@ -721,8 +695,21 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(LinDivs L, const
     t[threadIdx.x] = (t[threadIdx.x] + add) % HFP;
     __syncthreads();
   }
+  // the block's carry: the aggregates of every block after it (sums kernel), reduced here --
+  // no separate carry-scan launch
+  __shared__ uint32_t cs[SCAN_T];
+  {
+    uint32_t c = 0;
+    for (int b = (int)blockIdx.x + 1 + (int)threadIdx.x; b < D.nb; b += SCAN_T) c += D.bsum[b];
+    cs[threadIdx.x] = c % HFP;
+  }
+  __syncthreads();
+  for (int k = SCAN_T / 2; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) cs[threadIdx.x] += cs[threadIdx.x + k];
+    __syncthreads();
+  }
   // sum of w over elements after this thread's chunk
-  uint32_t run = ((int)threadIdx.x + 1 < SCAN_T ? t[threadIdx.x + 1] : 0u) + D.bsum[blockIdx.x];
+  uint32_t run = ((int)threadIdx.x + 1 < SCAN_T ? t[threadIdx.x + 1] : 0u) + cs[0] % HFP;
   const uint64_t ql = nl - 1;
 #pragma unroll
   for (int k = SCAN_E - 1; k >= 0; k--) {
@@ -1207,8 +1194,6 @@ int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs) {
   }
   if (!nd) return PLK_OK;
   hipLaunchKernelGGL(lin_scan_sums_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, L, P->d_S);
-  PLK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(lin_scan_carry_kernel, dim3(nd), dim3(1024), 0, P->st, L);
   PLK_HIP(hipGetLastError());
   // denominators poly_new({-z, 1}) and ({-z omega, 1}), src/plonk.h:604-613
   hipLaunchKernelGGL(lin_scan_apply_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, L, P->d_S);
