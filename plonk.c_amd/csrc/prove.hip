@@ -663,6 +663,74 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_sums_kernel(LinDivs L, const 
   if (threadIdx.x == 0) D.bsum[blockIdx.x] = red[0] % HFP;
 }
 
+// Round 5's two numerators (w_z(x)'s lincomb, z(x) - z_omega_z) and the scan's block aggregates
+// in one launch: block (c, d) writes numerator d's coefficients [4096 c, 4096 (c+1)) and their
+// aggregate sum_{i > 0} num[i] a^i.  Every term is 16-byte aligned and readable in whole 16-byte
+// chunks up to its length (host-checked), so each term's uint4 load is issued unconditionally
+// (clamped address, masked bytes) and all of them are in flight together.
+__device__ __forceinline__ void load16_masked(const uint8_t* p, uint64_t len, uint64_t i, uint32_t (&w)[4]) {
+  const bool in = i < len;
+  const uint4 q = *reinterpret_cast<const uint4*>(p + (in ? i : 0));
+  const uint32_t v[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int64_t cnt = in ? (int64_t)len - (int64_t)(i + 4 * k) : 0;   // valid bytes in word k
+    w[k] = cnt >= 4 ? v[k] : (cnt <= 0 ? 0u : v[k] & ((1u << (8 * cnt)) - 1u));
+  }
+}
+__global__ __launch_bounds__(SCAN_T) void lincomb_scan_kernel(LcBatch b, LinDivs L, const uint8_t* __restrict__ S) {
+  const int d = blockIdx.y;
+  const LcArgs& a = b.a[d];
+  const LinDiv& D = L.d[d];
+  if ((int)blockIdx.x >= D.nb) return;
+  uint32_t cf[LC_MAX];
+#pragma unroll
+  for (int t = 0; t < LC_MAX; t++) cf[t] = t < a.nt ? S[a.slot[t]] : 0u;
+  const uint32_t sc = S[a.scale];
+  const uint32_t c0 = a.c0 >= 0 ? S[a.c0] : 0u, c1 = a.c1 >= 0 ? S[a.c1] : 0u;
+  const uint64_t i = (uint64_t)blockIdx.x * SCAN_B + (uint64_t)threadIdx.x * SCAN_E;
+  uint32_t acc[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) acc[k] = 0;
+  if (i == 0) { acc[0] = c0; acc[1] = c1; }
+#pragma unroll
+  for (int t = 0; t < LC_MAX; t++) {
+    if (t < a.nt) {   // uniform
+      uint32_t w[4];
+      load16_masked(a.p[t], a.len[t], i, w);
+#pragma unroll
+      for (int k = 0; k < 16; k++) acc[k] += cf[t] * ((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+    }
+  }
+  const uint32_t av = S[D.aslot];
+  uint32_t pw[16];
+  pw[0] = 1;
+#pragma unroll
+  for (int j = 1; j < 16; j++) pw[j] = pw[j - 1] * av % HFP;
+  uint32_t o[4] = {0, 0, 0, 0}, agg = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint32_t v = i + k < a.out_len ? acc[k] % HFP * sc % HFP : 0u;
+    o[k >> 2] |= v << (8 * (k & 3));
+    if (i + k > 0) agg += v * pw[k];   // (i + k) mod 16 = k
+  }
+  if (i + 16 <= a.out_len) {
+    *reinterpret_cast<uint4*>(a.out + i) = make_uint4(o[0], o[1], o[2], o[3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      if (i + k < a.out_len) a.out[i + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
+  }
+  __shared__ uint32_t red[SCAN_T];
+  red[threadIdx.x] = agg % HFP;
+  __syncthreads();
+  for (int s2 = SCAN_T / 2; s2 > 0; s2 >>= 1) {
+    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) D.bsum[blockIdx.x] = red[0] % HFP;
+}
+
 // divisor x - a (d1 = 1, d0 = -a): q[j] = a^-(j+1) sum_{i>j} num[i] a^i, rem = num[0] + a q[0]
 __global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(LinDivs L, const uint8_t* __restrict__ S) {
   const LinDiv& D = L.d[blockIdx.y];
@@ -1178,7 +1246,19 @@ struct LinDivReq {
   uint8_t* q;
   uint32_t* flag;
 };
-int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs) {
+// lcs (optional): the numerators' lincombs, computed by the aggregate launch itself
+int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs, const LcBatch* lcs = nullptr) {
+  if (lcs) {   // a skipped (tiny) division would shift the numerators' order: compute them apart
+    int j = 0;
+    bool tiny = false;
+    for (const LinDivReq& r : reqs) tiny = tiny || r.nl < 2 || lcs->a[j++].out != r.num;
+    if (tiny) {
+      int rc = PLK_OK;
+      for (int i = 0; i < j && !rc; i++) rc = lincomb_batch(P, {lcs->a[i]});
+      if (rc) return rc;
+      lcs = nullptr;
+    }
+  }
   LinDivs L{};
   int nd = 0, nbmax = 0;
   uint32_t* bs = P->d_bsum;
@@ -1193,7 +1273,8 @@ int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs) {
     nbmax = std::max(nbmax, nb);
   }
   if (!nd) return PLK_OK;
-  hipLaunchKernelGGL(lin_scan_sums_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, L, P->d_S);
+  if (lcs) hipLaunchKernelGGL(lincomb_scan_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, *lcs, L, P->d_S);
+  else hipLaunchKernelGGL(lin_scan_sums_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, L, P->d_S);
   PLK_HIP(hipGetLastError());
   // denominators poly_new({-z, 1}) and ({-z omega, 1}), src/plonk.h:604-613
   hipLaunchKernelGGL(lin_scan_apply_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, L, P->d_S);
@@ -1484,15 +1565,27 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
            EV_POST_R4));
   // ---- round 5: opening polynomials (src/plonk.h:580-621)
   // w_z numerator and z(x) - z_omega_z, then both divisions, each pair in one launch per phase
-  RC(lincomb_batch(P, {make_lc({{cTlo, std::min<uint64_t>(part, L.ltx)}, {cTmid, lmid}, {cThi, lhi}, {QM, n},
-                                {QL, n}, {QR, n}, {QO, n}, {cZ, L.lzx}, {P->P3, L.lr3}, {cA, L.la}, {cB, L.la},
-                                {cC, L.la}, {S1, n}, {S2, n}},
-                               {S_ONE, S_ZN2, S_Z2N4, S_VAB, S_VAZ, S_VBZ, S_VCZ, S_VR24, S_VR3B, S_V2, S_V3, S_V4,
-                                S_V5, S_V6},
-                               S_W0, -1, S_ONE, -1, P->W, L.lw),
-                       make_lc({{cZ, L.lzx}}, {S_ONE}, S_NEGZWZ, -1, S_ONE, -1, P->ZZ, L.lzz)}));
-  RC(divide_linear(P, {{P->W, L.lw, S_Z, cWz, P->d_stat + ST_REM_W1},
-                       {P->ZZ, L.lzz, S_ZOMEGA, cWzw, P->d_stat + ST_REM_W2}}));
+  {
+    LcBatch nb5{};
+    nb5.a[0] = make_lc({{cTlo, std::min<uint64_t>(part, L.ltx)}, {cTmid, lmid}, {cThi, lhi}, {QM, n}, {QL, n},
+                        {QR, n}, {QO, n}, {cZ, L.lzx}, {P->P3, L.lr3}, {cA, L.la}, {cB, L.la}, {cC, L.la}, {S1, n},
+                        {S2, n}},
+                       {S_ONE, S_ZN2, S_Z2N4, S_VAB, S_VAZ, S_VBZ, S_VCZ, S_VR24, S_VR3B, S_V2, S_V3, S_V4, S_V5,
+                        S_V6},
+                       S_W0, -1, S_ONE, -1, P->W, L.lw);
+    nb5.a[1] = make_lc({{cZ, L.lzx}}, {S_ONE}, S_NEGZWZ, -1, S_ONE, -1, P->ZZ, L.lzz);
+    // fused numerators need 16-byte aligned terms readable in whole 16-byte chunks: the
+    // caller's polynomials (length n) qualify when n % 16 == 0 and they are aligned
+    bool fuse = n % 16 == 0 && nb5.a[0].nt > 0 && nb5.a[1].nt > 0;
+    for (int j = 0; j < 2; j++) {
+      fuse = fuse && (uintptr_t)nb5.a[j].out % 16 == 0;
+      for (int t = 0; t < nb5.a[j].nt; t++) fuse = fuse && (uintptr_t)nb5.a[j].p[t] % 16 == 0;
+    }
+    if (!fuse) RC(lincomb_batch(P, {nb5.a[0], nb5.a[1]}));
+    RC(divide_linear(P, {{P->W, L.lw, S_Z, cWz, P->d_stat + ST_REM_W1},
+                         {P->ZZ, L.lzz, S_ZOMEGA, cWzw, P->d_stat + ST_REM_W2}},
+                     fuse ? &nb5 : nullptr));
+  }
   // ---- trimmed lengths for the reference's exits
   {
     TrimArgs t{};
