@@ -375,7 +375,7 @@ struct TailJob {
   uint64_t base, ntt_len, rl;
   uint8_t* out8;
 };
-constexpr int TAIL_MAX_JOBS = 8;
+constexpr int TAIL_MAX_JOBS = 12;
 struct TailJobs {
   TailJob j[TAIL_MAX_JOBS];
 };
@@ -673,7 +673,7 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
   bool use29 = !no29 && k <= f29::TWO_ADICITY;
   for (int i = 0; i < m; i++) {
     const uint64_t mn = g[i].la < g[i].lb ? g[i].la : g[i].lb;
-    if (mn * 256 >= f29::P) use29 = false;
+    if (mn * 128 >= f29::P) use29 = false;   // centered residues (ntt_wave.hip F29::from_byte)
   }
   const uint32_t ninv = use29 ? f29::hpow(1ull << k, f29::P - 2) : bb::hpow(1ull << k, bb::P - 2);   // normal form
   WJob w[64];
@@ -804,7 +804,7 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
 
 // Standalone forward NTT (DIF, natural -> bit-reversed), in place on Montgomery-form u32,
 // or inverse (DIT, bit-reversed -> natural, NOT scaled by N^-1).  Same passes as poly_mul.
-// batch independent arrays at d + b 2^k share each pass's launch (up to 8 per launch).
+// batch independent arrays at d + b 2^k share each pass's launch (up to 12 per launch).
 int plk_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st) {
   if (k < 1 || k > bb::TWO_ADICITY || batch < 1) return PLK_ERR_RANGE;
   if (plk_wave_ntt_supported(k)) return plk_wave_ntt_launch(d, k, batch, inverse, st);

@@ -68,7 +68,7 @@ struct WPass {
 // A batch of independent transforms of one size: job j owns the u32 arrays A (and B for a
 // product), optionally reads its inputs as bytes (a8/la, b8/lb) in the first forward pass
 // and writes its product as bytes (out8, out_len) in the last inverse pass.
-constexpr int WT_MAX_JOBS = 8;
+constexpr int WT_MAX_JOBS = 12;
 struct WJobs {
   WJob j[WT_MAX_JOBS];
 };
@@ -137,9 +137,18 @@ struct F29 {
   // a, b < 4p: reduce one below 2p so that a b < p 2^32
   __device__ static __forceinline__ uint32_t pmul(uint32_t a, uint32_t b) { return f29::mmul(a, f29::red2(b)); }
   __device__ static __forceinline__ uint32_t colf(uint32_t cl, uint32_t ch) { return f29::red1(f29::mmul(cl, ch)); }
-  __device__ static __forceinline__ uint32_t from_byte(uint32_t b) { return f29::mmul(b % 17u, f29::R2); }
+  // Centered residues: a coefficient v in [0, 17) enters as v - 17 when v > 8, so every
+  // convolution term is at most 64 in absolute value and a product is exact while
+  // 64 min(la, lb) <= (p - 1) / 2 (min(la, lb) * 128 < p: up to 3,670,016 coefficients, four
+  // times the uncentered bound); a result y > (p - 1) / 2 stands for y - p.
+  __device__ static __forceinline__ uint32_t from_byte(uint32_t b) {
+    const uint32_t v = b % 17u;
+    return f29::mmul(v > 8u ? v + (f29::P - 17u) : v, f29::R2);
+  }
   __device__ static __forceinline__ uint32_t out17(uint32_t v, uint32_t ninv) {
-    return f29::red1(f29::mmul(v, ninv)) % 17u;
+    const uint32_t y = f29::red1(f29::mmul(v, ninv));
+    const uint32_t r = y % 17u;
+    return y > (f29::P - 1) / 2 ? (r + 17u - f29::P % 17u) % 17u : r;   // (y - p) mod 17
   }
 };
 
@@ -694,7 +703,7 @@ int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, int field, u
   return PLK_OK;
 }
 
-// batch independent in-place transforms of 2^k points: array i at d + i 2^k, <= 8 per launch
+// batch independent in-place transforms of 2^k points: array i at d + i 2^k, <= 12 per launch
 int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st) {
   for (int j0 = 0; j0 < batch; j0 += WT_MAX_JOBS) {
     const int m = batch - j0 < WT_MAX_JOBS ? batch - j0 : WT_MAX_JOBS;

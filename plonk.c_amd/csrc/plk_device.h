@@ -68,11 +68,9 @@ constexpr uint32_t GENERATOR = 31;           // generates F_p^*
 
 // ----------------------------------------------------------------------------------------
 // F29: p = 7 * 2^26 + 1 = 469762049 < 2^29, Montgomery R = 2^32, values kept LAZILY in
-// [0, 2p).  Because 8p < 2^32, REDC of any product of a value < 4p and one < 2p lands in
-// [0, 2p) with no final subtraction, and sums / differences of two lazy values stay < 4p:
-// a DIF butterfly is 7 VALU (BabyBear: 10).  Exact for poly_mul when every convolution term
-// fits: min(la, lb) * 256 < p, i.e. min(la, lb) <= 1835007 (the 2^20-gate prover's largest
-// product has min = 2^20 + 3); larger products use BabyBear.
+// [0, 8p) (bounds: ntt_wave.hip, F29 policy).  Exact for poly_mul when every convolution sum
+// fits: coefficients enter as centered residues in [-8, 8], so min(la, lb) * 128 < p, i.e.
+// min(la, lb) <= 3670016; larger products use BabyBear.
 // ----------------------------------------------------------------------------------------
 namespace f29 {
 constexpr uint32_t P = 469762049u;           // 7 * 2^26 + 1

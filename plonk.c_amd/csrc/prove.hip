@@ -1324,14 +1324,12 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   const uint64_t shapes[][2] = {{2, L.lz}, {3, L.lz}, {L.lzx, n}};
   for (const auto& s : shapes) ws = std::max(ws, plk_poly_mul_workspace_bytes(s[0], s[1]));
   const uint64_t g1[][2] = {{L.la, L.la}, {L.la, n}, {L.la, n}, {L.la, n}, {L.la, L.la}, {L.la, L.la}, {L.lz1, n},
-                              {L.lzx, n}};
-  const uint64_t g2[][2] = {{L.lab, n}, {L.l2a, L.la}, {L.l2a, L.la}};
-  const uint64_t g3[][2] = {{L.l2b, L.lzx}, {L.l2b, L.lzw}};
-  size_t w1 = 0, w2 = 0, w3 = 0;
+                              {L.lzx, n}, {L.la, L.lzx}, {L.la, L.lzw}};
+  const uint64_t g2[][2] = {{L.lab, n}, {L.l2a, L.la + L.lzx - 1}, {L.l2a, L.la + L.lzw - 1}};
+  size_t w1 = 0, w2 = 0;
   for (const auto& s : g1) w1 += plk_poly_mul_workspace_bytes(s[0], s[1]);
   for (const auto& s : g2) w2 += plk_poly_mul_workspace_bytes(s[0], s[1]);
-  for (const auto& s : g3) w3 += plk_poly_mul_workspace_bytes(s[0], s[1]);
-  ws = std::max(ws, std::max(w1, std::max(w2, w3)));
+  ws = std::max(ws, std::max(w1, w2));
   Bump B;
   const size_t o_srs = B.take(3 * P->srs_len + 16), o_zh = B.take(zl + 16), o_h3 = B.take(3 * n + 16),
                o_hinv = B.take(P->have_circuit_tables ? n * n + 16 : 16), o_S = B.take(NSLOT),
@@ -1490,8 +1488,8 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     RC(pmul(P, dS + P_BLZ, 3, P->d_zh, L.lz, P->zB));
     RC(lincomb(P, {{P->zB, L.lz + 2}, {ACC, n}}, {S_ONE, S_ONE}, -1, -1, S_ONE, -1, cZ, L.lzx));
     // ---- round 3: t(x) numerator (12 poly_mul), src/plonk.h:386-503.  The linear factors
-    // first, then the 12 products in three batches of independent ones (one launch per NTT pass
-    // for a whole batch): 7 first-level products, the 3 products of those, the last 2.
+    // first, then the products in two batches of independent ones (one launch per NTT pass for
+    // a whole batch): 10 at 2n (incl. the 17th and the re-associated C2 z, C3 z(omega x)), 3 at 4n.
     RC(lincomb_batch(P, {
         make_lc({{cA, L.la}}, {S_ONE}, S_GAMMA, S_BETA, S_ALPHA, -1, P->A2, L.la),   // alpha (a + gamma + beta x)
         make_lc({{cB, L.la}}, {S_ONE}, S_GAMMA, S_BK1, S_ONE, -1, P->B2, L.la),      // b + gamma + beta k1 x
@@ -1510,13 +1508,18 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
                                 // the 17th poly_mul, z_x s_sigma_3 (src/plonk.h:560), as z_x * s3:
                                 // its scalar beta z_omega_z (a round-4 value) moves into r(x)'s
                                 // lincomb (S_R3B), so the product joins this batch
-                                {cZ, L.lzx, S3, n, P->P3}};
-    RC(plk_poly_mul_batch_launch(g1, 8, P->work, P->work_bytes, P->st));
-    const PlkPolyMulJob g2[] = {{P->AB, L.lab, QM, n, P->ABQM}, {P->T2a, L.l2a, P->C2, L.la, P->T2b},
-                                {P->T3a, L.l2a, P->C3, L.la, P->T3b}};
+                                {cZ, L.lzx, S3, n, P->P3},
+                                // t_2 = ((A2 B2) C2) z and t_3 = ((A3 B3) C3) z(omega x)
+                                // (src/plonk.h:432-434, 471-473) re-associated as (A2 B2)(C2 z):
+                                // C2 z and C3 z(omega x) join this batch and the 4n products
+                                // come in one batch (associativity over GF(17); the centered F29
+                                // residues hold the 2n x 2n products exactly)
+                                {P->C2, L.la, cZ, L.lzx, P->T2b}, {P->C3, L.la, P->ZW, L.lzw, P->T3b}};
+    RC(plk_poly_mul_batch_launch(g1, 10, P->work, P->work_bytes, P->st));
+    const PlkPolyMulJob g2[] = {{P->AB, L.lab, QM, n, P->ABQM},
+                                {P->T2a, L.l2a, P->T2b, L.la + L.lzx - 1, P->T2},
+                                {P->T3a, L.l2a, P->T3b, L.la + L.lzw - 1, P->T3}};
     RC(plk_poly_mul_batch_launch(g2, 3, P->work, P->work_bytes, P->st));
-    const PlkPolyMulJob g3[] = {{P->T2b, L.l2b, cZ, L.lzx, P->T2}, {P->T3b, L.l2b, P->ZW, L.lzw, P->T3}};
-    RC(plk_poly_mul_batch_launch(g3, 2, P->work, P->work_bytes, P->st));
   }
   // t(x) = numerator / Z_H; t_lo / t_mid / t_hi = poly_slice(t_x, ...) with part n + 2
   // (src/plonk.h:494-519)

@@ -85,16 +85,33 @@ def test_device_api(hip, oracle):
 
 
 @pytest.mark.parametrize("m", [1835007, 1835008])
-def test_field_boundary_worst_case(hip, m):
-    """Products run over F29 (p = 7 2^26 + 1, lazy reduction) while every convolution term
-    fits, min(la, lb) * 256 < p, i.e. min(la, lb) <= 1835007, and over BabyBear above.  All
-    coefficients 16 make every term its maximum: c_i = 256 min(i + 1, la, lb, la + lb - 1 - i),
-    and 256 = 1 (mod 17)."""
+def test_all_sixteen_products(hip, m):
+    """All coefficients 16 (the uncentered maximum: c_i = 256 min(i + 1, la, lb, la + lb - 1 - i),
+    256 = 1 mod 17) at the old uncentered F29 boundary (min(la, lb) * 256 < p); both sides run
+    over F29 now that coefficients enter centered (16 = -1)."""
     la, lb = m, m + 1000
     a = np.full(la, 16, np.uint8)
     b = np.full(lb, 16, np.uint8)
     i = np.arange(la + lb - 1, dtype=np.int64)
     want = (np.minimum(np.minimum(i + 1, la), np.minimum(lb, la + lb - 1 - i)) % 17).astype(np.uint8)
+    nz = np.flatnonzero(want)
+    want = want[:int(nz[-1]) + 1]
+    assert hip.poly_mul(a, b) == want.tobytes()
+
+
+@pytest.mark.parametrize("m", [3670016, 3670017])
+@pytest.mark.parametrize("av,bv", [(9, 9), (9, 8)])
+def test_field_boundary_worst_case(hip, m, av, bv):
+    """Products run over F29 (p = 7 2^26 + 1) with coefficients as centered residues in [-8, 8]
+    while 64 min(la, lb) <= (p - 1) / 2, i.e. min(la, lb) * 128 < p (min <= 3670016), and over
+    BabyBear above (first at 3670017).  9 = -8 and 8 make every term +64 (9 x 9) or -64
+    (9 x 8): the extreme sums c_i = +-64 min(i + 1, la, lb, la + lb - 1 - i) on both sides."""
+    la, lb = m, m + 1000
+    a = np.full(la, av, np.uint8)
+    b = np.full(lb, bv, np.uint8)
+    i = np.arange(la + lb - 1, dtype=np.int64)
+    cnt = np.minimum(np.minimum(i + 1, la), np.minimum(lb, la + lb - 1 - i))
+    want = ((av * bv) * cnt % 17).astype(np.uint8)
     nz = np.flatnonzero(want)
     want = want[:int(nz[-1]) + 1]
     assert hip.poly_mul(a, b) == want.tobytes()
