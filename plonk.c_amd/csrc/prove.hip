@@ -132,6 +132,18 @@ __device__ __forceinline__ void load16(const uint8_t* p, uint64_t len, uint64_t 
     if (i + k < len) w[k >> 2] |= (uint32_t)p[i + k] << (8 * (k & 3));
 }
 
+// p readable in whole 16-byte chunks up to len (16-byte aligned): one unconditional uint4
+// load at a clamped address, bytes past len masked
+__device__ __forceinline__ void load16_masked(const uint8_t* p, uint64_t len, uint64_t i, uint32_t (&w)[4]) {
+  const bool in = i < len;
+  const uint4 q = *reinterpret_cast<const uint4*>(p + (in ? i : 0));
+  const uint32_t v[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int64_t cnt = in ? (int64_t)len - (int64_t)(i + 4 * k) : 0;   // valid bytes in word k
+    w[k] = cnt >= 4 ? v[k] : (cnt <= 0 ? 0u : v[k] & ((1u << (8 * cnt)) - 1u));
+  }
+}
 __global__ __launch_bounds__(256) void lincomb16_kernel(LcArgs a, const uint8_t* __restrict__ S) {
   uint32_t cf[LC_MAX];
 #pragma unroll
@@ -324,7 +336,7 @@ __global__ __launch_bounds__(256) void copy3_kernel(Copy3 c) {
 // ------------------------------------------------------------------ poly_eval (batched)
 // Horner of src/poly.h:265-272 == sum c_i x^i mod 17; x^i = x^(i mod 16) for x != 0.
 constexpr int EV_MAX = 16;
-constexpr int EV_BLOCKS = 256;
+constexpr int EV_BLOCKS = 64;   // x 256 threads x 4 uint4 loads in flight each
 constexpr int TICK_STRIDE = 32;   // one 128-byte line per arrival word
 enum EvPost : int { EV_POST_NONE = 0, EV_POST_ACC = 1, EV_POST_R4 = 4 };
 struct EvArgs {
@@ -359,6 +371,20 @@ __global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict
   const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (x == 0) {                       // poly_eval(p, 0) = p[0]
     if (gid == 0 && n) acc = p[0];
+  } else if (a.vec[e] == 2) {         // readable in whole chunks: 4 loads in flight per thread
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
+    for (uint64_t i0 = gid * 16; i0 < n; i0 += 4 * stride) {
+      uint32_t w[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) load16_masked(p, n, i0 + u * stride, w[u]);
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) s += pw[k] * ((w[u][k >> 2] >> (8 * (k & 3))) & 0xFFu);
+        acc = (acc + s) % HFP;
+      }
+    }
   } else if (a.vec[e]) {              // 16 coefficients per step: i = 0 mod 16 so x^(i+k) = x^k
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
     for (uint64_t i = gid * 16; i < n; i += stride) {
@@ -668,16 +694,6 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_sums_kernel(LinDivs L, const 
 // aggregate sum_{i > 0} num[i] a^i.  Every term is 16-byte aligned and readable in whole 16-byte
 // chunks up to its length (host-checked), so each term's uint4 load is issued unconditionally
 // (clamped address, masked bytes) and all of them are in flight together.
-__device__ __forceinline__ void load16_masked(const uint8_t* p, uint64_t len, uint64_t i, uint32_t (&w)[4]) {
-  const bool in = i < len;
-  const uint4 q = *reinterpret_cast<const uint4*>(p + (in ? i : 0));
-  const uint32_t v[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int64_t cnt = in ? (int64_t)len - (int64_t)(i + 4 * k) : 0;   // valid bytes in word k
-    w[k] = cnt >= 4 ? v[k] : (cnt <= 0 ? 0u : v[k] & ((1u << (8 * cnt)) - 1u));
-  }
-}
 __global__ __launch_bounds__(SCAN_T) void lincomb_scan_kernel(LcBatch b, LinDivs L, const uint8_t* __restrict__ S) {
   const int d = blockIdx.y;
   const LcArgs& a = b.a[d];
@@ -1199,7 +1215,10 @@ int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64
     a.len[e] = std::get<1>(t);
     a.xslot[e] = std::get<2>(t);
     a.out[e] = std::get<3>(t);
-    a.vec[e] = ((uintptr_t)a.p[e] % 16) == 0;
+    // 2: aligned and readable in whole 16-byte chunks (length a multiple of 16, or inside the
+    // prover's own padded allocation); 1: aligned; 0: bytes
+    const bool inside = a.p[e] >= P->mem && a.p[e] < P->mem + P->mem_bytes;
+    a.vec[e] = ((uintptr_t)a.p[e] % 16) != 0 ? 0 : ((a.len[e] % 16 == 0 || inside) ? 2 : 1);
     e++;
   }
   a.ne = e;
