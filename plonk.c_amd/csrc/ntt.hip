@@ -374,6 +374,9 @@ struct TailJob {
   int lt;           // <= 16
   uint64_t base, ntt_len, rl;
   uint8_t* out8;
+  // a sum group's members: the same shape, their own g and t added into the same outputs
+  const uint8_t* g2[2];
+  const uint8_t* t2[2];
 };
 constexpr int TAIL_MAX_JOBS = 12;
 struct TailJobs {
@@ -393,86 +396,95 @@ __device__ __forceinline__ uint32_t bytes_mod17(uint32_t x) {
   return r;
 }
 
-__global__ __launch_bounds__(256) void polymul_tail_batch_kernel(TailJobs J) {
-  const TailJob& jb = J.j[blockIdx.y];
+// 16 outputs' tail sums of one (g, t) pair, added into acc (bytes in packed words)
+__device__ __forceinline__ void tail_pair(const uint8_t* g, uint64_t lg, const uint8_t* t, int lt, int64_t o0,
+                                          int64_t s, bool galign, uint32_t (&acc)[16]) {
   uint32_t Tr[4] = {0, 0, 0, 0};   // byte j' = t[15 - j'] mod 17
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    const uint32_t v = j < jb.lt ? jb.t[j] % 17u : 0u;
+    const uint32_t v = j < lt ? t[j] % 17u : 0u;
     Tr[(15 - j) >> 2] |= v << (8 * ((15 - j) & 3));
   }
-  const uint64_t span = jb.rl - jb.base;
-  uint8_t* const ob = jb.out8 + jb.base;
-  const int64_t d = (int64_t)((uintptr_t)ob & 15);     // chunk c: outputs o in [16c - d, 16c - d + 16)
-  const int64_t s = (int64_t)((1 - d) & 15);           // window start mod 16
-  const bool galign = ((uintptr_t)jb.g & 15) == 0;
-  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 16 * c < span + d;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const int64_t o0 = (int64_t)(16 * c) - d;
-    const int64_t ws = o0 - 15;                        // window bytes g[ws + q], q < 32
-    uint32_t W[8];
-    const int64_t A = ws - s;                          // 16-byte aligned
-    if (galign && A >= 0 && (uint64_t)(A + 48) <= jb.lg) {
-      uint32_t L[12];
+  const int64_t ws = o0 - 15;                        // window bytes g[ws + q], q < 32
+  uint32_t W[8];
+  const int64_t A = ws - s;                          // 16-byte aligned
+  if (galign && A >= 0 && (uint64_t)(A + 48) <= lg) {
+    uint32_t L[12];
 #pragma unroll
-      for (int v = 0; v < 3; v++) {
-        const uint4 q = *reinterpret_cast<const uint4*>(jb.g + A + 16 * v);
-        L[4 * v] = q.x; L[4 * v + 1] = q.y; L[4 * v + 2] = q.z; L[4 * v + 3] = q.w;
-      }
-      const uint32_t r = (uint32_t)(s & 3);
-      switch (s >> 2) {   // uniform
+    for (int v = 0; v < 3; v++) {
+      const uint4 q = *reinterpret_cast<const uint4*>(g + A + 16 * v);
+      L[4 * v] = q.x; L[4 * v + 1] = q.y; L[4 * v + 2] = q.z; L[4 * v + 3] = q.w;
+    }
+    const uint32_t r = (uint32_t)(s & 3);
+    switch (s >> 2) {   // uniform
 #define PLK_TAIL_W(Q)                                                                          \
   case Q:                                                                                     \
     _Pragma("unroll") for (int m = 0; m < 8; m++) W[m] = __builtin_amdgcn_alignbyte(L[Q + m + 1], L[Q + m], r); \
     break;
-        PLK_TAIL_W(0) PLK_TAIL_W(1) PLK_TAIL_W(2) PLK_TAIL_W(3)
+      PLK_TAIL_W(0) PLK_TAIL_W(1) PLK_TAIL_W(2) PLK_TAIL_W(3)
 #undef PLK_TAIL_W
-      }
-    } else {
-#pragma unroll
-      for (int m = 0; m < 8; m++) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-          const int64_t o = ws + 4 * m + b;
-          if (o >= 0 && (uint64_t)o < jb.lg) w |= (uint32_t)jb.g[o] << (8 * b);
-        }
-        W[m] = w;
-      }
     }
-    bool big = false;
+  } else {
 #pragma unroll
-    for (int m = 0; m < 8; m++) big |= bytes_over16(W[m]);
-    if (big) {
+    for (int m = 0; m < 8; m++) {
+      uint32_t w = 0;
 #pragma unroll
-      for (int m = 0; m < 8; m++) W[m] = bytes_mod17(W[m]);
+      for (int b = 0; b < 4; b++) {
+        const int64_t o = ws + 4 * m + b;
+        if (o >= 0 && (uint64_t)o < lg) w |= (uint32_t)g[o] << (8 * b);
+      }
+      W[m] = w;
     }
+  }
+  bool big = false;
+#pragma unroll
+  for (int m = 0; m < 8; m++) big |= bytes_over16(W[m]);
+  if (big) {
+#pragma unroll
+    for (int m = 0; m < 8; m++) W[m] = bytes_mod17(W[m]);
+  }
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const int i = (k >> 2) + m;
+      const uint32_t wd = (k & 3) ? __builtin_amdgcn_alignbyte(W[i + 1], W[i], k & 3) : W[i];
+      acc[k] = __builtin_amdgcn_udot4(Tr[m], wd, acc[k], false);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void polymul_tail_batch_kernel(TailJobs J) {
+  const TailJob& jb = J.j[blockIdx.y];
+  const uint64_t span = jb.rl - jb.base;
+  uint8_t* const ob = jb.out8 + jb.base;
+  const int64_t d = (int64_t)((uintptr_t)ob & 15);     // chunk c: outputs o in [16c - d, 16c - d + 16)
+  const int64_t s = (int64_t)((1 - d) & 15);           // window start mod 16
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 16 * c < span + d;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const int64_t o0 = (int64_t)(16 * c) - d;
     // current outputs (0 where not yet written by the transform)
-    uint32_t cur[4] = {0, 0, 0, 0};
+    uint32_t acc[16];
     const bool full = o0 >= 0 && (uint64_t)(o0 + 16) <= span;
     if (full && jb.base + (uint64_t)o0 + 16 <= jb.ntt_len) {
       const uint4 q = *reinterpret_cast<const uint4*>(ob + o0);
-      cur[0] = q.x; cur[1] = q.y; cur[2] = q.z; cur[3] = q.w;
+      const uint32_t cur[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 0; k < 16; k++) acc[k] = (cur[k >> 2] >> (8 * (k & 3))) & 0xFFu;
     } else {
 #pragma unroll
       for (int k = 0; k < 16; k++) {
         const int64_t o = o0 + k;
-        if (o >= 0 && (uint64_t)o < span && jb.base + (uint64_t)o < jb.ntt_len)
-          cur[k >> 2] |= (uint32_t)ob[o] << (8 * (k & 3));
+        acc[k] = (o >= 0 && (uint64_t)o < span && jb.base + (uint64_t)o < jb.ntt_len) ? ob[o] : 0u;
       }
     }
+    tail_pair(jb.g, jb.lg, jb.t, jb.lt, o0, s, ((uintptr_t)jb.g & 15) == 0, acc);
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+      if (jb.g2[q]) tail_pair(jb.g2[q], jb.lg, jb.t2[q], jb.lt, o0, s, ((uintptr_t)jb.g2[q] & 15) == 0, acc);
     uint32_t res[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      uint32_t acc = (cur[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-#pragma unroll
-      for (int m = 0; m < 4; m++) {
-        const int i = (k >> 2) + m;
-        const uint32_t wd = (k & 3) ? __builtin_amdgcn_alignbyte(W[i + 1], W[i], k & 3) : W[i];
-        acc = __builtin_amdgcn_udot4(Tr[m], wd, acc, false);
-      }
-      res[k >> 2] |= mod17_small(acc) << (8 * (k & 3));
-    }
+    for (int k = 0; k < 16; k++) res[k >> 2] |= mod17_small(acc[k]) << (8 * (k & 3));
     if (full) {
       *reinterpret_cast<uint4*>(ob + o0) = make_uint4(res[0], res[1], res[2], res[3]);
     } else {
@@ -648,6 +660,12 @@ static int product_plan(uint64_t la, uint64_t lb, uint64_t* e_out) {
   return k;
 }
 
+// a product that goes through the transform engine (so it can be a sum-group member)
+bool plk_poly_mul_summable(uint64_t la, uint64_t lb) {
+  const uint64_t mn = la < lb ? la : lb;
+  return la && lb && mn > PLK_DIRECT_MAX && product_plan(la, lb, nullptr) > PLK_SMALL_LOG;
+}
+
 size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb) {
   if (la == 0 || lb == 0) return 0;
   const int k = product_plan(la, lb, nullptr);
@@ -672,8 +690,16 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
   }
   bool use29 = !no29 && k <= f29::TWO_ADICITY;
   for (int i = 0; i < m; i++) {
+    // a sum group of gs products must fit as a whole: gs * 64 min <= (p - 1) / 2
+    int gs = 1;
+    while (i + gs < m && g[i + gs].acc) gs++;
     const uint64_t mn = g[i].la < g[i].lb ? g[i].la : g[i].lb;
-    if (mn * 128 >= f29::P) use29 = false;   // centered residues (ntt_wave.hip F29::from_byte)
+    if ((uint64_t)gs * mn * 128 >= f29::P) use29 = false;   // centered residues (F29::from_byte)
+    if (!use29 && (uint64_t)gs * mn * 256 >= bb::P) {
+      plk_set_error("poly_mul batch: a sum of %d products of %llu coefficients exceeds both fields", gs,
+                    (unsigned long long)mn);
+      return PLK_ERR_RANGE;
+    }
   }
   const uint32_t ninv = use29 ? f29::hpow(1ull << k, f29::P - 2) : bb::hpow(1ull << k, bb::P - 2);   // normal form
   WJob w[64];
@@ -687,25 +713,57 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
     uint32_t* A = (uint32_t*)d_work + ((size_t)2 * i << k);
     w[i] = WJob{lgp, shp, llg - e, lsh, j.out, llg - e + lsh - 1, A, A + (1ull << k)};
   }
+  // sum groups: a member (acc) adds its center output into its leader's first inverse pass
+  int lead[64];
+  for (int i = 0; i < m; i++) {
+    lead[i] = i;
+    if (!g[i].acc) continue;
+    const int L = lead[i - (i > 0)];
+    if (i == 0 || g[L].la != g[i].la || g[L].lb != g[i].lb || (es && es[L] != es[i]) || (w[L].S1 && w[L].S2)) {
+      plk_set_error("poly_mul batch: invalid sum group at job %d", i);
+      return PLK_ERR_ARG;
+    }
+    lead[i] = L;
+    (w[L].S1 ? w[L].S2 : w[L].S1) = w[i].A;
+    w[i].skip_inv = 1;
+  }
   int rc = plk_wave_poly_mul_batch_launch(w, m, k, use29 ? 1 : 0, ninv, st);
   if (rc) return rc;
-  // the tails of the split products, one launch per 8
+  // the tails of the split products (a sum group's in its leader's tail job), one launch per 12
   TailJobs tj{};
-  int nt = 0;
+  int nt = 0, tj_of[64];
   uint64_t maxspan = 0;
   for (int i = 0; i <= m; i++) {
-    if (i < m && es && es[i]) {
-      const uint64_t rl = g[i].la + g[i].lb - 1, sa = w[i].la, lsh = w[i].lb;
-      tj.j[nt++] = TailJob{w[i].b8, lsh, w[i].a8 + sa, (int)es[i], sa, sa + lsh - 1, rl, g[i].out};
-      maxspan = std::max<uint64_t>(maxspan, rl - sa);
+    if (i < m && es && es[i] && g[i].acc) {
+      TailJob& L = tj.j[tj_of[lead[i]]];
+      const int q = L.g2[0] ? 1 : 0;
+      L.g2[q] = w[i].b8;
+      L.t2[q] = w[i].a8 + w[i].la;
+      continue;
     }
-    if (nt && (nt == TAIL_MAX_JOBS || i == m)) {
+    // a group's members follow their leader: flush only between groups
+    if (i < m && es && es[i]) {
+      if (nt == TAIL_MAX_JOBS) {
+        const uint64_t blocks64 = (maxspan + 16 * 256 - 1) / (16 * 256);
+        hipLaunchKernelGGL(polymul_tail_batch_kernel, dim3((unsigned)std::min<uint64_t>(blocks64, 4096), nt), dim3(256),
+                           0, st, tj);
+        PLK_HIP(hipGetLastError());
+        tj = TailJobs{};
+        nt = 0;
+        maxspan = 0;
+      }
+      const uint64_t rl = g[i].la + g[i].lb - 1, sa = w[i].la, lsh = w[i].lb;
+      tj_of[i] = nt;
+      tj.j[nt++] = TailJob{w[i].b8, lsh, w[i].a8 + sa, (int)es[i], sa, sa + lsh - 1, rl, g[i].out, {nullptr, nullptr},
+                           {nullptr, nullptr}};
+      maxspan = std::max<uint64_t>(maxspan, rl - sa);
+      continue;
+    }
+    if (nt && i == m) {
       const uint64_t blocks64 = (maxspan + 16 * 256 - 1) / (16 * 256);
       hipLaunchKernelGGL(polymul_tail_batch_kernel, dim3((unsigned)std::min<uint64_t>(blocks64, 4096), nt), dim3(256), 0,
                          st, tj);
       PLK_HIP(hipGetLastError());
-      nt = 0;
-      maxspan = 0;
     }
   }
   return PLK_OK;
@@ -769,6 +827,10 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
     if (j.la == 0 || j.lb == 0) return PLK_ERR_ARG;
     const uint64_t mn = j.la < j.lb ? j.la : j.lb;
     const int k = product_plan(j.la, j.lb, &es[i]);
+    if (j.acc && !(mn > PLK_DIRECT_MAX && k > PLK_SMALL_LOG)) {
+      plk_set_error("poly_mul batch: sum-group member %d is not a transform-sized product", i);
+      return PLK_ERR_ARG;
+    }
     if (mn > PLK_DIRECT_MAX && k > PLK_SMALL_LOG) {
       if (mn * 256 >= bb::P || k > bb::TWO_ADICITY) return PLK_ERR_RANGE;
       ks[i] = k;

@@ -101,6 +101,10 @@ struct FBB {
   }
   __device__ static __forceinline__ uint32_t mul(uint32_t a, uint32_t b) { return bb::mmul(a, b); }
   __device__ static __forceinline__ uint32_t pmul(uint32_t a, uint32_t b) { return bb::mmul(a, b); }
+  // a + b + c of center outputs (sum groups; c = 0 when absent)
+  __device__ static __forceinline__ uint32_t sum(uint32_t a, uint32_t b, uint32_t c) {
+    return bb::madd(bb::madd(a, b), c);
+  }
   __device__ static __forceinline__ uint32_t colf(uint32_t cl, uint32_t ch) { return bb::mmul(cl, ch); }
   __device__ static __forceinline__ uint32_t from_byte(uint32_t b) { return bb::mmul(b % 17u, bb::R2); }
   __device__ static __forceinline__ uint32_t out17(uint32_t v, uint32_t ninv) { return bb::mmul(v, ninv) % 17u; }
@@ -134,6 +138,10 @@ struct F29 {
     x = a + f29::P2 - xw;
   }
   __device__ static __forceinline__ uint32_t mul(uint32_t a, uint32_t b) { return f29::mmul(a, b); }
+  // a + b + c of center outputs (< 8p each): each brought below 2p, the sum < 6p (c = 0 if absent)
+  __device__ static __forceinline__ uint32_t sum(uint32_t a, uint32_t b, uint32_t c) {
+    return f29::red2(red4(a)) + f29::red2(red4(b)) + f29::red2(red4(c));
+  }
   // a, b < 4p: reduce one below 2p so that a b < p 2^32
   __device__ static __forceinline__ uint32_t pmul(uint32_t a, uint32_t b) { return f29::mmul(a, f29::red2(b)); }
   __device__ static __forceinline__ uint32_t colf(uint32_t cl, uint32_t ch) { return f29::red1(f29::mmul(cl, ch)); }
@@ -358,9 +366,12 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
   const WJob& jb = jobs.j[blockIdx.y];
+  if (jb.skip_inv) return;   // a sum-group member: its leader's pass adds it
   uint32_t* d = jb.A;
   uint8_t* out8 = jb.out8;
   const uint64_t out_len = jb.out_len;
+  const uint32_t* s1 = jb.S1;
+  const uint32_t* s2 = jb.S2;
 
   const uint32_t b0 = G::template base_q<0>(tid, true);
   constexpr int L0 = G::lbq(0, true);
@@ -371,6 +382,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
     const uint32_t e = b0 + ((uint32_t)k << L0);
     const uint64_t idx = G::index(p, tile, e);
     v[k] = d[idx];
+    if (s1) v[k] = F::sum(v[k], s1[idx], s2 ? s2[idx] : 0u);   // uniform branch
     if (G::HIGH) {
       if constexpr (COLT) {
         cl[k] = tw.col[idx];
@@ -629,10 +641,13 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
   hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F>), dim3(grid), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, jobs, twf,
                      (uint32_t)nj);
   PLK_HIP(hipGetLastError());
+  WJobs later = jobs;   // sum groups add their members in the FIRST inverse pass only
+  for (int j = 0; j < nj; j++) later.j[j].S1 = later.j[j].S2 = nullptr;
   for (int i = np - 2; i >= 0; i--) {
     const WPass p{k, lo[i]};
-    rc = i == 0 ? inv_m<TB, true, F>(Ms[i], p, jobs, nj, twf, ninv, st)
-                : inv_m<TB, false, F>(Ms[i], p, jobs, nj, twf, 0u, st);
+    const WJobs& jj = i == np - 2 ? jobs : later;
+    rc = i == 0 ? inv_m<TB, true, F>(Ms[i], p, jj, nj, twf, ninv, st)
+                : inv_m<TB, false, F>(Ms[i], p, jj, nj, twf, 0u, st);
     if (rc) return rc;
   }
   return PLK_OK;

@@ -58,8 +58,13 @@ struct PlkPolyMulJob {
   const uint8_t* b;
   uint64_t lb;
   uint8_t* out;   // la + lb - 1 bytes
+  // 1: ADD this product into the preceding job's output (a sum group: the leader and up to two
+  // members of the same shape, all of one transform size; the members' out is not written).
+  // The sum is exact while it fits the field (the caller's bound).
+  int acc = 0;
 };
 int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, size_t work_bytes, hipStream_t st);
+bool plk_poly_mul_summable(uint64_t la, uint64_t lb);
 
 // ntt_wave.hip (transforms of 2^13 .. 2^27 points).  One product job: u32 work arrays A, B
 // (2^k each), byte inputs a8[0, la), b8[0, lb), byte output out8[0, out_len).
@@ -71,6 +76,11 @@ struct WJob {
   uint64_t out_len;
   uint32_t* A;
   uint32_t* B;
+  // sum groups: the leader's inverse passes add the members' center outputs (linear), the
+  // members run no inverse pass of their own
+  uint32_t* S1 = nullptr;
+  uint32_t* S2 = nullptr;
+  int skip_inv = 0;
 };
 bool plk_wave_ntt_supported(int k);
 // field 0 = BabyBear, 1 = F29 (lazy; only when every job's min(la, lb) * 256 < f29::P);

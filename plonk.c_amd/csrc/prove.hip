@@ -1059,6 +1059,7 @@ struct plk_prover {
   uint32_t* d_stat = nullptr;      // status words
   uint32_t* d_tick = nullptr;      // eval arrival words (zeroed at create, re-armed by eval_kernel)
   uint8_t* d_rem = nullptr;        // Z_H division: one remainder vote per block
+  int lin_sum = 0;                 // round 3: a q_l + b q_r + c q_o computed as one sum (in AQL)
   uint64_t rem_blocks = 0;
   uint32_t* d_bsum = nullptr;      // scan block sums
   PlkMsmResult* d_res = nullptr;   // 9 MSM records
@@ -1520,8 +1521,12 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
         make_lc({{cZ, L.lzx}}, {S_ONE}, S_NEG1, -1, S_ALPHA2, -1, P->Z1, L.lz1)}));  // alpha^2 (z - 1)
   }
   {
+    // a_x q_l + b_x q_r + c_x q_o as ONE sum group (one inverse transform) when the sum fits
+    // F29's centered range: 3 * 64 n <= (p - 1) / 2 (n <= 1,223,338)
+    const int lin = plk_poly_mul_summable(L.la, n) && (uint64_t)3 * L.la * 128 < f29::P ? 1 : 0;
+    P->lin_sum = lin;
     const PlkPolyMulJob g1[] = {{cA, L.la, cB, L.la, P->AB},      {cA, L.la, QL, n, P->AQL},
-                                {cB, L.la, QR, n, P->BQR},        {cC, L.la, QO, n, P->CQO},
+                                {cB, L.la, QR, n, P->BQR, lin},   {cC, L.la, QO, n, P->CQO, lin},
                                 {P->A2, L.la, P->B2, L.la, P->T2a}, {P->A3, L.la, P->B3, L.la, P->T3a},
                                 {P->Z1, L.lz1, L1, n, P->T4},
                                 // the 17th poly_mul, z_x s_sigma_3 (src/plonk.h:560), as z_x * s3:
@@ -1545,25 +1550,34 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   const uint64_t part = n + 2;
   const uint64_t lmid = L.ltx > part ? std::min<uint64_t>(part, L.ltx - part) : 0;
   const uint64_t lhi = L.ltx > 2 * part ? L.ltx - 2 * part : 0;
-  const LcArgs num = make_lc({{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {P->BQR, L.lq1}, {P->CQO, L.lq1}, {QC, n},
-                              {P->T2, L.l2}, {P->T3, L.l3}, {P->T4, L.lt4}},
-                             {S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_NEG1, S_ONE}, -1, -1, S_ONE, -1, P->NUM,
-                             L.lnum);
+  const LcArgs num = P->lin_sum
+                         ? make_lc({{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {QC, n}, {P->T2, L.l2}, {P->T3, L.l3},
+                                    {P->T4, L.lt4}},
+                                   {S_ONE, S_ONE, S_ONE, S_ONE, S_NEG1, S_ONE}, -1, -1, S_ONE, -1, P->NUM, L.lnum)
+                         : make_lc({{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {P->BQR, L.lq1}, {P->CQO, L.lq1}, {QC, n},
+                                    {P->T2, L.l2}, {P->T3, L.l3}, {P->T4, L.lt4}},
+                                   {S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_NEG1, S_ONE}, -1, -1, S_ONE, -1,
+                                   P->NUM, L.lnum);
   // (q_c is the caller's buffer: n % 4 == 0 keeps its last dword inside it; the intermediates
   // carry >= 16 bytes of padding)
-  bool fused = P->zh_kind == 0 && (P->zh_len - 1) % 4 == 0 && L.lnum > P->zh_len - 1 && num.nt == 8 &&
+  bool fused = P->zh_kind == 0 && (P->zh_len - 1) % 4 == 0 && L.lnum > P->zh_len - 1 && (num.nt == 8 || num.nt == 6) &&
                (uintptr_t)P->TX % 4 == 0 && n % 4 == 0 && (P->zh_len - 1) / 4 < (1ull << 31) && L.ltx / (P->zh_len - 1) < 8;
   for (int t = 0; t < num.nt; t++) fused = fused && (uintptr_t)num.p[t] % 4 == 0;
   if (fused) {
     const uint64_t m = P->zh_len - 1, ql = L.ltx, nb = (m / 4 + 255) / 256;
     const Slices3 sl{{cTlo, cTmid, cThi}, {std::min<uint64_t>(part, L.ltx), lmid, lhi}, part};
     const uint64_t cq = ql ? (ql - 1) / m : 0, cr = ql ? (ql - 1) % m : 0;
-    if (cq + 1 <= 4)
-      hipLaunchKernelGGL((numdiv_kernel<8, 4>), dim3((unsigned)nb), dim3(256), 0, P->st, num, dS, m, P->zh_lead, P->zh_c,
-                         P->TX, ql, cq, cr, sl, P->d_rem);
-    else
-      hipLaunchKernelGGL((numdiv_kernel<8, 8>), dim3((unsigned)nb), dim3(256), 0, P->st, num, dS, m, P->zh_lead, P->zh_c,
-                         P->TX, ql, cq, cr, sl, P->d_rem);
+#define PLK_NUMDIV(NT_, K_)                                                                                      \
+  hipLaunchKernelGGL((numdiv_kernel<NT_, K_>), dim3((unsigned)nb), dim3(256), 0, P->st, num, dS, m, P->zh_lead, P->zh_c, \
+                     P->TX, ql, cq, cr, sl, P->d_rem)
+    if (num.nt == 6) {
+      if (cq + 1 <= 4) PLK_NUMDIV(6, 4);
+      else PLK_NUMDIV(6, 8);
+    } else {
+      if (cq + 1 <= 4) PLK_NUMDIV(8, 4);
+      else PLK_NUMDIV(8, 8);
+    }
+#undef PLK_NUMDIV
     PLK_HIP(hipGetLastError());
     P->rem_blocks = nb;   // trim_many_kernel folds the votes into ST_REM_T
   } else {
