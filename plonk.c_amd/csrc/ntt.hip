@@ -362,141 +362,6 @@ __global__ __launch_bounds__(256) void polymul_direct_kernel(const uint8_t* lg, 
   (void)nz;   // trimmed length: trim_kernel
 }
 
-// Batched tails of split products (one launch for a whole product group, blockIdx.y = job):
-// out[i] += sum_{j < lt} t[j] g[i - base - j] for i in [base, rl), out[i] for i >= ntt_len not
-// yet written (taken as 0).  16 outputs per thread, chunks aligned to the OUTPUT (one uint4
-// read-modify-write); the 32-byte g window is funnel-shifted out of three aligned uint4 loads
-// and each output is four v_dot4_u32_u8 of the reversed t against the window's bytes.
-struct TailJob {
-  const uint8_t* g;
-  uint64_t lg;
-  const uint8_t* t;
-  int lt;           // <= 16
-  uint64_t base, ntt_len, rl;
-  uint8_t* out8;
-  // a sum group's members: the same shape, their own g and t added into the same outputs
-  const uint8_t* g2[2];
-  const uint8_t* t2[2];
-};
-constexpr int TAIL_MAX_JOBS = 12;
-struct TailJobs {
-  TailJob j[TAIL_MAX_JOBS];
-};
-
-__device__ __forceinline__ uint32_t mod17_small(uint32_t a) {   // a < 2^13
-  const uint32_t q = (a * 61681u) >> 20;
-  return a - 17u * q;
-}
-// any byte of x above 16 (false positives only next to bytes >= 0x80)
-__device__ __forceinline__ bool bytes_over16(uint32_t x) { return (((x + 0x6F6F6F6Fu) | x) & 0x80808080u) != 0; }
-__device__ __forceinline__ uint32_t bytes_mod17(uint32_t x) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int b = 0; b < 4; b++) r |= (((x >> (8 * b)) & 0xFFu) % 17u) << (8 * b);
-  return r;
-}
-
-// 16 outputs' tail sums of one (g, t) pair, added into acc (bytes in packed words)
-__device__ __forceinline__ void tail_pair(const uint8_t* g, uint64_t lg, const uint8_t* t, int lt, int64_t o0,
-                                          int64_t s, bool galign, uint32_t (&acc)[16]) {
-  uint32_t Tr[4] = {0, 0, 0, 0};   // byte j' = t[15 - j'] mod 17
-#pragma unroll
-  for (int j = 0; j < 16; j++) {
-    const uint32_t v = j < lt ? t[j] % 17u : 0u;
-    Tr[(15 - j) >> 2] |= v << (8 * ((15 - j) & 3));
-  }
-  const int64_t ws = o0 - 15;                        // window bytes g[ws + q], q < 32
-  uint32_t W[8];
-  const int64_t A = ws - s;                          // 16-byte aligned
-  if (galign && A >= 0 && (uint64_t)(A + 48) <= lg) {
-    uint32_t L[12];
-#pragma unroll
-    for (int v = 0; v < 3; v++) {
-      const uint4 q = *reinterpret_cast<const uint4*>(g + A + 16 * v);
-      L[4 * v] = q.x; L[4 * v + 1] = q.y; L[4 * v + 2] = q.z; L[4 * v + 3] = q.w;
-    }
-    const uint32_t r = (uint32_t)(s & 3);
-    switch (s >> 2) {   // uniform
-#define PLK_TAIL_W(Q)                                                                          \
-  case Q:                                                                                     \
-    _Pragma("unroll") for (int m = 0; m < 8; m++) W[m] = __builtin_amdgcn_alignbyte(L[Q + m + 1], L[Q + m], r); \
-    break;
-      PLK_TAIL_W(0) PLK_TAIL_W(1) PLK_TAIL_W(2) PLK_TAIL_W(3)
-#undef PLK_TAIL_W
-    }
-  } else {
-#pragma unroll
-    for (int m = 0; m < 8; m++) {
-      uint32_t w = 0;
-#pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const int64_t o = ws + 4 * m + b;
-        if (o >= 0 && (uint64_t)o < lg) w |= (uint32_t)g[o] << (8 * b);
-      }
-      W[m] = w;
-    }
-  }
-  bool big = false;
-#pragma unroll
-  for (int m = 0; m < 8; m++) big |= bytes_over16(W[m]);
-  if (big) {
-#pragma unroll
-    for (int m = 0; m < 8; m++) W[m] = bytes_mod17(W[m]);
-  }
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-      const int i = (k >> 2) + m;
-      const uint32_t wd = (k & 3) ? __builtin_amdgcn_alignbyte(W[i + 1], W[i], k & 3) : W[i];
-      acc[k] = __builtin_amdgcn_udot4(Tr[m], wd, acc[k], false);
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void polymul_tail_batch_kernel(TailJobs J) {
-  const TailJob& jb = J.j[blockIdx.y];
-  const uint64_t span = jb.rl - jb.base;
-  uint8_t* const ob = jb.out8 + jb.base;
-  const int64_t d = (int64_t)((uintptr_t)ob & 15);     // chunk c: outputs o in [16c - d, 16c - d + 16)
-  const int64_t s = (int64_t)((1 - d) & 15);           // window start mod 16
-  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 16 * c < span + d;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const int64_t o0 = (int64_t)(16 * c) - d;
-    // current outputs (0 where not yet written by the transform)
-    uint32_t acc[16];
-    const bool full = o0 >= 0 && (uint64_t)(o0 + 16) <= span;
-    if (full && jb.base + (uint64_t)o0 + 16 <= jb.ntt_len) {
-      const uint4 q = *reinterpret_cast<const uint4*>(ob + o0);
-      const uint32_t cur[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-      for (int k = 0; k < 16; k++) acc[k] = (cur[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        const int64_t o = o0 + k;
-        acc[k] = (o >= 0 && (uint64_t)o < span && jb.base + (uint64_t)o < jb.ntt_len) ? ob[o] : 0u;
-      }
-    }
-    tail_pair(jb.g, jb.lg, jb.t, jb.lt, o0, s, ((uintptr_t)jb.g & 15) == 0, acc);
-#pragma unroll
-    for (int q = 0; q < 2; q++)
-      if (jb.g2[q]) tail_pair(jb.g2[q], jb.lg, jb.t2[q], jb.lt, o0, s, ((uintptr_t)jb.g2[q] & 15) == 0, acc);
-    uint32_t res[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 16; k++) res[k >> 2] |= mod17_small(acc[k]) << (8 * (k & 3));
-    if (full) {
-      *reinterpret_cast<uint4*>(ob + o0) = make_uint4(res[0], res[1], res[2], res[3]);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        const int64_t o = o0 + k;
-        if (o >= 0 && (uint64_t)o < span) ob[o] = (uint8_t)(res[k >> 2] >> (8 * (k & 3)));
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------ host side
 namespace {
 
@@ -643,9 +508,12 @@ static int log2_ceil(uint64_t v) {
 }
 
 // NTT size of a product.  A result just above a power of two (la + lb - 1 = 2^K + e, e small,
-// as every prover shape n+2, 2n+3, 4n+6 at n = 2^m is) is split: the longer operand's last e
-// coefficients t are taken out, the rest times the other operand fills exactly 2^K, and
-// x^(la-e) t(x) b(x) is added by polymul_tail_batch_kernel -- half the transform size for O(e n) MACs.
+// as every prover shape n+2, 2n+3, 4n+6 at n = 2^m is) is WRAPPED: the full operands go
+// through a cyclic transform of 2^K points, so c[2^K + j] (j < e) lands on c[j] (each cyclic
+// output still sums at most min(la, lb) terms: exactness bounds unchanged).  Those top e
+// coefficients involve only the operands' last e coefficients (e - j terms each): the last
+// inverse pass computes them from the bytes and corrects both ends -- half the transform
+// size for O(e^2) MACs.
 constexpr uint64_t PLK_SPLIT_MAX = 16;
 static int product_plan(uint64_t la, uint64_t lb, uint64_t* e_out) {
   const uint64_t rl = la + lb - 1;
@@ -679,8 +547,7 @@ static size_t pass_lds(int M, int C, bool center) {
 }
 
 // m products of one transform size 2^k through the wave engine (workspace 2^(k+3) bytes each);
-// es[i] > 0: the split plan (product_plan) -- the longer operand's last es[i] coefficients are
-// multiplied in directly by polymul_tail_batch_kernel after the transform.
+// es[i] > 0: a wrapped product (product_plan) with es[i] top coefficients.
 static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, void* d_work, hipStream_t st) {
   // F29 (lazy reduction, fewer VALU per butterfly) whenever every convolution term fits it
   static int no29 = -1;
@@ -702,71 +569,69 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
     }
   }
   const uint32_t ninv = use29 ? f29::hpow(1ull << k, f29::P - 2) : bb::hpow(1ull << k, bb::P - 2);   // normal form
+  // operands: job i owns slots 2i (a) and 2i+1 (b) of d_work; an operand equal (same bytes,
+  // same length) to an earlier one of the group reuses that slot's transform
+  static int noshare = -1;
+  if (noshare < 0) {
+    const char* e = getenv("PLK_NTT_NO_SHARE");
+    noshare = e && atoi(e) != 0;
+  }
+  uint32_t* W = (uint32_t*)d_work;
+  int slot[64][2], refs[128] = {0};
+  for (int i = 0; i < m; i++)
+    for (int s = 0; s < 2; s++) {
+      const uint8_t* ptr = s ? g[i].b : g[i].a;
+      const uint64_t len = s ? g[i].lb : g[i].la;
+      slot[i][s] = 2 * i + s;
+      for (int q = 0; q <= i && !noshare; q++)
+        for (int t = 0; t < 2 && (q < i || t < s); t++)
+          if ((t ? g[q].b : g[q].a) == ptr && (t ? g[q].lb : g[q].la) == len && slot[q][t] == 2 * q + t) {
+            slot[i][s] = 2 * q + t;
+            q = i + 1;
+            break;
+          }
+      refs[slot[i][s]]++;
+    }
+  // the center output of job i goes to an operand slot only job i reads, else to a free slot
+  int cslot[64], nfree = 0, freel[128];
+  for (int x = 0; x < 2 * m; x++)
+    if (!refs[x]) freel[nfree++] = x;
+  for (int i = 0; i < m; i++) {
+    cslot[i] = -1;
+    for (int s = 0; s < 2 && cslot[i] < 0; s++)
+      if (slot[i][s] == 2 * i + s && refs[2 * i + s] == 1) cslot[i] = 2 * i + s;
+    if (cslot[i] < 0) {
+      if (!nfree) {   // (cannot happen: every shared reference leaves a slot unused)
+        plk_set_error("poly_mul batch: no free work array for job %d", i);
+        return PLK_ERR_ARG;
+      }
+      cslot[i] = freel[--nfree];
+    }
+  }
   WJob w[64];
   for (int i = 0; i < m; i++) {
     const PlkPolyMulJob& j = g[i];
     const uint64_t e = es ? es[i] : 0;
-    const bool swap = e && j.lb > j.la;                   // a := the longer operand when splitting
-    const uint8_t* lgp = swap ? j.b : j.a;
-    const uint8_t* shp = swap ? j.a : j.b;
-    const uint64_t llg = swap ? j.lb : j.la, lsh = swap ? j.la : j.lb;
-    uint32_t* A = (uint32_t*)d_work + ((size_t)2 * i << k);
-    w[i] = WJob{lgp, shp, llg - e, lsh, j.out, llg - e + lsh - 1, A, A + (1ull << k)};
+    w[i] = WJob{j.a, j.b, j.la, j.lb, j.out, j.la + j.lb - 1 - e, W + ((size_t)slot[i][0] << k),
+                W + ((size_t)slot[i][1] << k), W + ((size_t)cslot[i] << k)};
+    w[i].ntop = (int)e;
   }
   // sum groups: a member (acc) adds its center output into its leader's first inverse pass
-  int lead[64];
-  for (int i = 0; i < m; i++) {
-    lead[i] = i;
-    if (!g[i].acc) continue;
-    const int L = lead[i - (i > 0)];
-    if (i == 0 || g[L].la != g[i].la || g[L].lb != g[i].lb || (es && es[L] != es[i]) || (w[L].S1 && w[L].S2)) {
+  for (int i = 0, L = 0; i < m; i++) {
+    if (!g[i].acc) {
+      L = i;
+      continue;
+    }
+    if (i == 0 || g[L].la != g[i].la || g[L].lb != g[i].lb || (es && es[L] != es[i]) || w[L].ngroup == 2) {
       plk_set_error("poly_mul batch: invalid sum group at job %d", i);
       return PLK_ERR_ARG;
     }
-    lead[i] = L;
-    (w[L].S1 ? w[L].S2 : w[L].S1) = w[i].A;
+    (w[L].ngroup ? w[L].S2 : w[L].S1) = w[i].C;
+    w[L].ga8[w[L].ngroup] = w[i].a8;
+    w[L].gb8[w[L].ngroup++] = w[i].b8;
     w[i].skip_inv = 1;
   }
-  int rc = plk_wave_poly_mul_batch_launch(w, m, k, use29 ? 1 : 0, ninv, st);
-  if (rc) return rc;
-  // the tails of the split products (a sum group's in its leader's tail job), one launch per 12
-  TailJobs tj{};
-  int nt = 0, tj_of[64];
-  uint64_t maxspan = 0;
-  for (int i = 0; i <= m; i++) {
-    if (i < m && es && es[i] && g[i].acc) {
-      TailJob& L = tj.j[tj_of[lead[i]]];
-      const int q = L.g2[0] ? 1 : 0;
-      L.g2[q] = w[i].b8;
-      L.t2[q] = w[i].a8 + w[i].la;
-      continue;
-    }
-    // a group's members follow their leader: flush only between groups
-    if (i < m && es && es[i]) {
-      if (nt == TAIL_MAX_JOBS) {
-        const uint64_t blocks64 = (maxspan + 16 * 256 - 1) / (16 * 256);
-        hipLaunchKernelGGL(polymul_tail_batch_kernel, dim3((unsigned)std::min<uint64_t>(blocks64, 4096), nt), dim3(256),
-                           0, st, tj);
-        PLK_HIP(hipGetLastError());
-        tj = TailJobs{};
-        nt = 0;
-        maxspan = 0;
-      }
-      const uint64_t rl = g[i].la + g[i].lb - 1, sa = w[i].la, lsh = w[i].lb;
-      tj_of[i] = nt;
-      tj.j[nt++] = TailJob{w[i].b8, lsh, w[i].a8 + sa, (int)es[i], sa, sa + lsh - 1, rl, g[i].out, {nullptr, nullptr},
-                           {nullptr, nullptr}};
-      maxspan = std::max<uint64_t>(maxspan, rl - sa);
-      continue;
-    }
-    if (nt && i == m) {
-      const uint64_t blocks64 = (maxspan + 16 * 256 - 1) / (16 * 256);
-      hipLaunchKernelGGL(polymul_tail_batch_kernel, dim3((unsigned)std::min<uint64_t>(blocks64, 4096), nt), dim3(256), 0,
-                         st, tj);
-      PLK_HIP(hipGetLastError());
-    }
-  }
-  return PLK_OK;
+  return plk_wave_poly_mul_batch_launch(w, m, k, use29 ? 1 : 0, ninv, st);
 }
 
 // d_out must hold la+lb-1 bytes; *d_nz (if not NULL) receives the trimmed length (0 means "all zero" ->

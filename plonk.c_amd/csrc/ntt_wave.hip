@@ -72,6 +72,17 @@ constexpr int WT_MAX_JOBS = 12;
 struct WJobs {
   WJob j[WT_MAX_JOBS];
 };
+// the distinct arrays of a batch that forward passes transform in place (a product's two
+// operands, or one standalone transform): u32 array d, first pass from bytes s8[0, ls)
+struct WArr {
+  uint32_t* d;
+  const uint8_t* s8;
+  uint64_t ls;
+};
+constexpr int WT_MAX_ARRS = 2 * WT_MAX_JOBS;
+struct WArrs {
+  WArr a[WT_MAX_ARRS];
+};
 
 struct WTw {
   const uint32_t* small;   // T[2^j + r] = w_{2^(j+1)}^r (Montgomery), 2^PLK_NTT_SMALL_LOG entries
@@ -299,23 +310,22 @@ __device__ __forceinline__ void load_pass_tw(uint32_t* Tsm, const uint32_t* smal
 
 }  // namespace
 
-// Forward (DIF) pass over ARR (1 or 2) arrays of each job (blockIdx.y = job * ARR + array),
-// u32 in place, or the first pass reading bytes (zero padded, reduced mod 17, to Montgomery).
+// Forward (DIF) pass over a batch's distinct arrays (blockIdx.y = array), u32 in place, or
+// the first pass reading bytes (zero padded, reduced mod 17, to Montgomery).
 // COLT: the column factors come from tw.col (one word per element, indexed like the data)
 // instead of lo * hi (two words and a multiply per element).
-template <int TB, int R, int M, bool FROM_U8, int ARR, class F, bool COLT = false>
-__global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WJobs jobs, WTw tw) {
+template <int TB, int R, int M, bool FROM_U8, class F, bool COLT = false>
+__global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, WTw tw) {
   using G = Eng<TB, R, M, F>;
   static_assert(G::NT == wt_nt(TB), "tile block size");
   __shared__ uint32_t Tsm[1 << M];
   __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
-  const WJob& jb = jobs.j[blockIdx.y / ARR];
-  const bool second = ARR == 2 && (blockIdx.y & 1);
-  uint32_t* d = second ? jb.B : jb.A;
-  const uint8_t* s8 = second ? jb.b8 : jb.a8;
-  const uint64_t ls = second ? jb.lb : jb.la;
+  const WArr& ar = arrs.a[blockIdx.y];
+  uint32_t* d = ar.d;
+  const uint8_t* s8 = ar.s8;
+  const uint64_t ls = ar.ls;
 
   const uint32_t b0 = G::template base_q<0>(tid, false);
   constexpr int L0 = G::lbq(0, false);
@@ -355,7 +365,31 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WJobs jobs, 
   }
 }
 
-// Inverse (DIT) pass, u32 in place; the final pass (TO_U8) scales by N^-1 (normal form,
+
+// Wrapped products (la + lb - 1 = N + ntop): the last inverse pass wrote c[j] + c[N + j] mod 17
+// at j < ntop.  c[N + j] (sum group: of the group's sum) has only the terms a[i] b[N + j - i]
+// with i >= la - ntop + j (ntop - j <= 16 of them): computed from the bytes by the few threads
+// that hold such j, after the pass's stores (a rare path outside the unrolled store loop).
+template <class G>
+__device__ __forceinline__ void wrap_fix(const WJob& jb, uint32_t wrapped, const WPass& p, uint32_t tile, uint32_t bf,
+                                      int LF, uint64_t N) {
+  for (int k = 0; k < G::E; k++) {
+    if (!(wrapped >> k & 1)) continue;
+    const uint64_t idx = G::index(p, tile, bf + ((uint32_t)k << LF));
+    const uint64_t j = (N - idx) & (N - 1);
+    uint32_t s = 0;
+    for (int g = 0; g <= jb.ngroup; g++) {
+      const uint8_t* a = g ? jb.ga8[g - 1] : jb.a8;
+      const uint8_t* b = g ? jb.gb8[g - 1] : jb.b8;
+      for (uint64_t i = jb.la - (uint64_t)jb.ntop + j; i < jb.la; i++) s += (a[i] % 17u) * (b[N + j - i] % 17u);
+    }
+    s %= 17u;
+    jb.out8[j] = (uint8_t)((jb.out8[j] + 17u - s) % 17u);
+    jb.out8[N + j] = (uint8_t)s;
+  }
+}
+
+// Inverse (DIT) pass, u32 in place (the job's C); the final pass (TO_U8) scales by N^-1 (normal form,
 // which also leaves Montgomery form), reduces mod 17 and writes bytes for idx < out_len.
 template <int TB, int R, int M, bool TO_U8, class F, bool COLT = false>
 __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, WTw tw, uint32_t ninv) {
@@ -367,7 +401,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   const uint32_t tile = block_tile();
   const WJob& jb = jobs.j[blockIdx.y];
   if (jb.skip_inv) return;   // a sum-group member: its leader's pass adds it
-  uint32_t* d = jb.A;
+  uint32_t* d = jb.C;
   uint8_t* out8 = jb.out8;
   const uint64_t out_len = jb.out_len;
   const uint32_t* s1 = jb.S1;
@@ -405,6 +439,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   G::template pass<true>(v, tid, bufs, 0, Tsm);
   constexpr int LF = G::lbq(G::NR - 1, true);
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, true);
+  uint32_t wrapped = 0;   // elements of this thread that hold c[j] + c[N + j] (j < ntop)
 #pragma unroll
   for (int k = 0; k < G::E; k++) {
     const uint64_t idx = G::index(p, tile, bf + ((uint32_t)k << LF));
@@ -414,13 +449,19 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
       // poly_mul runs its inverse with the FORWARD roots (no inverse table in LDS): that
       // yields N c[-idx mod N], so the coefficient lands at the negated position
       const uint64_t j = ((1ull << p.k) - idx) & ((1ull << p.k) - 1);
-      if (j < out_len) out8[j] = (uint8_t)F::out17(v[k], ninv);
+      if (j < out_len) {
+        const uint32_t r = F::out17(v[k], ninv);
+        out8[j] = (uint8_t)r;
+        if (j < (uint64_t)jb.ntop) wrapped |= 1u << k;
+      }
     }
   }
+  if (TO_U8 && wrapped) wrap_fix<G>(jb, wrapped, p, tile, bf, LF, 1ull << p.k);
 }
 
 // Center of poly_mul: last forward pass (lo = 0) of a and b, pointwise product, first
-// inverse pass, all in registers of one block; result written over a.  The last DIF round
+// inverse pass, all in registers of one block; result written to the job's C (A, B or a
+// free array: A and B may be read by other jobs of the batch).  The last DIF round
 // and the first DIT round both have local bits [0, R), so no exchange sits in between.
 // Stage twiddles: ONE table T in LDS (2^TB words): the inverse runs with the forward roots
 // (the DIT of the forward DFT; the final pass negates output positions, wt_inv_kernel), which
@@ -446,8 +487,9 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
   bool first = true;
   for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
     const uint32_t job = it / tiles, tile = it - job * tiles;
-    uint32_t* d0 = jobs.j[job].A;
+    const uint32_t* d0 = jobs.j[job].A;
     const uint32_t* d1 = jobs.j[job].B;
+    uint32_t* dc = jobs.j[job].C;
     uint32_t va[G::E], vb[G::E];
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
@@ -466,7 +508,7 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
     for (int k = 0; k < G::E; k++) va[k] = F::pmul(va[k], vb[k]);
     G::template pass<true>(va, tid, bufs, 2 * G::XCH, Tf);
 #pragma unroll
-    for (int k = 0; k < G::E; k++) d0[G::index(p, tile, bf + ((uint32_t)k << LF))] = va[k];
+    for (int k = 0; k < G::E; k++) dc[G::index(p, tile, bf + ((uint32_t)k << LF))] = va[k];
   }
 }
 
@@ -539,18 +581,17 @@ WTw fwd_wtw(int k) {
 // the table path applies to the pass whose bits reach the top (lo + M = k): a plan's first
 // forward and last inverse pass; byte-input forward / byte-output inverse or single-array
 // forward passes are the only ones instantiated with it
-template <int TB, int M, bool U8, int ARR, class F>
-void launch_fwd(WPass p, const WJobs& jobs, int nj, WTw tw, hipStream_t st) {
+template <int TB, int M, bool U8, class F>
+void launch_fwd(WPass p, const WArrs& arrs, int na, WTw tw, hipStream_t st) {
   constexpr int R = wt_r(TB);
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB);
-  if constexpr (M < TB && (U8 || ARR == 1)) {
+  if constexpr (M < TB) {
     if (tw.col && p.lo + M == p.k) {
-      hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, ARR, F, true>), dim3(tiles, ARR * nj), dim3(wt_nt(TB)), 0, st, p,
-                         jobs, tw);
+      hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, F, true>), dim3(tiles, na), dim3(wt_nt(TB)), 0, st, p, arrs, tw);
       return;
     }
   }
-  hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, ARR, F>), dim3(tiles, ARR * nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw);
+  hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, F>), dim3(tiles, na), dim3(wt_nt(TB)), 0, st, p, arrs, tw);
 }
 template <int TB, int M, bool U8, class F>
 void launch_inv(WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipStream_t st) {
@@ -567,9 +608,9 @@ void launch_inv(WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipSt
 }
 
 // pass widths: 1..8 for both tile sizes, 9..10 for 2^13 tiles, M = TB for the lo = 0 pass
-template <int TB, bool U8, int ARR, class F>
-int fwd_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, hipStream_t st) {
-#define PLK_FWD(m) launch_fwd<TB, m, U8, ARR, F>(p, jobs, nj, tw, st)
+template <int TB, bool U8, class F>
+int fwd_m(int M, WPass p, const WArrs& arrs, int na, WTw tw, hipStream_t st) {
+#define PLK_FWD(m) launch_fwd<TB, m, U8, F>(p, arrs, na, tw, st)
   switch (M) {
     case 1: PLK_FWD(1); break;
     case 2: PLK_FWD(2); break;
@@ -585,7 +626,7 @@ int fwd_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, hipStream_t st) {
         if (M == 10) { PLK_FWD(10); break; }
       }
       if constexpr (!U8) {
-        if (M == TB) { launch_fwd<TB, TB, false, ARR, F>(p, jobs, nj, tw, st); break; }
+        if (M == TB) { launch_fwd<TB, TB, false, F>(p, arrs, na, tw, st); break; }
       }
       plk_set_error("wave plan: unsupported pass width %d (tile bits %d)", M, TB);
       return PLK_ERR_ARG;
@@ -630,10 +671,20 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
   const int np = wave_plan(k, TB, Ms);
   int lo[4];
   for (int i = 0, top = k; i < np; i++) { lo[i] = top - Ms[i]; top = lo[i]; }
+  // the distinct operand arrays (jobs may share one)
+  WArrs arrs{};
+  int na = 0;
+  for (int j = 0; j < nj; j++)
+    for (int s = 0; s < 2; s++) {
+      const WArr a = s ? WArr{jobs.j[j].B, jobs.j[j].b8, jobs.j[j].lb} : WArr{jobs.j[j].A, jobs.j[j].a8, jobs.j[j].la};
+      bool seen = false;
+      for (int q = 0; q < na; q++) seen |= arrs.a[q].d == a.d;
+      if (!seen) arrs.a[na++] = a;
+    }
   int rc;
   for (int i = 0; i < np - 1; i++) {
     const WPass p{k, lo[i]};
-    rc = i == 0 ? fwd_m<TB, true, 2, F>(Ms[i], p, jobs, nj, twf, st) : fwd_m<TB, false, 2, F>(Ms[i], p, jobs, nj, twf, st);
+    rc = i == 0 ? fwd_m<TB, true, F>(Ms[i], p, arrs, na, twf, st) : fwd_m<TB, false, F>(Ms[i], p, arrs, na, twf, st);
     if (rc) return rc;
   }
   const uint32_t tiles = (uint32_t)((1ull << k) >> TB);
@@ -654,7 +705,7 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
 }
 
 template <int TB>
-int wave_ntt_t(const WJobs& jobs, int nj, int k, int inverse, hipStream_t st) {
+int wave_ntt_t(const WJobs& jobs, const WArrs& arrs, int nj, int k, int inverse, hipStream_t st) {
   const PlkTwTables t = plk_ntt_tables();
   int Ms[4];
   const int np = wave_plan(k, TB, Ms);
@@ -664,7 +715,7 @@ int wave_ntt_t(const WJobs& jobs, int nj, int k, int inverse, hipStream_t st) {
     const int i = inverse ? np - 1 - s : s;
     const WPass p{k, lo[i]};
     const int rc = inverse ? inv_m<TB, false, FBB>(Ms[i], p, jobs, nj, to_wtw(t, true), 0u, st)
-                           : fwd_m<TB, false, 1, FBB>(Ms[i], p, jobs, nj, fwd_wtw<FBB>(k), st);
+                           : fwd_m<TB, false, FBB>(Ms[i], p, arrs, nj, fwd_wtw<FBB>(k), st);
     if (rc) return rc;
   }
   return PLK_OK;
@@ -723,8 +774,11 @@ int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t 
   for (int j0 = 0; j0 < batch; j0 += WT_MAX_JOBS) {
     const int m = batch - j0 < WT_MAX_JOBS ? batch - j0 : WT_MAX_JOBS;
     WJobs w{};
-    for (int i = 0; i < m; i++) w.j[i].A = d + ((uint64_t)(j0 + i) << k);
-    const int rc = tile_bits(k) == 13 ? wave_ntt_t<13>(w, m, k, inverse, st) : wave_ntt_t<12>(w, m, k, inverse, st);
+    WArrs a{};
+    for (int i = 0; i < m; i++) {
+      w.j[i].A = w.j[i].C = a.a[i].d = d + ((uint64_t)(j0 + i) << k);
+    }
+    const int rc = tile_bits(k) == 13 ? wave_ntt_t<13>(w, a, m, k, inverse, st) : wave_ntt_t<12>(w, a, m, k, inverse, st);
     if (rc) return rc;
   }
   return PLK_OK;

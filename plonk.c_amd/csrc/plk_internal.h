@@ -67,20 +67,29 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
 bool plk_poly_mul_summable(uint64_t la, uint64_t lb);
 
 // ntt_wave.hip (transforms of 2^13 .. 2^27 points).  One product job: u32 work arrays A, B
-// (2^k each), byte inputs a8[0, la), b8[0, lb), byte output out8[0, out_len).
+// (2^k each; a batch's jobs may share one when their operands are the same bytes), byte
+// inputs a8[0, la), b8[0, lb), byte output out8[0, out_len + ntop).
 struct WJob {
   const uint8_t* a8;
   const uint8_t* b8;
   uint64_t la, lb;
   uint8_t* out8;
-  uint64_t out_len;
+  uint64_t out_len;                // outputs of the cyclic transform: min(la + lb - 1, 2^k)
   uint32_t* A;
   uint32_t* B;
+  uint32_t* C = nullptr;           // center output and inverse work array (read by no other job)
   // sum groups: the leader's inverse passes add the members' center outputs (linear), the
   // members run no inverse pass of their own
   uint32_t* S1 = nullptr;
   uint32_t* S2 = nullptr;
   int skip_inv = 0;
+  // wrapped products (la + lb - 1 = 2^k + ntop): the top ntop coefficients alias onto the
+  // first ntop; the last inverse pass computes them from the bytes (also the sum group's
+  // members' ga8/gb8) and corrects both ends
+  int ntop = 0;
+  int ngroup = 0;
+  const uint8_t* ga8[2] = {nullptr, nullptr};
+  const uint8_t* gb8[2] = {nullptr, nullptr};
 };
 bool plk_wave_ntt_supported(int k);
 // field 0 = BabyBear, 1 = F29 (lazy; only when every job's min(la, lb) * 256 < f29::P);

@@ -39,9 +39,12 @@ SHAPES = [(1, 1), (33, 33), (32, 1000), (33, 1000), (2048, 2049), (2049, 2048), 
           (4097, 33), (3000, 5000), (1 << 12, 1 << 12), ((1 << 13) + 1, 999),
           (1 << 15, (1 << 15) + 1), (100000, 3), (70000, 90000), ((1 << 19), (1 << 19)),
           ((1 << 20) + 3, (1 << 20) + 5), (3 * (1 << 20) + 4, (1 << 20) + 3),
-          # split products: la + lb - 1 = 2^K + e, e <= 16 (tail of the longer operand direct)
+          # wrapped products: la + lb - 1 = 2^K + e, e <= 16 (cyclic 2^K transform, the top e
+          # coefficients computed directly)
           (4097, 4100), (8193, 8196), (8196, 8193), (8200, 8201), (8200, 8202), (16386, 100),
           ((1 << 16) + 2, (1 << 16)), (3 * (1 << 14) + 4, (1 << 14) + 3)]
+# every wrap width e = 1..16 against the shortest transform-path operand (33 coefficients), both orders
+SHAPES += [((1 << 13) - 32 + e, 33)[::1 if e % 2 else -1] for e in range(1, 17)]
 
 
 @pytest.mark.parametrize("la,lb", SHAPES)
