@@ -657,7 +657,36 @@ struct LinDiv {
   uint8_t* q;
   uint32_t* flag;
   uint32_t* bsum;
+  int vec;             // num and q 16-byte aligned: uint4 loads / stores
 };
+
+// wave-level (64 lanes) sums by cross-lane shuffles: no LDS, no barrier
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+// inclusive suffix sum: lane l gets the sum over lanes l .. 63
+__device__ __forceinline__ uint32_t wave_suffix(uint32_t x) {
+  const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_down(x, d, 64);
+    if (lane + d < 64) x += v;
+  }
+  return x;
+}
+// block sum of SCAN_T threads' values (< 2^26 / SCAN_T each) for thread 0: wave sums + one barrier
+__device__ __forceinline__ uint32_t scan_block_sum(uint32_t x) {
+  __shared__ uint32_t ws[SCAN_T / 64];
+  x = wave_sum(x);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = x;
+  __syncthreads();
+  uint32_t t = 0;
+#pragma unroll
+  for (int u = 0; u < SCAN_T / 64; u++) t += ws[u];
+  return t;
+}
 struct LinDivs {
   LinDiv d[2];
 };
@@ -679,14 +708,8 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_sums_kernel(LinDivs L, const 
     const uint64_t i = base + (uint64_t)k * SCAN_T;
     if (i < nl && i > 0) acc += num[i] * pw[i & 15];
   }
-  __shared__ uint32_t red[SCAN_T];
-  red[threadIdx.x] = acc % HFP;
-  __syncthreads();
-  for (int s = SCAN_T / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) D.bsum[blockIdx.x] = red[0] % HFP;
+  const uint32_t t = scan_block_sum(acc % HFP);
+  if (threadIdx.x == 0) D.bsum[blockIdx.x] = t % HFP;
 }
 
 // Round 5's two numerators (w_z(x)'s lincomb, z(x) - z_omega_z) and the scan's block aggregates
@@ -737,17 +760,13 @@ __global__ __launch_bounds__(SCAN_T) void lincomb_scan_kernel(LcBatch b, LinDivs
     for (int k = 0; k < 16; k++)
       if (i + k < a.out_len) a.out[i + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
   }
-  __shared__ uint32_t red[SCAN_T];
-  red[threadIdx.x] = agg % HFP;
-  __syncthreads();
-  for (int s2 = SCAN_T / 2; s2 > 0; s2 >>= 1) {
-    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) D.bsum[blockIdx.x] = red[0] % HFP;
+  const uint32_t t = scan_block_sum(agg % HFP);
+  if (threadIdx.x == 0) D.bsum[blockIdx.x] = t % HFP;
 }
 
-// divisor x - a (d1 = 1, d0 = -a): q[j] = a^-(j+1) sum_{i>j} num[i] a^i, rem = num[0] + a q[0]
+// divisor x - a (d1 = 1, d0 = -a): q[j] = a^-(j+1) sum_{i>j} num[i] a^i, rem = num[0] + a q[0].
+// The block's suffix sums by wave shuffles; the carry (the aggregates of every block after this
+// one, from the sums phase) reduced in the same pass: ONE barrier per block.
 __global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(LinDivs L, const uint8_t* __restrict__ S) {
   const LinDiv& D = L.d[blockIdx.y];
   if ((int)blockIdx.x >= D.nb) return;
@@ -760,55 +779,56 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(LinDivs L, const
   const uint32_t ai = hinv(a);
 #pragma unroll
   for (int j = 1; j < 16; j++) { pw[j] = pw[j - 1] * a % HFP; ipw[j] = ipw[j - 1] * ai % HFP; }
-  // thread owns SCAN_E consecutive elements [base, base + SCAN_E)
+  // thread owns SCAN_E = 16 consecutive elements [base, base + 16): base % 16 = 0
   const uint64_t base = (uint64_t)blockIdx.x * SCAN_B + (uint64_t)threadIdx.x * SCAN_E;
+  uint32_t nb8[4] = {0, 0, 0, 0};
+  if (D.vec) {
+    load16(num, nl, base, nb8);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      if (base + k < nl) nb8[k >> 2] |= (uint32_t)num[base + k] << (8 * (k & 3));
+  }
   uint32_t w[SCAN_E];
   uint32_t tot = 0;
 #pragma unroll
   for (int k = 0; k < SCAN_E; k++) {
     const uint64_t i = base + k;
-    w[k] = (i < nl && i > 0) ? num[i] * pw[i & 15] % HFP : 0u;
+    w[k] = (i > 0) ? ((nb8[k >> 2] >> (8 * (k & 3))) & 0xFFu) * pw[k] % HFP : 0u;
     tot += w[k];
   }
-  __shared__ uint32_t t[SCAN_T];
-  t[threadIdx.x] = tot % HFP;
-  __syncthreads();
-  for (int s = 1; s < SCAN_T; s <<= 1) {
-    const uint32_t add = (int)threadIdx.x + s < SCAN_T ? t[threadIdx.x + s] : 0u;
-    __syncthreads();
-    t[threadIdx.x] = (t[threadIdx.x] + add) % HFP;
-    __syncthreads();
-  }
-  // the block's carry: the aggregates of every block after it (sums kernel), reduced here --
-  // no separate carry-scan launch
-  __shared__ uint32_t cs[SCAN_T];
-  {
-    uint32_t c = 0;
-    for (int b = (int)blockIdx.x + 1 + (int)threadIdx.x; b < D.nb; b += SCAN_T) c += D.bsum[b];
-    cs[threadIdx.x] = c % HFP;
+  uint32_t c = 0;
+  for (int b = (int)blockIdx.x + 1 + (int)threadIdx.x; b < D.nb; b += SCAN_T) c += D.bsum[b];
+  const uint32_t suf = wave_suffix(tot);   // this lane's chunk and every later lane's
+  const uint32_t cw = wave_sum(c % HFP);
+  __shared__ uint32_t ws[2][SCAN_T / 64];
+  const int wv = (int)(threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0) {
+    ws[0][wv] = suf;   // lane 0: the wave's total
+    ws[1][wv] = cw;
   }
   __syncthreads();
-  for (int k = SCAN_T / 2; k > 0; k >>= 1) {
-    if ((int)threadIdx.x < k) cs[threadIdx.x] += cs[threadIdx.x + k];
-    __syncthreads();
-  }
-  // sum of w over elements after this thread's chunk
-  uint32_t run = ((int)threadIdx.x + 1 < SCAN_T ? t[threadIdx.x + 1] : 0u) + cs[0] % HFP;
+  uint32_t run = suf - tot;   // sum of w over elements after this thread's chunk
+#pragma unroll
+  for (int u = 0; u < SCAN_T / 64; u++) run += (u > wv ? ws[0][u] : 0u) + ws[1][u];
   const uint64_t ql = nl - 1;
+  uint32_t o[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int k = SCAN_E - 1; k >= 0; k--) {
     const uint64_t j = base + k;   // run = sum_{i > j} w_i
     if (j < ql) {
-      uint32_t v;
-      if (a == 0) v = num[j + 1];
-      else v = run % HFP * ipw[(j + 1) & 15] % HFP;
-      q[j] = (uint8_t)v;
-      if (j == 0) {
-        const uint32_t r0 = (num[0] + a * v) % HFP;
-        if (r0) atomicOr(D.flag, 1u);
-      }
+      const uint32_t v = a == 0 ? (uint32_t)num[j + 1] : run % HFP * ipw[(k + 1) & 15] % HFP;
+      o[k >> 2] |= v << (8 * (k & 3));
+      if (j == 0 && (num[0] + a * v) % HFP) atomicOr(D.flag, 1u);
     }
     run += w[k];
+  }
+  if (D.vec && base + 16 <= ql) {
+    *reinterpret_cast<uint4*>(q + base) = make_uint4(o[0], o[1], o[2], o[3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      if (base + k < ql) q[base + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
   }
 }
 
@@ -1288,7 +1308,8 @@ int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs, const Lc
       continue;
     }
     const int nb = (int)((r.nl + SCAN_B - 1) / SCAN_B);
-    L.d[nd++] = LinDiv{r.num, r.nl, r.aslot, nb, r.q, r.flag, bs};
+    const int vec = ((uintptr_t)r.num % 16 == 0) && ((uintptr_t)r.q % 16 == 0);
+    L.d[nd++] = LinDiv{r.num, r.nl, r.aslot, nb, r.q, r.flag, bs, vec};
     bs += nb + 2;
     nbmax = std::max(nbmax, nb);
   }
