@@ -540,7 +540,7 @@ __global__ __launch_bounds__(256) void divide_binomial4_kernel(const uint8_t* __
       if (r < m && r < nl && (num[r] + nc * prev) % HFP) rv = 1;
     }
   }
-  // one vote byte per block (trim_many_kernel ORs them into the status word): the blocks run
+  // one vote byte per block (trim_pack_kernel ORs them into the status word): the blocks run
   // together, so a "skip if already set" atomic would still serialise ~1000 same-address ORs
   const int vote = __syncthreads_or(rv != 0);
   if (threadIdx.x == 0) rem_part[blockIdx.x] = vote ? 1 : 0;
@@ -863,33 +863,6 @@ struct TrimArgs {
   uint64_t len[11];
   int dst[11];
 };
-__global__ __launch_bounds__(256) void trim_many_kernel(TrimArgs a, uint32_t* __restrict__ stat) {
-  const uint8_t* p = a.p[blockIdx.x];
-  const uint64_t n = a.len[blockIdx.x];
-  __shared__ uint32_t best;
-  if (threadIdx.x == 0) best = 0;
-  __syncthreads();
-  for (uint64_t hi = n; hi > 0;) {
-    const uint64_t lo = hi > 4096 ? hi - 4096 : 0;
-    uint32_t last = 0;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
-      if (p[i]) last = max(last, (uint32_t)(i + 1));
-    if (last) atomicMax(&best, last);
-    __syncthreads();
-    const uint32_t b = best;
-    __syncthreads();
-    if (b) break;
-    hi = lo;
-  }
-  if (threadIdx.x != 0) return;
-  const int d = a.dst[blockIdx.x];
-  if (d & TRIM_ANY) {
-    if (best) stat[d & ~TRIM_ANY] = 1u;
-  } else {
-    stat[d] = best ? best : 1u;
-  }
-}
-
 // ------------------------------------------------------------------ scalar programs
 __device__ void scalars_r4(uint8_t* S) {
   const uint32_t al = S[S_ALPHA], be = S[S_BETA], ga = S[S_GAMMA], z = S[S_Z];
@@ -952,9 +925,55 @@ __global__ void scalars_init_kernel(SlotFile f, uint8_t* __restrict__ S, uint32_
 // The proof bytes and the status words go straight to mapped pinned host memory (`host`:
 // 64 proof bytes, then NSTAT words), so the call's end is one stream synchronize and no
 // device->host copies.
-__global__ void proof_pack_kernel(const PlkMsmResult* __restrict__ res, const uint8_t* __restrict__ S,
-                                  const uint32_t* __restrict__ stat, uint8_t* __restrict__ host) {
-  const int t = threadIdx.x;
+// The trimmed lengths (formerly a kernel of their own) and the packing in ONE block of 1024 threads, after
+// the MSM (which runs over the committed length and does not need them): wave w < ntrim finds
+// buffer w's last non-zero byte from the top, 1 KB per step (16 bytes per lane, the highest
+// non-zero lane by ballot); the remaining waves OR the remainder-vote bytes (TRIM_ANY).
+constexpr int PACK_T = 1024;
+__global__ __launch_bounds__(PACK_T) void trim_pack_kernel(TrimArgs a, int nt, const PlkMsmResult* __restrict__ res,
+                                                           const uint8_t* __restrict__ S, uint32_t* __restrict__ stat,
+                                                           uint8_t* __restrict__ host) {
+  const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
+  const int ntrim = nt > 0 && (a.dst[nt - 1] & TRIM_ANY) ? nt - 1 : nt;   // the vote buffer comes last
+  __shared__ uint32_t got[11];
+  if (t < 11) got[t] = 0;
+  __syncthreads();
+  if (wv < ntrim) {
+    const uint8_t* p = a.p[wv];
+    for (uint64_t hi = a.len[wv]; hi > 0;) {
+      const uint64_t lo = hi > 1024 ? hi - 1024 : 0;
+      uint32_t found = 0;   // index + 1 of this lane's highest non-zero byte
+#pragma unroll
+      for (int k = 15; k >= 0; k--) {   // lane l: bytes hi - 16 (l + 1) .. hi - 16 l - 1
+        const int64_t i = (int64_t)hi - 16 * (lane + 1) + k;
+        const bool nz = i >= (int64_t)lo && p[i < (int64_t)lo ? lo : i] != 0;
+        found = (!found && nz) ? (uint32_t)(i + 1) : found;
+      }
+      const unsigned long long bal = __ballot(found != 0);
+      if (bal) {
+        const uint32_t v = __shfl(found, __ffsll(bal) - 1, 64);   // lowest lane = highest bytes
+        if (lane == 0) got[wv] = v;
+        break;
+      }
+      hi = lo;
+    }
+  } else if (ntrim < nt) {
+    const uint8_t* p = a.p[nt - 1];
+    const uint64_t n = a.len[nt - 1];
+    uint32_t any = 0;
+    for (uint64_t i = (uint64_t)(t - ntrim * 64); i < n; i += (uint64_t)(PACK_T - ntrim * 64)) any |= p[i];
+    if (any) got[nt - 1] = 1;
+  }
+  __syncthreads();
+  if (t < nt) {
+    const int d = a.dst[t];
+    if (d & TRIM_ANY) {
+      if (got[t]) stat[d & ~TRIM_ANY] = 1u;
+    } else {
+      stat[d] = got[t] ? got[t] : 1u;   // at least 1 (src/poly.h:20-24)
+    }
+  }
+  __syncthreads();   // the stat words written above, visible to the block
   if (t < 27) host[t] = res[t / 3].g1[t % 3];
   const int ev[7] = {S_AZ, S_BZ, S_CZ, S_S1Z, S_S2Z, S_RZ, S_ZWZ};
   if (t >= 27 && t < 34) host[t] = S[ev[t - 27]];
@@ -1095,7 +1114,7 @@ struct plk_prover {
   void* work = nullptr;
   size_t work_bytes = 0;
   hipStream_t st = nullptr;
-  // mapped pinned host memory: 64 proof bytes + NSTAT status words (proof_pack_kernel)
+  // mapped pinned host memory: 64 proof bytes + NSTAT status words (trim_pack_kernel)
   uint8_t* h_res = nullptr;
   uint8_t* d_res_host = nullptr;   // its device address
 };
@@ -1264,7 +1283,7 @@ int divide_zh(plk_prover* P, const uint8_t* num, uint64_t nl, uint8_t* q, uint64
       const uint64_t nb = (m / 4 + 255) / 256;
       hipLaunchKernelGGL(divide_binomial4_kernel, dim3((unsigned)nb), dim3(256), 0, P->st, num, nl, m, P->zh_lead,
                          P->zh_c, q, ql, ql ? (ql - 1) / m : 0, ql ? (ql - 1) % m : 0, P->d_rem);
-      P->rem_blocks = nb;   // trim_many_kernel folds the votes into *flag (ST_REM_T)
+      P->rem_blocks = nb;   // trim_pack_kernel folds the votes into *flag (ST_REM_T)
     } else {
       hipLaunchKernelGGL(divide_binomial_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, P->st, num, nl, m,
                          P->zh_lead, P->zh_c, q, ql, flag);
@@ -1600,7 +1619,7 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     }
 #undef PLK_NUMDIV
     PLK_HIP(hipGetLastError());
-    P->rem_blocks = nb;   // trim_many_kernel folds the votes into ST_REM_T
+    P->rem_blocks = nb;   // trim_pack_kernel folds the votes into ST_REM_T
   } else {
     RC(lincomb_batch(P, {num}));
     RC(divide_zh(P, P->NUM, L.lnum, P->TX, L.ltx, P->d_stat + ST_REM_T));
@@ -1643,7 +1662,9 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
                          {P->ZZ, L.lzz, S_ZOMEGA, cWzw, P->d_stat + ST_REM_W2}},
                      fuse ? &nb5 : nullptr));
   }
-  // ---- trimmed lengths for the reference's exits
+  // ---- trimmed lengths for the reference's exits: computed by the packing kernel after the MSM
+  TrimArgs trims{};
+  int ntrims = 0;
   {
     TrimArgs t{};
     const uint8_t* cps[9] = {cA, cB, cC, cZ, cTlo, cTmid, cThi, cWz, cWzw};
@@ -1652,8 +1673,8 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     t.p[9] = P->TX; t.len[9] = L.ltx; t.dst[9] = ST_TXLEN;
     int nt = 10;
     if (P->rem_blocks) { t.p[10] = P->d_rem; t.len[10] = P->rem_blocks; t.dst[10] = ST_REM_T | TRIM_ANY; nt = 11; }
-    hipLaunchKernelGGL(trim_many_kernel, dim3(nt), dim3(256), 0, P->st, t, P->d_stat);
-    PLK_HIP(hipGetLastError());
+    trims = t;
+    ntrims = nt;
   }
   // ---- the 9 commitments: one batched MSM over the arena (srs_eval_at_s, src/srs.h:53-68)
   const uint64_t nm = std::min<uint64_t>(P->cmax, P->srs_len);
@@ -1664,7 +1685,8 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     for (int i = 0; i < 9; i++) RC(plk_msm_serial_launch(P->d_srs, P->arena + i * P->cstride, nm, P->d_res + i, P->st));
   }
   // (each record's finishing block already wrote its point: no finalize launch)
-  hipLaunchKernelGGL(proof_pack_kernel, dim3(1), dim3(64), 0, P->st, P->d_res, P->d_S, P->d_stat, P->d_res_host);
+  hipLaunchKernelGGL(trim_pack_kernel, dim3(1), dim3(PACK_T), 0, P->st, trims, ntrims, P->d_res, P->d_S, P->d_stat,
+                     P->d_res_host);
   PLK_HIP(hipGetLastError());
 #undef RC
   return PLK_OK;
@@ -1691,7 +1713,7 @@ int check_status(const plk_prover* P, const uint32_t* st, int strict, int circui
 }
 
 int finish(plk_prover* P, int strict, int circuit, uint8_t proof[34]) {
-  PLK_HIP(hipStreamSynchronize(P->st));   // proof_pack_kernel wrote P->h_res (mapped pinned)
+  PLK_HIP(hipStreamSynchronize(P->st));   // trim_pack_kernel wrote P->h_res (mapped pinned)
   uint32_t hs[NSTAT];
   memcpy(hs, P->h_res + 64, sizeof hs);
   const int rc = check_status(P, hs, strict, circuit);
