@@ -568,7 +568,11 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
       return PLK_ERR_RANGE;
     }
   }
-  const uint32_t ninv = use29 ? f29::hpow(1ull << k, f29::P - 2) : bb::hpow(1ull << k, bb::P - 2);   // normal form
+  // final scale: the transform's inputs are normal-form byte values (not Montgomery), so the
+  // Montgomery pointwise product leaves a factor R^-1: N^-1 R^2, applied by one more Montgomery
+  // multiply, gives the normal-form coefficient
+  const uint32_t ninv = use29 ? (uint32_t)((uint64_t)f29::hpow(1ull << k, f29::P - 2) * f29::R2 % f29::P)
+                              : (uint32_t)((uint64_t)bb::hpow(1ull << k, bb::P - 2) * bb::R2 % bb::P);
   // operands: job i owns slots 2i (a) and 2i+1 (b) of d_work; an operand equal (same bytes,
   // same length) to an earlier one of the group reuses that slot's transform
   static int noshare = -1;

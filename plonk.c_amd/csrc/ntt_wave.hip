@@ -117,7 +117,9 @@ struct FBB {
     return bb::madd(bb::madd(a, b), c);
   }
   __device__ static __forceinline__ uint32_t colf(uint32_t cl, uint32_t ch) { return bb::mmul(cl, ch); }
-  __device__ static __forceinline__ uint32_t from_byte(uint32_t b) { return bb::mmul(b % 17u, bb::R2); }
+  // a byte's value, NORMAL form (Montgomery twiddles keep a normal-form input normal; the
+  // pointwise product's R^-1 is folded into the final scale, see ntt_group)
+  __device__ static __forceinline__ uint32_t byte_val(uint32_t b) { return b % 17u; }
   __device__ static __forceinline__ uint32_t out17(uint32_t v, uint32_t ninv) { return bb::mmul(v, ninv) % 17u; }
 };
 // F29 bounds.  Montgomery REDC of t < p 2^32 lands in [0, 2p); so a product of ANY u32 with a
@@ -160,9 +162,9 @@ struct F29 {
   // convolution term is at most 64 in absolute value and a product is exact while
   // 64 min(la, lb) <= (p - 1) / 2 (min(la, lb) * 128 < p: up to 3,670,016 coefficients, four
   // times the uncentered bound); a result y > (p - 1) / 2 stands for y - p.
-  __device__ static __forceinline__ uint32_t from_byte(uint32_t b) {
+  __device__ static __forceinline__ uint32_t byte_val(uint32_t b) {   // normal form (FBB::byte_val)
     const uint32_t v = b % 17u;
-    return f29::mmul(v > 8u ? v + (f29::P - 17u) : v, f29::R2);
+    return v > 8u ? v + (f29::P - 17u) : v;
   }
   __device__ static __forceinline__ uint32_t out17(uint32_t v, uint32_t ninv) {
     const uint32_t y = f29::red1(f29::mmul(v, ninv));
@@ -281,6 +283,27 @@ struct Eng {
     return (H << (p.lo + M)) | ((uint64_t)r << p.lo) | L;
   }
 
+  // the same index split into a uniform tile base and a 32-bit offset (no shared bits):
+  // index = tbase + toff(e), toff < 2^(lo + M) <= 2^k
+  __device__ static __forceinline__ uint64_t tbase(const WPass& p, uint32_t tile) {
+    if (M == TB) return (uint64_t)tile << TB;
+    constexpr int cb = TB - M;
+    const int sh = p.lo - cb;
+    return ((uint64_t)(tile >> sh) << (p.lo + M)) | ((uint64_t)(tile & ((1u << sh) - 1)) << cb);
+  }
+  __device__ static __forceinline__ uint32_t toff(const WPass& p, uint32_t e) {
+    if (M == TB) return e;
+    return ((e & ((1u << M) - 1)) << p.lo) | (e >> M);
+  }
+  // offset of element b + (k << lb) of round q: the register index k only moves row bits when
+  // lb + R <= M (every column-mapped round), so it is toff(b) + (k << (lb + lo))
+  template <int Q, bool INV>
+  __device__ static __forceinline__ uint32_t toff_k(const WPass& p, uint32_t o0, uint32_t b, int k) {
+    constexpr int LB = lbq(Q, INV);
+    if constexpr (M == TB || LB + R <= M) return o0 + (((uint32_t)k << LB) << (M == TB ? 0 : p.lo));   // (lo = 0 when M = TB)
+    else return toff(p, b + ((uint32_t)k << LB));
+  }
+
   // column factor exponent (in w_{2^27} units) for element e of a high-bit pass
   __device__ static __forceinline__ uint32_t col_exp(const WPass& p, uint32_t tile, uint32_t e) {
     constexpr int cb = TB - M;
@@ -327,24 +350,36 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
   const uint8_t* s8 = ar.s8;
   const uint64_t ls = ar.ls;
 
+  // uniform tile base pointers, 32-bit element offsets
+  const uint64_t tb = G::tbase(p, tile);
+  uint32_t* dt = d + tb;
+  const uint32_t* colt = COLT ? tw.col + tb : nullptr;
   const uint32_t b0 = G::template base_q<0>(tid, false);
-  constexpr int L0 = G::lbq(0, false);
+  const uint32_t o0 = G::toff(p, b0);
   uint32_t v[G::E];
+  if constexpr (FROM_U8) {
+    // raw bytes now (0 past the operand), their values through an LDS table after the barrier
+    const uint8_t* st = s8 + tb;
+    const uint32_t lim = ls > tb ? (uint32_t)(ls - tb < 0xFFFFFFFFull ? ls - tb : 0xFFFFFFFFull) : 0u;
 #pragma unroll
-  for (int k = 0; k < G::E; k++) {
-    const uint64_t idx = G::index(p, tile, b0 + ((uint32_t)k << L0));
-    if (FROM_U8) v[k] = idx < ls ? F::from_byte(s8[idx]) : 0u;
-    else v[k] = d[idx];
+    for (int k = 0; k < G::E; k++) {
+      const uint32_t o = G::template toff_k<0, false>(p, o0, b0, k);
+      v[k] = o < lim ? st[o] : 0u;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < G::E; k++) v[k] = dt[G::template toff_k<0, false>(p, o0, b0, k)];
   }
   // column factor table words of the elements this thread stores (HIGH passes)
   constexpr int LF = G::lbq(G::NR - 1, false);
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, false);
+  const uint32_t of = G::toff(p, bf);
   uint32_t cl[G::HIGH ? G::E : 1], ch[G::HIGH && !COLT ? G::E : 1];
   if (G::HIGH) {
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
       if constexpr (COLT) {
-        cl[k] = tw.col[G::index(p, tile, bf + ((uint32_t)k << LF))];
+        cl[k] = colt[G::template toff_k<G::NR - 1, false>(p, of, bf, k)];
       } else {
         const uint32_t ex = G::col_exp(p, tile, bf + ((uint32_t)k << LF));
         cl[k] = tw.lo[ex & 4095u];
@@ -352,16 +387,21 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
       }
     }
   }
+  __shared__ uint32_t lut[FROM_U8 ? 256 : 1];
+  if (FROM_U8 && tid < 256) lut[tid] = F::byte_val(tid);
   load_pass_tw<M, G::NT>(Tsm, tw.small);
   __syncthreads();
+  if constexpr (FROM_U8) {
+#pragma unroll
+    for (int k = 0; k < G::E; k++) v[k] = lut[v[k]];
+  }
   G::template pass<false>(v, tid, bufs, 0, Tsm);
 #pragma unroll
   for (int k = 0; k < G::E; k++) {
-    const uint32_t e = bf + ((uint32_t)k << LF);
     uint32_t x = v[k];
     if constexpr (G::HIGH && COLT) x = F::mul(x, cl[k]);
     else if constexpr (G::HIGH) x = F::mul(x, F::colf(cl[k], ch[k]));
-    d[G::index(p, tile, e)] = x;
+    dt[G::template toff_k<G::NR - 1, false>(p, of, bf, k)] = x;
   }
 }
 
@@ -407,19 +447,26 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   const uint32_t* s1 = jb.S1;
   const uint32_t* s2 = jb.S2;
 
+  // uniform tile base pointers, 32-bit element offsets
+  const uint64_t tb = G::tbase(p, tile);
+  uint32_t* dt = d + tb;
+  const uint32_t* s1t = s1 ? s1 + tb : nullptr;
+  const uint32_t* s2t = s2 ? s2 + tb : nullptr;
+  const uint32_t* colt = COLT ? tw.col + tb : nullptr;
   const uint32_t b0 = G::template base_q<0>(tid, true);
+  const uint32_t o0 = G::toff(p, b0);
   constexpr int L0 = G::lbq(0, true);
   uint32_t v[G::E];
   uint32_t cl[G::HIGH ? G::E : 1], ch[G::HIGH && !COLT ? G::E : 1];
 #pragma unroll
   for (int k = 0; k < G::E; k++) {
     const uint32_t e = b0 + ((uint32_t)k << L0);
-    const uint64_t idx = G::index(p, tile, e);
-    v[k] = d[idx];
-    if (s1) v[k] = F::sum(v[k], s1[idx], s2 ? s2[idx] : 0u);   // uniform branch
+    const uint32_t o = G::template toff_k<0, true>(p, o0, b0, k);
+    v[k] = dt[o];
+    if (s1) v[k] = F::sum(v[k], s1t[o], s2 ? s2t[o] : 0u);   // uniform branch
     if (G::HIGH) {
       if constexpr (COLT) {
-        cl[k] = tw.col[idx];
+        cl[k] = colt[o];
       } else {
         const uint32_t ex = G::col_exp(p, tile, e);   // roots of tw (inverse or forward)
         cl[k] = tw.lo[ex & 4095u];
@@ -439,20 +486,23 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   G::template pass<true>(v, tid, bufs, 0, Tsm);
   constexpr int LF = G::lbq(G::NR - 1, true);
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, true);
+  const uint32_t of = G::toff(p, bf);
   uint32_t wrapped = 0;   // elements of this thread that hold c[j] + c[N + j] (j < ntop)
+  const uint32_t N = 1u << p.k;   // (k <= 27: every index fits 32 bits)
+  const uint32_t lim = out_len < N ? (uint32_t)out_len : N;
 #pragma unroll
   for (int k = 0; k < G::E; k++) {
-    const uint64_t idx = G::index(p, tile, bf + ((uint32_t)k << LF));
+    const uint32_t o = G::template toff_k<G::NR - 1, true>(p, of, bf, k);
     if (!TO_U8) {
-      d[idx] = v[k];
+      dt[o] = v[k];
     } else {
       // poly_mul runs its inverse with the FORWARD roots (no inverse table in LDS): that
       // yields N c[-idx mod N], so the coefficient lands at the negated position
-      const uint64_t j = ((1ull << p.k) - idx) & ((1ull << p.k) - 1);
-      if (j < out_len) {
+      const uint32_t j = (N - ((uint32_t)tb + o)) & (N - 1);
+      if (j < lim) {
         const uint32_t r = F::out17(v[k], ninv);
         out8[j] = (uint8_t)r;
-        if (j < (uint64_t)jb.ntop) wrapped |= 1u << k;
+        if (j < (uint32_t)jb.ntop) wrapped |= 1u << k;
       }
     }
   }
