@@ -168,8 +168,9 @@ struct F29 {
   }
   __device__ static __forceinline__ uint32_t out17(uint32_t v, uint32_t ninv) {
     const uint32_t y = f29::red1(f29::mmul(v, ninv));
-    const uint32_t r = y % 17u;
-    return y > (f29::P - 1) / 2 ? (r + 17u - f29::P % 17u) % 17u : r;   // (y - p) mod 17
+    // y > (p - 1) / 2 stands for y - p = y + C - 17 2^25 with C = 17 2^25 - p > 0: one mod 17
+    constexpr uint32_t C = (17u << 25) - f29::P;
+    return (y + (y > (f29::P - 1) / 2 ? C : 0u)) % 17u;
   }
 };
 
