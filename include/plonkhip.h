@@ -107,6 +107,24 @@ size_t plk_poly_mul_workspace(size_t la, size_t lb);
 int plk_poly_mul_dev(const uint8_t *d_a, size_t la, const uint8_t *d_b, size_t lb, uint8_t *d_out,
                      uint32_t *d_out_nz, void *d_work, void *stream);
 
+/* A batch of independent poly_mul products on device buffers (the prover's round-3 products
+ * run this way; replaces a sequence of poly_mul calls, src/poly.h:106-122): products of one
+ * transform size share each pass's launch, and operands given by the same pointer and length
+ * are transformed once.  acc = 1 ADDS the product into the preceding job's output (a sum group:
+ * a leader and up to two members of one shape; the members' out is not written).  Outputs are
+ * untrimmed (la + lb - 1 bytes).  d_work: at least the largest single job's
+ * plk_poly_mul_workspace(); plk_poly_mul_batch_workspace() bytes run every size group in one go. */
+typedef struct {
+  const uint8_t *a;
+  size_t la;
+  const uint8_t *b;
+  size_t lb;
+  uint8_t *out;
+  int acc;
+} plk_polymul_job_t;
+size_t plk_poly_mul_batch_workspace(const plk_polymul_job_t *jobs, int n);
+int plk_poly_mul_batch_dev(const plk_polymul_job_t *jobs, int n, void *d_work, size_t work_bytes, void *stream);
+
 /* Radix-2 NTT over BabyBear p = 15*2^27+1 on 2^log_n Montgomery-form u32, in place:
  * forward = DIF natural -> bit-reversed; inverse = DIT bit-reversed -> natural, unscaled. */
 int plk_ntt_dev(uint32_t *d_data, int log_n, int inverse, void *stream);

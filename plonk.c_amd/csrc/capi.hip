@@ -326,6 +326,39 @@ int plk_poly_mul_dev(const uint8_t* d_a, size_t la, const uint8_t* d_b, size_t l
   return plk_poly_mul_launch(d_a, la, d_b, lb, d_out, d_out_nz, d_work, pick(stream));
 }
 
+size_t plk_poly_mul_batch_workspace(const plk_polymul_job_t* jobs, int n) {
+  // the size groups run one after another on the stream and reuse the workspace: the largest
+  // group's need (jobs of one size 2^k take 2^(k+3) bytes each)
+  size_t per_k[64] = {0}, best = 0;
+  for (int i = 0; jobs && i < n; i++) {
+    const size_t w = plk_poly_mul_workspace_bytes(jobs[i].la, jobs[i].lb);
+    if (!w) continue;
+    int k = 0;
+    while (((size_t)8 << k) < w) k++;
+    per_k[k] += w;
+    best = per_k[k] > best ? per_k[k] : best;
+  }
+  return best;
+}
+
+int plk_poly_mul_batch_dev(const plk_polymul_job_t* jobs, int n, void* d_work, size_t work_bytes, void* stream) {
+  int rc = ensure();
+  if (rc) return rc;
+  if (!jobs || n < 1 || n > 64) {
+    plk_set_error("plk_poly_mul_batch_dev: %d jobs (1..64)", n);
+    return PLK_ERR_ARG;
+  }
+  PlkPolyMulJob js[64];
+  for (int i = 0; i < n; i++) {
+    if (!jobs[i].a || !jobs[i].b || !jobs[i].out) {
+      plk_set_error("plk_poly_mul_batch_dev: null buffer in job %d", i);
+      return PLK_ERR_ARG;
+    }
+    js[i] = PlkPolyMulJob{jobs[i].a, jobs[i].la, jobs[i].b, jobs[i].lb, jobs[i].out, jobs[i].acc ? 1 : 0};
+  }
+  return plk_poly_mul_batch_launch(js, n, d_work, work_bytes, pick(stream));
+}
+
 int plk_ntt_dev(uint32_t* d_data, int log_n, int inverse, void* stream) {
   int rc = ensure();
   if (rc) return rc;

@@ -574,7 +574,8 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
   const uint32_t ninv = use29 ? (uint32_t)((uint64_t)f29::hpow(1ull << k, f29::P - 2) * f29::R2 % f29::P)
                               : (uint32_t)((uint64_t)bb::hpow(1ull << k, bb::P - 2) * bb::R2 % bb::P);
   // operands: job i owns slots 2i (a) and 2i+1 (b) of d_work; an operand equal (same bytes,
-  // same length) to an earlier one of the group reuses that slot's transform
+  // same length) to an earlier one of the same launch chunk (PLK_WAVE_MAX_JOBS jobs: a chunk's
+  // forward passes transform its distinct arrays) reuses that slot's transform
   static int noshare = -1;
   if (noshare < 0) {
     const char* e = getenv("PLK_NTT_NO_SHARE");
@@ -587,7 +588,7 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
       const uint8_t* ptr = s ? g[i].b : g[i].a;
       const uint64_t len = s ? g[i].lb : g[i].la;
       slot[i][s] = 2 * i + s;
-      for (int q = 0; q <= i && !noshare; q++)
+      for (int q = i - i % PLK_WAVE_MAX_JOBS; q <= i && !noshare; q++)
         for (int t = 0; t < 2 && (q < i || t < s); t++)
           if ((t ? g[q].b : g[q].a) == ptr && (t ? g[q].lb : g[q].la) == len && slot[q][t] == 2 * q + t) {
             slot[i][s] = 2 * q + t;
@@ -626,7 +627,8 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
       L = i;
       continue;
     }
-    if (i == 0 || g[L].la != g[i].la || g[L].lb != g[i].lb || (es && es[L] != es[i]) || w[L].ngroup == 2) {
+    if (i == 0 || g[L].la != g[i].la || g[L].lb != g[i].lb || (es && es[L] != es[i]) || w[L].ngroup == 2 ||
+        L / PLK_WAVE_MAX_JOBS != i / PLK_WAVE_MAX_JOBS) {   // (a group runs in one launch chunk)
       plk_set_error("poly_mul batch: invalid sum group at job %d", i);
       return PLK_ERR_ARG;
     }

@@ -68,7 +68,7 @@ struct WPass {
 // A batch of independent transforms of one size: job j owns the u32 arrays A (and B for a
 // product), optionally reads its inputs as bytes (a8/la, b8/lb) in the first forward pass
 // and writes its product as bytes (out8, out_len) in the last inverse pass.
-constexpr int WT_MAX_JOBS = 12;
+constexpr int WT_MAX_JOBS = PLK_WAVE_MAX_JOBS;
 struct WJobs {
   WJob j[WT_MAX_JOBS];
 };

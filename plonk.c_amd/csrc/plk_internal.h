@@ -91,6 +91,7 @@ struct WJob {
   const uint8_t* ga8[2] = {nullptr, nullptr};
   const uint8_t* gb8[2] = {nullptr, nullptr};
 };
+constexpr int PLK_WAVE_MAX_JOBS = 12;   // jobs per launch of the wave engine (larger batches run in chunks)
 bool plk_wave_ntt_supported(int k);
 // field 0 = BabyBear, 1 = F29 (lazy; only when every job's min(la, lb) * 256 < f29::P);
 // ninv = 2^-k mod p in normal form for that field

@@ -47,6 +47,8 @@ SIGNATURES = {
     "plk_dlog_generator": (C.c_int, [_u8p]),
     "plk_poly_mul_workspace": (_sz, [_sz, _sz]),
     "plk_poly_mul_dev": (C.c_int, [_vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp]),
+    "plk_poly_mul_batch_workspace": (_sz, [_vp, C.c_int]),
+    "plk_poly_mul_batch_dev": (C.c_int, [_vp, C.c_int, _vp, _sz, _vp]),
     "plk_ntt_dev": (C.c_int, [_vp, C.c_int, C.c_int, _vp]),
     "plk_ntt_batch_dev": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, _vp]),
     "plk_prover_create": (C.c_int, [_vp, C.POINTER(_vp)]),
@@ -224,6 +226,31 @@ def poly_mul_workspace(la, lb):
 def poly_mul_dev(a, la, b, lb, out, nz, work, stream=None):
     _check("plk_poly_mul_dev", lib().plk_poly_mul_dev(_ptr(a), int(la), _ptr(b), int(lb), _ptr(out),
                                                       _ptr(nz), _ptr(work), _stream(stream)))
+
+
+class PolyMulJob(C.Structure):
+    """plk_polymul_job_t (include/plonkhip.h)"""
+    _fields_ = [("a", C.c_void_p), ("la", C.c_size_t), ("b", C.c_void_p), ("lb", C.c_size_t),
+                ("out", C.c_void_p), ("acc", C.c_int)]
+
+
+def _jobs(jobs):
+    arr = (PolyMulJob * len(jobs))()
+    for i, (a, la, b, lb, out, acc) in enumerate(jobs):
+        arr[i] = PolyMulJob(_ptr(a), int(la), _ptr(b), int(lb), _ptr(out), int(acc))
+    return arr
+
+
+def poly_mul_batch_workspace(jobs):
+    """jobs: (a, la, b, lb, out, acc) tuples of device tensors / pointers"""
+    arr = _jobs(jobs)
+    return int(lib().plk_poly_mul_batch_workspace(arr, len(jobs)))
+
+
+def poly_mul_batch_dev(jobs, work, work_bytes, stream=None):
+    arr = _jobs(jobs)
+    _check("plk_poly_mul_batch_dev", lib().plk_poly_mul_batch_dev(arr, len(jobs), _ptr(work), int(work_bytes),
+                                                                  _stream(stream)))
 
 
 def ntt_dev(data, log_n, inverse=False, stream=None):

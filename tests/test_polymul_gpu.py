@@ -118,3 +118,65 @@ def test_field_boundary_worst_case(hip, m, av, bv):
     nz = np.flatnonzero(want)
     want = want[:int(nz[-1]) + 1]
     assert hip.poly_mul(a, b) == want.tobytes()
+
+
+# ---- batched products (plk_poly_mul_batch_dev: the prover's round-3 path) -------------------
+def _trim(bts):
+    bts = bts.rstrip(b"\x00")
+    return bts if bts else b"\x00"
+
+
+def _run_batch(hip, polys, spec):
+    """spec: (ia, ib, acc) jobs over the operand pool; returns each job's untrimmed output"""
+    import torch
+    dev = torch.device("cuda:0")
+    dp = [torch.from_numpy(p).to(dev) for p in polys]
+    outs = [torch.full((len(polys[i]) + len(polys[j]) - 1,), 0xEE, dtype=torch.uint8, device=dev)
+            for i, j, _ in spec]
+    jobs = [(dp[i], len(polys[i]), dp[j], len(polys[j]), o, acc) for (i, j, acc), o in zip(spec, outs)]
+    ws = hip.poly_mul_batch_workspace(jobs)
+    work = torch.zeros(max(ws, 16), dtype=torch.uint8, device=dev)
+    hip.poly_mul_batch_dev(jobs, work, ws, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    return [bytes(o.cpu().numpy()) for o in outs]
+
+
+# lengths whose pairwise products all take 2^13-point transforms (plain and wrapped, e <= 16)
+_POOL = [4097, 4100, 4096, 4000, 4099, 4090, 4097, 4100]
+
+
+def test_batch_shared_operands(hip, oracle):
+    """15 products of one size: two launch chunks (12 + 3), operands reused within and across
+    the chunks, squarings, a repeated job (both operands shared: a fresh work array)."""
+    polys = [np.frombuffer(gen.poly_inputs(40 + i, n, 1)[0], np.uint8) for i, n in enumerate(_POOL)]
+    spec = [(0, 1, 0), (0, 2, 0), (1, 2, 0), (0, 0, 0), (3, 4, 0), (4, 5, 0), (2, 5, 0), (1, 1, 0),
+            (0, 3, 0), (2, 3, 0), (5, 5, 0), (1, 4, 0), (0, 1, 0), (3, 3, 0), (2, 4, 0)]
+    outs = _run_batch(hip, polys, spec)
+    for (i, j, _), out in zip(spec, outs):
+        assert _trim(out) == oracle.poly_mul(polys[i].tobytes(), polys[j].tobytes()), (i, j)
+
+
+def test_batch_sum_group(hip, oracle):
+    """a_0 a_1 + a_6 a_7 + a_0 a_7 (one shape, wrapped by 4) in one inverse transform"""
+    polys = [np.frombuffer(gen.poly_inputs(60 + i, n, 1)[0], np.uint8) for i, n in enumerate(_POOL)]
+    spec = [(2, 3, 0), (0, 1, 0), (6, 7, 1), (0, 7, 1), (4, 5, 0)]
+    outs = _run_batch(hip, polys, spec)
+    full = len(polys[0]) + len(polys[1]) - 1
+
+    def prod(i, j):
+        p = np.frombuffer(oracle.poly_mul(polys[i].tobytes(), polys[j].tobytes()), np.uint8).astype(np.int64)
+        return np.pad(p, (0, full - len(p)))
+    want = (prod(0, 1) + prod(6, 7) + prod(0, 7)) % 17
+    assert outs[1] == want.astype(np.uint8).tobytes()
+    assert outs[2] == b"\xEE" * full and outs[3] == b"\xEE" * full   # members' outputs untouched
+    for k in (0, 4):
+        i, j, _ = spec[k]
+        assert _trim(outs[k]) == oracle.poly_mul(polys[i].tobytes(), polys[j].tobytes())
+
+
+def test_batch_rejects_group_across_launch_chunks(hip):
+    """a sum group must run in one launch chunk (12 products): leader at 11, member at 12"""
+    polys = [np.frombuffer(gen.poly_inputs(80 + i, n, 1)[0], np.uint8) for i, n in enumerate(_POOL)]
+    spec = [(k % 6, (k + 1) % 6, 0) for k in range(11)] + [(0, 1, 0), (6, 7, 1)]
+    with pytest.raises(Exception, match="sum group"):
+        _run_batch(hip, polys, spec)
