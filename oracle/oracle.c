@@ -214,11 +214,10 @@ static void np_ntt(uint32_t *a, size_t n, int inv) {
   }
 }
 
-/* returns trimmed length, or 0 on allocation failure / size out of range */
-size_t orc_poly_mul_ntt(const uint8_t *a, size_t la, const uint8_t *b, size_t lb, uint8_t *out) {
+/* untrimmed product mod 17 into out[0, la + lb - 1) for la + lb - 1 <= 2^23 (998244353 =
+ * 119 2^23 + 1: no larger power-of-two transform exists); 0 on allocation failure */
+static int np_mul_raw(const uint8_t *a, size_t la, const uint8_t *b, size_t lb, uint8_t *out) {
   size_t rl = la + lb - 1, n = 1;
-  size_t mn = la < lb ? la : lb;
-  if (mn * 256 >= NP) return 0;
   while (n < rl) n <<= 1;
   uint32_t *fa = calloc(n, 4), *fb = calloc(n, 4);
   if (!fa || !fb) { free(fa); free(fb); return 0; }
@@ -231,6 +230,32 @@ size_t orc_poly_mul_ntt(const uint8_t *a, size_t la, const uint8_t *b, size_t lb
   for (size_t i = 0; i < rl; i++) out[i] = (uint8_t)(fa[i] % P_HF);
   free(fa);
   free(fb);
+  return 1;
+}
+
+/* returns trimmed length, or 0 on allocation failure / size out of range.  Products longer
+ * than 2^23 split the longer operand into chunks whose products fit 2^23 points and add the
+ * shifted chunk products mod 17 (exact: each chunk product is). */
+size_t orc_poly_mul_ntt(const uint8_t *a, size_t la, const uint8_t *b, size_t lb, uint8_t *out) {
+  const size_t NMAX = (size_t)1 << 23;
+  size_t rl = la + lb - 1;
+  size_t mn = la < lb ? la : lb;
+  if (mn * 256 >= NP) return 0;
+  if (rl <= NMAX) return np_mul_raw(a, la, b, lb, out) ? trim(out, rl) : 0;
+  if (la < lb) {   /* a := the longer operand */
+    const uint8_t *t = a; a = b; b = t;
+    size_t u = la; la = lb; lb = u;
+  }
+  const size_t h = NMAX - lb + 1;   /* chunk length: h + lb - 1 = 2^23 */
+  uint8_t *part = malloc(NMAX);
+  if (!part) return 0;
+  memset(out, 0, rl);
+  for (size_t s = 0; s < la; s += h) {
+    const size_t cl = la - s < h ? la - s : h;
+    if (!np_mul_raw(a + s, cl, b, lb, part)) { free(part); return 0; }
+    for (size_t i = 0; i < cl + lb - 1; i++) out[s + i] = (uint8_t)((out[s + i] + part[i]) % P_HF);
+  }
+  free(part);
   return trim(out, rl);
 }
 

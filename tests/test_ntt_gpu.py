@@ -38,7 +38,7 @@ def test_forward_vs_dft(hip, k):
         assert y[bitrev(j, k)] == want, (k, j)
 
 
-@pytest.mark.parametrize("k", [16, 20, 23])
+@pytest.mark.parametrize("k", [16, 20, 23, 24, 25, 27])   # 24+: three-pass plans, up to the 2-adicity
 def test_roundtrip_and_linearity(hip, k):
     import torch
     n = 1 << k
@@ -84,7 +84,7 @@ def ntt_dif_reference(x, k):
     return a
 
 
-@pytest.mark.parametrize("k", [13, 14, 15, 17, 19, 20, 21, 22, 23])
+@pytest.mark.parametrize("k", [13, 14, 15, 17, 19, 20, 21, 22, 23, 24])
 def test_forward_vs_numpy_reference(hip, k):
     """Every pass plan of the wave-tile engine (remainder pass of 1..10 bits on top, 10-bit
     passes below) against an independent full transform."""

@@ -142,3 +142,19 @@ def test_toy_proof_fixture_shape():
     # the identity, src/srs.h:27-36), evaluations a_z..z_omega_z = 15 13 5 1 12 15 15
     assert base["proof"] == "000001" * 9 + "0f0d05010c0f0f"
     assert all(len(bytes.fromhex(p["proof"])) == 34 for p in g["proofs"])
+
+
+def test_poly_mul_ntt_beyond_two_adicity(oracle):
+    """998244353 = 119 2^23 + 1 has no 2^24-point transform: the checker splits longer products
+    into chunks; its result must equal two half products added at a different split point."""
+    a, b = gen.poly_inputs(7, 5000000, 3600000)
+    got = oracle.poly_mul_ntt(a, b)
+    h = 2500000
+    r1 = np.frombuffer(oracle.poly_mul_ntt(a[:h], b), np.uint8).astype(np.int64)
+    r2 = np.frombuffer(oracle.poly_mul_ntt(a[h:], b), np.uint8).astype(np.int64)
+    full = np.zeros(len(a) + len(b) - 1, np.int64)
+    full[:len(r1)] += r1
+    full[h:h + len(r2)] += r2
+    want = (full % 17).astype(np.uint8).tobytes().rstrip(b"\x00") or b"\x00"
+    ok = got == want
+    assert ok

@@ -43,6 +43,9 @@ SHAPES = [(1, 1), (33, 33), (32, 1000), (33, 1000), (2048, 2049), (2049, 2048), 
           # coefficients computed directly)
           (4097, 4100), (8193, 8196), (8196, 8193), (8200, 8201), (8200, 8202), (16386, 100),
           ((1 << 16) + 2, (1 << 16)), (3 * (1 << 14) + 4, (1 << 14) + 3)]
+# 2^24-point transforms (three-pass plans): F29 (min * 128 < p) and BabyBear (min above the F29
+# bound, below the oracle's 998244353 one)
+SHAPES += [(5000000, 3600000), (5000000, 3800000)]
 # every wrap width e = 1..16 against the shortest transform-path operand (33 coefficients), both orders
 SHAPES += [((1 << 13) - 32 + e, 33)[::1 if e % 2 else -1] for e in range(1, 17)]
 
@@ -51,7 +54,8 @@ SHAPES += [((1 << 13) - 32 + e, 33)[::1 if e % 2 else -1] for e in range(1, 17)]
 def test_shapes_vs_oracle(hip, oracle, la, lb):
     a, b = gen.poly_inputs(la * 31 + lb, la, lb)
     want = oracle.poly_mul(a, b) if la * lb <= (1 << 24) else oracle.poly_mul_ntt(a, b)
-    assert hip.poly_mul(a, b) == want
+    ok = hip.poly_mul(a, b) == want   # (a failing assert on megabyte operands makes pytest diff them for minutes)
+    assert ok, (la, lb)
 
 
 def test_trailing_cancellation_and_zero(hip, oracle):
