@@ -272,11 +272,31 @@ int orc_poly_divide(const uint8_t *num, size_t ln, const uint8_t *den, size_t ld
   uint8_t *qq = calloc(ln ? ln : 1, 1), *rr = calloc(ln ? ln : 1, 1);
   memcpy(rr, num, ln);
   uint8_t li = hf_inv_tab[den[ld - 1] % P_HF];
+  /* With a canonical numerator (every byte < 17) every value of the division stays canonical,
+   * and then h_sub(x, h_mul(c, d)) == x whenever d = 0 mod 17: the divisor's zero coefficients
+   * can be skipped (Z_H = x^n - 1 has two non-zero ones) -- the same bytes, O(q nnz) instead of
+   * O(q ld).  A non-canonical byte is changed by h_sub(x, 0) (int8 arithmetic), so raw inputs
+   * take the reference's full loop. */
+  int canon = 1;
+  for (size_t i = 0; i < ln && canon; i++) canon = num[i] < P_HF;
+  long *nzj = NULL;
+  long nnz = 0;
+  if (canon) {
+    nzj = malloc(ld * sizeof(long));
+    if (nzj)
+      for (long j = 0; j < (long)ld; j++)
+        if (den[ld - 1 - j] % P_HF) nzj[nnz++] = j;
+  }
   for (long i = (long)ln - 1; i >= (long)(ld - 1); i--) {
     uint8_t c = h_mul(rr[i], li);
     qq[i - (ld - 1)] = c;
-    for (long j = 0; j < (long)ld; j++) rr[i - j] = h_sub(rr[i - j], h_mul(c, den[ld - 1 - j]));
+    if (nzj) {
+      for (long t = 0; t < nnz; t++) rr[i - nzj[t]] = h_sub(rr[i - nzj[t]], h_mul(c, den[ld - 1 - nzj[t]]));
+    } else {
+      for (long j = 0; j < (long)ld; j++) rr[i - j] = h_sub(rr[i - j], h_mul(c, den[ld - 1 - j]));
+    }
   }
+  free(nzj);
   size_t ql = ln >= ld ? ln - ld + 1 : 1;
   ql = trim(qq, ql);
   size_t rl = ld - 1;

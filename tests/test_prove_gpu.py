@@ -161,6 +161,18 @@ def test_rounds_2_16_vs_oracle(hip, oracle):
     assert got.hex() == c["want"].hex()
 
 
+def test_rounds_2_20_vs_golden(hip):
+    """Config C5 itself: n = 2^20 gates, the 34 proof bytes against the CPU oracle's answer
+    (tests/golden/prove_2_20.json, made by tests/golden/make_prove_2_20.py -- 21 s of oracle
+    time, so recorded once rather than recomputed here)."""
+    g = load_golden("prove_2_20.json")
+    n = g["n"]
+    polys, chal, rnd, zh, pts = _synthetic(n, g["seed"], g["srs_len"])
+    pr = hip.Prover(n, zh, pts)
+    got = pr.rounds_dev([torch.from_numpy(p).to("cuda") for p in polys], chal, rnd)
+    assert got.hex() == g["proof"]
+
+
 _TILE13_SCRIPT = r"""
 import sys, numpy as np, torch
 sys.path[:0] = sys.argv[1:2]
