@@ -81,3 +81,18 @@ def digest(c):
     """SHA-256 of the raw bytes, hex -- the fixture digest for long outputs."""
     import hashlib
     return hashlib.sha256(np.asarray(c, dtype=np.uint8).tobytes()).hexdigest()
+
+
+def prove_instance(n, seed, srs_len):
+    """Prove-shaped synthetic instance (rounds 1-5 at n gates): 13 random 'interpolated'
+    polynomials of length n, challenges / blinding scalars, Z_H = x^n - 1, an SRS over the whole
+    group (tests/test_prove_gpu.py, tests/golden/make_prove_2_20.py, bench.py)."""
+    r = splitmix64(seed, 13 * n + 64)
+    polys = [(r[i * n:(i + 1) * n] % np.uint64(17)).astype(np.uint8) for i in range(13)]
+    chal = [int(x % np.uint64(17)) for x in r[13 * n:13 * n + 5]]
+    rnd = [int(x % np.uint64(17)) for x in r[13 * n + 5:13 * n + 14]]
+    chal[3] = max(chal[3], 2)            # z: avoid the degenerate z in {0, 1}
+    zh = np.zeros(n + 1, np.uint8)
+    zh[0], zh[n] = 16, 1
+    pts, _ = msm_inputs(seed ^ 0x5A5A, srs_len, "full")
+    return polys, chal, rnd, zh, pts

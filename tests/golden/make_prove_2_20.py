@@ -21,24 +21,11 @@ from pyoracle import Oracle  # noqa: E402
 SEED = 51
 
 
-def synthetic(n, seed, srs_len):
-    """the same instance as tests/test_prove_gpu.py::_synthetic"""
-    r = gen.splitmix64(seed, 13 * n + 64)
-    polys = [(r[i * n:(i + 1) * n] % np.uint64(17)).astype(np.uint8) for i in range(13)]
-    chal = [int(x % np.uint64(17)) for x in r[13 * n:13 * n + 5]]
-    rnd = [int(x % np.uint64(17)) for x in r[13 * n + 5:13 * n + 14]]
-    chal[3] = max(chal[3], 2)
-    zh = np.zeros(n + 1, np.uint8)
-    zh[0], zh[n] = 16, 1
-    pts, _ = gen.msm_inputs(seed ^ 0x5A5A, srs_len, "full")
-    return polys, chal, rnd, zh, pts
-
-
 def main():
     k = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     n = 1 << k
     srs_len = 2 * n + 8
-    polys, chal, rnd, zh, pts = synthetic(n, SEED, srs_len)
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, SEED, srs_len)
     t = time.time()
     ref = RefProver(Oracle(), pts.tobytes(), n, z_h=zh.tobytes())
     proof = ref.rounds(polys, chal, rnd, strict=False)

@@ -56,15 +56,7 @@ def test_prove_rejects_what_the_reference_rejects(hip):
 
 def _synthetic(n, seed, srs_len):
     """13 random 'interpolated' polynomials of length n, Z_H = x^n - 1, random SRS."""
-    r = gen.splitmix64(seed, 13 * n + 64)
-    polys = [(r[i * n:(i + 1) * n] % np.uint64(17)).astype(np.uint8) for i in range(13)]
-    chal = [int(x % np.uint64(17)) for x in r[13 * n:13 * n + 5]]
-    rnd = [int(x % np.uint64(17)) for x in r[13 * n + 5:13 * n + 14]]
-    chal[3] = max(chal[3], 2)            # z: avoid the degenerate z in {0, 1}
-    zh = np.zeros(n + 1, np.uint8)
-    zh[0], zh[n] = 16, 1
-    pts, _ = gen.msm_inputs(seed ^ 0x5A5A, srs_len, "full")
-    return polys, chal, rnd, zh, pts
+    return gen.prove_instance(n, seed, srs_len)
 
 
 @pytest.mark.parametrize("n,seed", [(8, 1), (37, 2), (256, 3), (1000, 4), (3000, 5)])
@@ -143,7 +135,7 @@ _BIG = {}
 
 
 def _big_case(oracle):
-    """n = 2^16 prove-shaped instance and its CPU answer (~11 s of oracle time, computed once)."""
+    """n = 2^16 prove-shaped instance and its CPU answer (computed once per session)."""
     if not _BIG:
         n = 1 << 16
         polys, chal, rnd, zh, pts = _synthetic(n, 41, 2 * n + 8)
