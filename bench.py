@@ -80,6 +80,38 @@ def event_avg_ms(torch, st, fn, reps, rounds=3):
     return per[0], per[len(per) // 2]
 
 
+def graph_avg_ms(torch, fn, reps, rounds=3):
+    """Device time per call of fn(i, stream) with the host out of the loop: `reps` calls
+    captured once into a HIP graph (the library's launches go to the capture stream), the graph
+    replayed between an event pair.  Short kernels launched one Python call at a time are
+    host-rate bound (the ctypes call + hipLaunchKernel ~6 us); replayed they run back to back
+    with only the dependent-launch boundary between them.  Returns (best, median) or None when
+    capture is not possible."""
+    try:
+        cs = torch.cuda.Stream()
+        with torch.cuda.stream(cs):
+            fn(0, cs)                            # warm (lazy init outside the capture)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cs):
+            for i in range(reps):
+                fn(i, cs)
+        torch.cuda.synchronize()
+    except Exception:
+        return None
+    per = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(cs):
+            e0.record(cs)
+            g.replay()
+            e1.record(cs)
+        torch.cuda.synchronize()
+        per.append(e0.elapsed_time(e1) / reps)
+    per.sort()
+    return per[0], per[len(per) // 2]
+
+
 def cpu_baseline(pts_np, sc_np, budget_s, gpu_g1):
     """Reference CPU MSM (oracle/_ref = the unmodified reference srs_eval_at_s, -O2) on this
     host, 1 thread; falls back to the oracle restatement if the reference build is absent."""
@@ -110,7 +142,9 @@ def components(torch, hip, dev, st):
     n = 1 << 16
     pts, sc = make_msm_sets(torch, n, 8, dev, 7)
     res = torch.zeros((64, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
-    avg, med = event_avg_ms(torch, st, lambda i: hip.msm_g1_dev(pts[i % 8], sc[i % 8], n, res[i % 64], st), 64)
+    eag, _ = event_avg_ms(torch, st, lambda i: hip.msm_g1_dev(pts[i % 8], sc[i % 8], n, res[i % 64], st), 64)
+    gr = graph_avg_ms(torch, lambda i, s: hip.msm_g1_dev(pts[i % 8], sc[i % 8], n, res[i % 64], s), 64)
+    avg, med = gr if gr else (eag, eag)
     ph, sh = pts[0].cpu().numpy(), sc[0].cpu().numpy()
     hip.msm_g1(ph, sh)
     t0 = time.perf_counter()
@@ -119,16 +153,21 @@ def components(torch, hip, dev, st):
     host_us = (time.perf_counter() - t0) / 20 * 1e6
     out["msm_2^16"] = {"device_us_per_msm": round(avg * 1e3, 2), "median_us": round(med * 1e3, 2),
                        "Mpoint_s": round(n / (avg * 1e-3) / 1e6, 1),
+                       "eager_us_per_call": round(eag * 1e3, 2),
                        "host_call_us_incl_pcie": round(host_us, 1),
-                       "note": "one launch per MSM, back-to-back on one stream"}
+                       "note": "one launch per MSM, back-to-back on one stream: device time from 64 launches "
+                               "replayed as a HIP graph%s; eager_us_per_call = one Python call per launch "
+                               "(host-rate bound)" % ("" if gr else " (capture unavailable: eager)")}
     # C3: forward NTT 2^20 over BabyBear (Montgomery u32, in place, 2 passes)
     k = 20
     bufs = [torch.randint(0, 2013265921, (1 << k,), dtype=torch.int64, device=dev).to(torch.int32)
             for _ in range(4)]
     for b in bufs:
         hip.ntt_dev(b, k, False, st)
-    avg, med = event_avg_ms(torch, st, lambda i: hip.ntt_dev(bufs[i % 4], k, False, st), 50)
-    out["ntt_2^20_forward"] = {"ms": round(avg, 4), "Gelem_s": round((1 << k) / (avg * 1e-3) / 1e9, 2),
+    eag, _ = event_avg_ms(torch, st, lambda i: hip.ntt_dev(bufs[i % 4], k, False, st), 50)
+    gr = graph_avg_ms(torch, lambda i, s: hip.ntt_dev(bufs[i % 4], k, False, s), 50)
+    avg, med = gr if gr else (eag, eag)
+    out["ntt_2^20_forward"] = {"ms": round(avg, 4), "eager_ms": round(eag, 4), "Gelem_s": round((1 << k) / (avg * 1e-3) / 1e9, 2),
                                "passes": 2, "alg_bytes": 2 * 4 * (1 << k) * 2,
                                "GB_s_alg": round(2 * 8 * (1 << k) / (avg * 1e-3) / 1e9, 1)}
     # the same transform, 8 independent arrays sharing each pass's launch (plk_ntt_batch_dev)
