@@ -101,8 +101,9 @@ int plk_msm_finalize_dev(const uint32_t *d_logs, int batch, int stride, uint8_t 
  * order) */
 int plk_dlog_generator(uint8_t out[3]);
 
-/* poly_mul on device buffers: d_out holds la+lb-1 bytes; *d_out_nz receives the trimmed
- * length (0 = the zero polynomial, i.e. length 1).  d_work: plk_poly_mul_workspace() bytes. */
+/* poly_mul on device buffers: d_out holds la+lb-1 bytes (not overlapping d_a / d_b); *d_out_nz
+ * receives the trimmed length (0 = the zero polynomial, i.e. length 1).  d_work:
+ * plk_poly_mul_workspace() bytes. */
 size_t plk_poly_mul_workspace(size_t la, size_t lb);
 int plk_poly_mul_dev(const uint8_t *d_a, size_t la, const uint8_t *d_b, size_t lb, uint8_t *d_out,
                      uint32_t *d_out_nz, void *d_work, void *stream);
@@ -112,8 +113,9 @@ int plk_poly_mul_dev(const uint8_t *d_a, size_t la, const uint8_t *d_b, size_t l
  * transform size share each pass's launch, and operands given by the same pointer and length
  * are transformed once.  acc = 1 ADDS the product into the preceding job's output (a sum group:
  * a leader and up to two members of one shape; the members' out is not written).  Outputs are
- * untrimmed (la + lb - 1 bytes).  d_work: at least the largest single job's
- * plk_poly_mul_workspace(); plk_poly_mul_batch_workspace() bytes run every size group in one go. */
+ * untrimmed (la + lb - 1 bytes) and must not overlap any job's inputs (the last pass still reads
+ * input bytes for the top coefficients of wrapped products).  d_work: at least the largest single
+ * job's plk_poly_mul_workspace(); plk_poly_mul_batch_workspace() bytes run every size group in one go. */
 typedef struct {
   const uint8_t *a;
   size_t la;
