@@ -514,7 +514,7 @@ static int log2_ceil(uint64_t v) {
 // coefficients involve only the operands' last e coefficients (e - j terms each): the last
 // inverse pass computes them from the bytes and corrects both ends -- half the transform
 // size for O(e^2) MACs.
-constexpr uint64_t PLK_SPLIT_MAX = 16;
+constexpr uint64_t PLK_WRAP_MAX = 16;
 static int product_plan(uint64_t la, uint64_t lb, uint64_t* e_out) {
   const uint64_t rl = la + lb - 1;
   int k = log2_ceil(rl);
@@ -522,7 +522,7 @@ static int product_plan(uint64_t la, uint64_t lb, uint64_t* e_out) {
   const uint64_t lg = la > lb ? la : lb;
   if (k - 1 > PLK_SMALL_LOG) {
     const uint64_t ex = rl - (1ull << (k - 1));
-    if (ex <= PLK_SPLIT_MAX && ex < lg) { e = ex; k -= 1; }
+    if (ex <= PLK_WRAP_MAX && ex < lg) { e = ex; k -= 1; }
   }
   if (e_out) *e_out = e;
   return k;
@@ -561,7 +561,7 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
     int gs = 1;
     while (i + gs < m && g[i + gs].acc) gs++;
     const uint64_t mn = g[i].la < g[i].lb ? g[i].la : g[i].lb;
-    if ((uint64_t)gs * mn * 128 >= f29::P) use29 = false;   // centered residues (F29::from_byte)
+    if ((uint64_t)gs * mn * 128 >= f29::P) use29 = false;   // centered residues (F29::byte_val)
     if (!use29 && (uint64_t)gs * mn * 256 >= bb::P) {
       plk_set_error("poly_mul batch: a sum of %d products of %llu coefficients exceeds both fields", gs,
                     (unsigned long long)mn);
@@ -665,7 +665,7 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
   const int k = product_plan(la, lb, &e);
   if (k > bb::TWO_ADICITY) return PLK_ERR_RANGE;
   const uint32_t ninv = bb::hpow(1ull << k, bb::P - 2);   // normal form on purpose
-  if (k <= PLK_SMALL_LOG) {   // (never split: product_plan only splits above 2^(SMALL_LOG+1))
+  if (k <= PLK_SMALL_LOG) {   // (never wrapped: product_plan only wraps above 2^(SMALL_LOG+1))
     const size_t lds = (size_t)4 * (2 * col_stride(1 << k) + 2 * (1 << k));
     hipLaunchKernelGGL(polymul_small_kernel, dim3(1), dim3(1024), lds, st, d_a, la, d_b, lb, k, tw_fwd(), tw_inv(),
                        d_out, ninv, d_nz);
