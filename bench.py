@@ -30,8 +30,9 @@ MSM_BYTES_PER_POINT = 4  # 3 B G1 + 1 B HF read once
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50,
+                    help="timed steps; a step is ONE batched launch of --msm-batch MSMs over distinct input sets")
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log2n", type=int, default=22)
     ap.add_argument("--msm-batch", type=int, default=40,
                     help="MSMs per kernel launch (plk_msm_g1_batch_dev); every MSM is one step")
@@ -259,9 +260,9 @@ def main():
     sets = max(2 * B, -(-args.rotate_mib * (1 << 20) // (MSM_BYTES_PER_POINT * n)))
     sets = -(-sets // B) * B                       # whole launches never wrap the rotation
     pts, sc = make_msm_sets(torch, n, sets, dev, 1234 + rank)
-    K, W = args.steps, args.warmup
-    res = torch.zeros((W + K, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
-    outs = torch.zeros((K, 4), dtype=torch.uint8, device=dev)
+    K, W = args.steps, args.warmup            # steps of B MSMs (one batched launch each)
+    res = torch.zeros(((W + K) * B, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
+    outs = torch.zeros((K * B, 4), dtype=torch.uint8, device=dev)
 
     def launch(first, count):
         """MSMs first .. first+count-1 (one result record each), B per launch; MSM i reads
@@ -273,17 +274,17 @@ def main():
             hip.msm_g1_batch_dev(pts[s0], 3 * n, sc[s0], n, n, b, res[i], st)
             i += b
 
-    launch(0, W)
+    launch(0, W * B)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    launch(W, K)
-    logs = res[W:].view(torch.int32)[:, hip.MSM_LOG_OFFSET // 4].contiguous()
+    launch(W * B, K * B)
+    logs = res[W * B:].view(torch.int32)[:, hip.MSM_LOG_OFFSET // 4].contiguous()
     if world > 1:
         dist.all_reduce(logs, op=dist.ReduceOp.SUM)
-    hip.msm_finalize_dev(logs, K, 1, outs, st)
+    hip.msm_finalize_dev(logs, K * B, 1, outs, st)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -303,10 +304,10 @@ def main():
     # around L back-to-back launches of B MSMs (a pair around every launch would add its
     # own ~6 us per pair); the average includes the launch gaps, so it is an upper bound on
     # the kernel duration that rocprofv3 reports for the same command.
-    L = max(8, min(64, K // B))
+    L = max(8, min(64, K))
     res2 = torch.zeros((B, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    base = W + K
+    base = (W + K) * B
 
     def one(j):
         s0 = (base + j * B) % sets
@@ -334,7 +335,7 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
-    value = world * n * K / elapsed / 1e6
+    value = world * n * B * K / elapsed / 1e6
     line = {
         "metric": "G1-MSM Mpoint/s + NTT Gelem/s; end-to-end prove ms at 2^20 gates",
         "value": round(value, 1),
@@ -350,10 +351,10 @@ def main():
         "data": "synthetic: SRS points kG (k uniform 1..16), HF scalars uniform 0..16, %d distinct "
                 "input sets (%d MiB) rotated so every step reads cold data, resident in HBM"
                 % (sets, sets * MSM_BYTES_PER_POINT * n >> 20),
-        "config": {"workload": "2^%d-point G1 MSM (srs_eval_at_s) per GPU per step, point-range "
-                               "sharded over %d GPU(s); one RCCL all-reduce of the K partial logs"
-                               % (args.log2n, world),
-                   "points_per_gpu": n, "msms_per_launch": B, "parallelism": "dp%d" % world},
+        "config": {"workload": "%d x 2^%d-point G1 MSMs (srs_eval_at_s) per GPU per step: one batched "
+                               "launch over %d distinct input sets; point-range sharded over %d GPU(s), one "
+                               "RCCL all-reduce of the partial logs of all K steps" % (B, args.log2n, B, world),
+                   "points_per_gpu": n, "msms_per_step": B, "msms_per_launch": B, "parallelism": "dp%d" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": kname,
