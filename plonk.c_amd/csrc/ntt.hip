@@ -348,7 +348,7 @@ __global__ __launch_bounds__(1024) void trim_kernel(const uint8_t* __restrict__ 
 __global__ __launch_bounds__(256) void polymul_direct_kernel(const uint8_t* lg, uint64_t llg, const uint8_t* sh,
                                                              int lsh, uint8_t* out8, uint32_t* nz) {
   __shared__ uint32_t S[64];
-  if (threadIdx.x < lsh) S[threadIdx.x] = sh[threadIdx.x] % 17u;
+  if ((int)threadIdx.x < lsh) S[threadIdx.x] = sh[threadIdx.x] % 17u;
   __syncthreads();
   const uint64_t rl = llg + lsh - 1;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rl; i += (uint64_t)gridDim.x * blockDim.x) {
