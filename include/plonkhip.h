@@ -115,7 +115,9 @@ int plk_poly_mul_dev(const uint8_t *d_a, size_t la, const uint8_t *d_b, size_t l
  * a leader and up to two members of one shape; the members' out is not written).  Outputs are
  * untrimmed (la + lb - 1 bytes) and must not overlap any job's inputs (the last pass still reads
  * input bytes for the top coefficients of wrapped products).  d_work: at least the largest single
- * job's plk_poly_mul_workspace(); plk_poly_mul_batch_workspace() bytes run every size group in one go. */
+ * job's plk_poly_mul_workspace() (a sum group of g products: g times its member's); products run
+ * in launches of up to 12, cut between sum groups; plk_poly_mul_batch_workspace() bytes run every
+ * size group at full width. */
 typedef struct {
   const uint8_t *a;
   size_t la;

@@ -702,6 +702,10 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
       plk_set_error("poly_mul batch: sum-group member %d is not a transform-sized product", i);
       return PLK_ERR_ARG;
     }
+    if (j.acc && (i == 0 || jobs[i - 1].la != j.la || jobs[i - 1].lb != j.lb)) {   // adds into job i-1
+      plk_set_error("poly_mul batch: sum-group member %d does not follow a product of its shape", i);
+      return PLK_ERR_ARG;
+    }
     if (mn > PLK_DIRECT_MAX && k > PLK_SMALL_LOG) {
       if (mn * 256 >= bb::P || k > bb::TWO_ADICITY) return PLK_ERR_RANGE;
       ks[i] = k;
@@ -715,7 +719,10 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
     if (ks[i] < 0 || done[i]) continue;
     const int k = ks[i];
     const size_t per = (size_t)8 << k;
-    const int cap = (int)(work_bytes / per);
+    // a sub-group fits the workspace and one launch chunk of the wave engine, and never splits
+    // a sum group (a leader and the acc members right after it)
+    const size_t fit = work_bytes / per;
+    const int cap = (int)(fit < (size_t)PLK_WAVE_MAX_JOBS ? fit : (size_t)PLK_WAVE_MAX_JOBS);
     if (cap < 1) {
       plk_set_error("poly_mul batch: workspace %zu bytes < %zu", work_bytes, per);
       return PLK_ERR_ARG;
@@ -723,12 +730,23 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
     PlkPolyMulJob g[64];
     uint64_t ge[64];
     int m = 0;
-    for (int q = i; q < nj && m < cap; q++)
-      if (!done[q] && ks[q] == k) {
-        g[m] = jobs[q];
-        ge[m++] = es[q];
-        done[q] = true;
+    for (int q = i; q < nj; q++) {
+      if (done[q] || ks[q] != k || jobs[q].acc) continue;   // (members come with their leader)
+      int gs = 1;
+      while (q + gs < nj && jobs[q + gs].acc) gs++;
+      if (m + gs > cap) {
+        if (m == 0) {
+          plk_set_error("poly_mul batch: a sum group of %d products needs %zu workspace bytes", gs, per * gs);
+          return PLK_ERR_ARG;
+        }
+        break;
       }
+      for (int u = 0; u < gs; u++) {
+        g[m] = jobs[q + u];
+        ge[m++] = es[q + u];
+        done[q + u] = true;
+      }
+    }
     const int rc = ntt_group(g, m, k, ge, d_work, st);
     if (rc) return rc;
   }

@@ -178,9 +178,45 @@ def test_batch_sum_group(hip, oracle):
         assert _trim(outs[k]) == oracle.poly_mul(polys[i].tobytes(), polys[j].tobytes())
 
 
-def test_batch_rejects_group_across_launch_chunks(hip):
-    """a sum group must run in one launch chunk (12 products): leader at 11, member at 12"""
+def test_batch_group_across_launch_chunks(hip, oracle):
+    """13 products with a sum group at positions 11-12: the batch is cut into launch chunks of at
+    most 12 products at a group boundary (never inside a group)"""
     polys = [np.frombuffer(gen.poly_inputs(80 + i, n, 1)[0], np.uint8) for i, n in enumerate(_POOL)]
     spec = [(k % 6, (k + 1) % 6, 0) for k in range(11)] + [(0, 1, 0), (6, 7, 1)]
+    outs = _run_batch(hip, polys, spec)
+    for k in range(11):
+        i, j, _ = spec[k]
+        assert _trim(outs[k]) == oracle.poly_mul(polys[i].tobytes(), polys[j].tobytes()), k
+    full = len(polys[0]) + len(polys[1]) - 1
+    p1 = np.frombuffer(oracle.poly_mul(polys[0].tobytes(), polys[1].tobytes()), np.uint8).astype(np.int64)
+    p2 = np.frombuffer(oracle.poly_mul(polys[6].tobytes(), polys[7].tobytes()), np.uint8).astype(np.int64)
+    want = (np.pad(p1, (0, full - len(p1))) + np.pad(p2, (0, full - len(p2)))) % 17
+    assert outs[11] == want.astype(np.uint8).tobytes()
+
+
+def test_batch_small_workspace_and_bad_groups(hip, oracle):
+    """a workspace of one product's size runs every product (and a 2-product group needs two);
+    a member must follow a product of its own shape"""
+    import torch
+    dev = torch.device("cuda:0")
+    polys = [np.frombuffer(gen.poly_inputs(90 + i, n, 1)[0], np.uint8) for i, n in enumerate(_POOL)]
+    dp = [torch.from_numpy(p).to(dev) for p in polys]
+
+    def run(spec, ws):
+        outs = [torch.zeros(len(polys[i]) + len(polys[j]) - 1, dtype=torch.uint8, device=dev) for i, j, _ in spec]
+        jobs = [(dp[i], len(polys[i]), dp[j], len(polys[j]), o, acc) for (i, j, acc), o in zip(spec, outs)]
+        work = torch.zeros(ws, dtype=torch.uint8, device=dev)
+        hip.poly_mul_batch_dev(jobs, work, ws, torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        return [bytes(o.cpu().numpy()) for o in outs]
+
+    one = hip.poly_mul_workspace(len(polys[0]), len(polys[1]))
+    spec = [(0, 1, 0), (2, 3, 0), (4, 5, 0)]
+    for (i, j, _), out in zip(spec, run(spec, one)):
+        assert _trim(out) == oracle.poly_mul(polys[i].tobytes(), polys[j].tobytes())
     with pytest.raises(Exception, match="sum group"):
-        _run_batch(hip, polys, spec)
+        run([(0, 1, 0), (6, 7, 1)], one)                 # the group needs two products' workspace
+    outs = run([(0, 1, 0), (6, 7, 1)], 2 * one)
+    assert len(outs[0]) == len(polys[0]) + len(polys[1]) - 1
+    with pytest.raises(Exception, match="does not follow"):
+        run([(2, 3, 0), (0, 1, 1)], 2 * one)              # shape differs from the preceding job
