@@ -41,7 +41,12 @@ __constant__ uint8_t c_inv101[PLK_GF_P];       // a^-1 mod 101 (0 -> 0), for the
 
 namespace {
 
-constexpr int COPIES = 32;                     // one table copy per LDS bank
+#ifndef PLK_MSM_COPIES
+#define PLK_MSM_COPIES 8
+#endif
+constexpr int COPIES = PLK_MSM_COPIES;         // table copies, lane mod COPIES (8: a quarter of the fill of 32, no loss)
+constexpr int COPY_SHIFT = COPIES == 32 ? 7 : (COPIES == 16 ? 6 : (COPIES == 8 ? 5 : 4));   // log2(4 COPIES)
+static_assert(COPIES == 32 || COPIES == 16 || COPIES == 8 || COPIES == 4, "table copies");
 constexpr int TAB_ENTRIES = 512;
 
 // Encoded point j (0..15) of a 48-byte group held in w[0..11]: bytes 3j..3j+2 -> k = byte
@@ -65,7 +70,7 @@ __device__ __forceinline__ uint32_t point_term(uint32_t k, uint32_t c, const uin
 #if PLK_MSM_DIAG & 1
   const uint32_t e = idx * 0x9E37u + lane4;
 #else
-  const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + ((idx << 7) | lane4));
+  const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + ((idx << COPY_SHIFT) | lane4));
 #endif
   const uint32_t d = e - k;
   bad |= d >= 256u;
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, u
 
   const uint64_t tid = (uint64_t)blockIdx.x * NT + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * NT;
-  const uint32_t lane4 = (threadIdx.x & 31u) << 2;
+  const uint32_t lane4 = (threadIdx.x & (COPIES - 1u)) << 2;
   uint32_t acc = 0;
   bool bad = false;
   TableFill<NT> fill;
