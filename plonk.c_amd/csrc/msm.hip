@@ -432,7 +432,9 @@ void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* gpt
   if (b > 8ull * 65535ull) b = 8ull * 65535ull;   // the finish's per-shard ticket field is 16 bits
   const uint64_t per_thread = groups / (b * (uint64_t)th);
   int g = 1;
-  const int gmax = (env_g == 1 || env_g == 2 || env_g == 4) ? env_g : 1;
+  // two groups in flight per thread where a thread has them (with the 16 KB table four blocks
+  // share a CU; +1.5-2 % on the headline over one group; PLK_MSM_G overrides)
+  const int gmax = (env_g == 1 || env_g == 2 || env_g == 4) ? env_g : 2;
   while (g < gmax && (uint64_t)(2 * g) <= per_thread) g *= 2;
   *threads = th;
   *blocks = (int)b;
