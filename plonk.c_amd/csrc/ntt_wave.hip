@@ -47,6 +47,9 @@ namespace {
 #ifndef PLK_NTT_RC13
 #define PLK_NTT_RC13 3         // register bits per thread of the 2^13-tile center kernel
 #endif
+#ifndef PLK_NTT_BYTE_LUT
+#define PLK_NTT_BYTE_LUT 1     // byte values through a 256-entry LDS table (0: arithmetic in registers)
+#endif
 #ifndef PLK_NTT_CW13
 #define PLK_NTT_CW13 8         // min waves per SIMD (launch bound): 8 = two 1024-thread blocks per CU
 #endif
@@ -366,6 +369,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
     for (int k = 0; k < G::E; k++) {
       const uint32_t o = G::template toff_k<0, false>(p, o0, b0, k);
       v[k] = o < lim ? st[o] : 0u;
+      if (!PLK_NTT_BYTE_LUT) v[k] = F::byte_val(v[k]);
     }
   } else {
 #pragma unroll
@@ -388,11 +392,11 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
       }
     }
   }
-  __shared__ uint32_t lut[FROM_U8 ? 256 : 1];
-  if (FROM_U8 && tid < 256) lut[tid] = F::byte_val(tid);
+  __shared__ uint32_t lut[FROM_U8 && PLK_NTT_BYTE_LUT ? 256 : 1];
+  if (FROM_U8 && PLK_NTT_BYTE_LUT && tid < 256) lut[tid] = F::byte_val(tid);
   load_pass_tw<M, G::NT>(Tsm, tw.small);
   __syncthreads();
-  if constexpr (FROM_U8) {
+  if constexpr (FROM_U8 && PLK_NTT_BYTE_LUT) {
 #pragma unroll
     for (int k = 0; k < G::E; k++) v[k] = lut[v[k]];
   }
