@@ -336,7 +336,10 @@ __global__ __launch_bounds__(256) void copy3_kernel(Copy3 c) {
 // ------------------------------------------------------------------ poly_eval (batched)
 // Horner of src/poly.h:265-272 == sum c_i x^i mod 17; x^i = x^(i mod 16) for x != 0.
 constexpr int EV_MAX = 16;
-constexpr int EV_BLOCKS = 64;   // x 256 threads x 4 uint4 loads in flight each
+#ifndef PLK_EV_BLOCKS
+#define PLK_EV_BLOCKS 64
+#endif
+constexpr int EV_BLOCKS = PLK_EV_BLOCKS;   // x 256 threads x 4 uint4 loads in flight each
 constexpr int TICK_STRIDE = 32;   // one 128-byte line per arrival word
 enum EvPost : int { EV_POST_NONE = 0, EV_POST_ACC = 1, EV_POST_R4 = 4 };
 struct EvArgs {
