@@ -41,12 +41,11 @@ __constant__ uint8_t c_inv101[PLK_GF_P];       // a^-1 mod 101 (0 -> 0), for the
 
 namespace {
 
-#ifndef PLK_MSM_COPIES
-#define PLK_MSM_COPIES 8
-#endif
-constexpr int COPIES = PLK_MSM_COPIES;         // table copies, lane mod COPIES (8: a quarter of the fill of 32, no loss)
-constexpr int COPY_SHIFT = COPIES == 32 ? 7 : (COPIES == 16 ? 6 : (COPIES == 8 ? 5 : 4));   // log2(4 COPIES)
-static_assert(COPIES == 32 || COPIES == 16 || COPIES == 8 || COPIES == 4, "table copies");
+// The table is kept in C copies (copy = lane mod C, entry-major: the C copies of an entry are
+// consecutive words): more copies mean fewer bank conflicts in the gathers but a bigger
+// per-block fill.  The launcher picks C per launch shape (plk_msm_geometry).
+template <int C>
+constexpr int copy_shift() { return C == 32 ? 7 : (C == 16 ? 6 : (C == 8 ? 5 : (C == 4 ? 4 : (C == 2 ? 3 : 2)))); }
 constexpr int TAB_ENTRIES = 512;
 
 // Encoded point j (0..15) of a 48-byte group held in w[0..11]: bytes 3j..3j+2 -> k = byte
@@ -64,13 +63,14 @@ __device__ __forceinline__ uint32_t encode(uint32_t x, uint32_t y, uint32_t f) {
 
 // log(P) * c for one encoded point; flags non-canonical encodings in bad.  The product of
 // a flagged point is garbage, which is fine: the result is then recomputed serially.
+template <int C>
 __device__ __forceinline__ uint32_t point_term(uint32_t k, uint32_t c, const uint32_t* tab, uint32_t lane4,
                                                bool& bad) {
   const uint32_t idx = (k >> 16) & 0x1FFu;
 #if PLK_MSM_DIAG & 1
   const uint32_t e = idx * 0x9E37u + lane4;
 #else
-  const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + ((idx << COPY_SHIFT) | lane4));
+  const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + ((idx << copy_shift<C>()) | lane4));
 #endif
   const uint32_t d = e - k;
   bad |= d >= 256u;
@@ -81,26 +81,31 @@ __device__ __forceinline__ uint32_t point_term(uint32_t k, uint32_t c, const uin
 // source words are loaded FIRST, the group loads after, and the LDS writes then wait with a
 // counted vmcnt for the table words only (a fill loop that waits vmcnt(0) would also wait
 // for the whole first group to arrive from HBM -- ~2 us per launch).
-template <int NT>
+// C >= 4: uint4 stores of 4 copies of one entry; C < 4: one word store per (entry, copy).
+template <int NT, int C>
 struct TableFill {
-  static constexpr int PER = TAB_ENTRIES * COPIES / 4 / NT;   // uint4 stores per thread
+  static constexpr int W = C >= 4 ? 4 : 1;                     // words per store
+  static constexpr int STORES = TAB_ENTRIES * C / W;
+  static constexpr int PER = (STORES + NT - 1) / NT;            // stores per thread
   uint32_t v[PER];
   __device__ __forceinline__ void load() {
 #pragma unroll
-    for (int j = 0; j < PER; j++) v[j] = c_ytab[(threadIdx.x + j * NT) / (COPIES / 4)];
+    for (int j = 0; j < PER; j++) {
+      const uint32_t i = threadIdx.x + j * NT;
+      v[j] = c_ytab[(i * W / C) & (TAB_ENTRIES - 1)];
+    }
   }
   __device__ __forceinline__ void store(uint32_t* tab) const {
-    uint4* t4 = reinterpret_cast<uint4*>(tab);
 #pragma unroll
-    for (int j = 0; j < PER; j++) t4[threadIdx.x + j * NT] = make_uint4(v[j], v[j], v[j], v[j]);
+    for (int j = 0; j < PER; j++) {
+      const uint32_t i = threadIdx.x + j * NT;
+      if (STORES % NT == 0 || i < STORES) {
+        if (W == 4) reinterpret_cast<uint4*>(tab)[i] = make_uint4(v[j], v[j], v[j], v[j]);
+        else tab[i] = v[j];
+      }
+    }
   }
 };
-
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, PLK_WAVE);
-  return v;
-}
 
 struct Group {
   uint4 q0, q1, q2, s;
@@ -126,25 +131,26 @@ __device__ __forceinline__ Group load_group(const uint4* p4, const uint4* s4, ui
   return r;
 }
 
-template <int J>
+template <int C, int J>
 __device__ __forceinline__ void group_term(const uint32_t (&w)[12], const uint32_t (&sw)[4], const uint32_t* tab,
                                            uint32_t lane4, bool& bad, uint32_t& part) {
-  part += point_term(point_bytes<J>(w), (sw[J >> 2] >> (8 * (J & 3))) & 0xFFu, tab, lane4, bad);
+  part += point_term<C>(point_bytes<J>(w), (sw[J >> 2] >> (8 * (J & 3))) & 0xFFu, tab, lane4, bad);
 }
 
+template <int C>
 __device__ __forceinline__ uint32_t group_sum(const Group& g, const uint32_t* tab, uint32_t lane4, bool& bad) {
   const uint32_t w[12] = {g.q0.x, g.q0.y, g.q0.z, g.q0.w, g.q1.x, g.q1.y, g.q1.z, g.q1.w,
                           g.q2.x, g.q2.y, g.q2.z, g.q2.w};
   const uint32_t sw[4] = {g.s.x, g.s.y, g.s.z, g.s.w};
   uint32_t part = 0;
-  group_term<0>(w, sw, tab, lane4, bad, part);   group_term<1>(w, sw, tab, lane4, bad, part);
-  group_term<2>(w, sw, tab, lane4, bad, part);   group_term<3>(w, sw, tab, lane4, bad, part);
-  group_term<4>(w, sw, tab, lane4, bad, part);   group_term<5>(w, sw, tab, lane4, bad, part);
-  group_term<6>(w, sw, tab, lane4, bad, part);   group_term<7>(w, sw, tab, lane4, bad, part);
-  group_term<8>(w, sw, tab, lane4, bad, part);   group_term<9>(w, sw, tab, lane4, bad, part);
-  group_term<10>(w, sw, tab, lane4, bad, part);  group_term<11>(w, sw, tab, lane4, bad, part);
-  group_term<12>(w, sw, tab, lane4, bad, part);  group_term<13>(w, sw, tab, lane4, bad, part);
-  group_term<14>(w, sw, tab, lane4, bad, part);  group_term<15>(w, sw, tab, lane4, bad, part);
+  group_term<C, 0>(w, sw, tab, lane4, bad, part);   group_term<C, 1>(w, sw, tab, lane4, bad, part);
+  group_term<C, 2>(w, sw, tab, lane4, bad, part);   group_term<C, 3>(w, sw, tab, lane4, bad, part);
+  group_term<C, 4>(w, sw, tab, lane4, bad, part);   group_term<C, 5>(w, sw, tab, lane4, bad, part);
+  group_term<C, 6>(w, sw, tab, lane4, bad, part);   group_term<C, 7>(w, sw, tab, lane4, bad, part);
+  group_term<C, 8>(w, sw, tab, lane4, bad, part);   group_term<C, 9>(w, sw, tab, lane4, bad, part);
+  group_term<C, 10>(w, sw, tab, lane4, bad, part);  group_term<C, 11>(w, sw, tab, lane4, bad, part);
+  group_term<C, 12>(w, sw, tab, lane4, bad, part);  group_term<C, 13>(w, sw, tab, lane4, bad, part);
+  group_term<C, 14>(w, sw, tab, lane4, bad, part);  group_term<C, 15>(w, sw, tab, lane4, bad, part);
   return part;                                   // <= 16 * 101 * 255
 }
 
@@ -165,10 +171,10 @@ __device__ __forceinline__ uint32_t group_sum(const Group& g, const uint32_t* ta
 // no fence or re-read needed), re-arms the shard word and adds the shard total to
 // res[b].top the same way; the last shard's finisher writes log / irregular / g1 and
 // re-arms top.  Every word is zero again when the launch ends.
-template <bool ALIGNED, int NT, int G>
+template <bool ALIGNED, int NT, int G, int COPIES>
 __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, uint64_t pstride,
                                                       const uint8_t* sc_base, uint64_t sstride,
-                                                      uint64_t n, PlkMsmResult* res_base) {
+                                                      uint64_t n, uint32_t full, PlkMsmResult* res_base) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[TAB_ENTRIES * COPIES];
   __shared__ uint32_t wsum[NT / PLK_WAVE];
   __shared__ uint32_t wbad[NT / PLK_WAVE];
@@ -181,79 +187,83 @@ __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, u
   const uint32_t lane4 = (threadIdx.x & (COPIES - 1u)) << 2;
   uint32_t acc = 0;
   bool bad = false;
-  TableFill<NT> fill;
+  TableFill<NT, COPIES> fill;
   fill.load();                                  // table words first ...
 
   const uint64_t ngroups = n >> 4;
-  if (ALIGNED && ngroups > 0) {
+  if (ALIGNED) {
     // 16 points per thread-step: 48 B of points (3 x dwordx4) + 16 B of scalars (1 x dwordx4)
     const uint4* p4 = reinterpret_cast<const uint4*>(pts);
     const uint4* s4 = reinterpret_cast<const uint4*>(sc);
-    const uint64_t last = ngroups - 1;
-    // Each iteration issues the loads of G groups (g, g + stride, ..., g + (G-1) stride;
-    // indices clamped to the last group -- a cache hit -- and masked in the sums) and then
-    // consumes them in issue order within the same iteration: no loaded register is carried
-    // around the loop (a loop-carried prefetch makes the register allocator copy the
-    // arrived group at the latch, i.e. wait for it, serialising loads and compute), the
-    // compiler's vmcnt bookkeeping is exact (vmcnt(4 (G-1-j)) before group j) and a thread
-    // has up to 64 G bytes in flight.  Block-uniform trip count; the first iteration is
-    // peeled so the table fill sits between its loads and its compute.
+    // `full` (from the host: ngroups / (stride G)) iterations in which every thread of the grid
+    // has G groups, then one masked remainder step.  An iteration issues the loads of its G
+    // groups (g, g + stride, ...) and then consumes them in issue order: no loaded register is
+    // carried around the loop (a loop-carried prefetch makes the register allocator copy the
+    // arrived group at the latch, i.e. wait for it), the compiler's vmcnt bookkeeping is exact
+    // (vmcnt(4 (G-1-j)) before group j), and a group's lookups run while the later groups of
+    // the same iteration are still arriving -- in a launch of one resident round (a single
+    // MSM) that hides all but the last group's VALU work behind the stream.  The first
+    // iteration is peeled so the table fill sits between its loads and its compute.
     const uint64_t span = stride * G;
-    const uint32_t iters = (uint32_t)((ngroups - (uint64_t)blockIdx.x * NT + span - 1) / span);
     uint64_t g = tid;
-    {
+    if (full > 0) {
       Group cur[G];
       asm volatile("" ::: "memory");
 #pragma unroll
       for (int j = 0; j < G; j++) {
-        const uint64_t gj = g + j * stride;
-        cur[j] = load_group(p4, s4, gj < last ? gj : last);
+        cur[j] = load_group(p4, s4, g + j * stride);
         asm volatile("" ::: "memory");               // keep group j's loads older than j+1's
       }
       if (!(PLK_MSM_DIAG & 1)) {
         fill.store(tab);                              // ... LDS fill waits for the table words only
         __syncthreads();
       }
+      uint32_t part = 0;
 #pragma unroll
-      for (int j = 0; j < G; j++) {
-        const uint32_t part = group_sum(cur[j], tab, lane4, bad) % PLK_GROUP_ORDER;
-        acc += g + j * stride < ngroups ? part : 0u;
-      }
-    }
-    for (uint32_t it = 1; it < iters; it++) {
+      for (int j = 0; j < G; j++) part += group_sum<COPIES>(cur[j], tab, lane4, bad);
+      acc = part % PLK_GROUP_ORDER;
       g += span;
+    } else if (!(PLK_MSM_DIAG & 1)) {
+      fill.store(tab);
+      __syncthreads();
+    }
+    for (uint32_t it = 1; it < full; it++, g += span) {
       Group cur[G];
       asm volatile("" ::: "memory");
 #pragma unroll
       for (int j = 0; j < G; j++) {
-        const uint64_t gj = g + j * stride;
-        cur[j] = load_group(p4, s4, gj < last ? gj : last);
+        cur[j] = load_group(p4, s4, g + j * stride);
         asm volatile("" ::: "memory");
       }
+      uint32_t part = 0;
 #pragma unroll
-      for (int j = 0; j < G; j++) {
-        const uint32_t part = group_sum(cur[j], tab, lane4, bad) % PLK_GROUP_ORDER;
-        acc += g + j * stride < ngroups ? part : 0u;
-      }
+      for (int j = 0; j < G; j++) part += group_sum<COPIES>(cur[j], tab, lane4, bad);
+      acc += part % PLK_GROUP_ORDER;
+    }
+    // remainder: fewer than G groups per thread
+#pragma unroll
+    for (int j = 0; j < G; j++) {
+      const uint64_t gj = g + j * stride;
+      if (gj < ngroups) acc += group_sum<COPIES>(load_group(p4, s4, gj), tab, lane4, bad) % PLK_GROUP_ORDER;
     }
     // tail (n mod 16 points), one point per thread of the first block
     const uint64_t base = ngroups << 4;
     if (blockIdx.x == 0 && base + threadIdx.x < n) {
       const uint64_t i = base + threadIdx.x;
-      acc += point_term(encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), sc[i], tab, lane4, bad);
+      acc += point_term<COPIES>(encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), sc[i], tab, lane4, bad);
     }
   } else {
     fill.store(tab);
     __syncthreads();
     for (uint64_t i = tid; i < n; i += stride) {
-      acc += point_term(encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), sc[i], tab, lane4, bad);
+      acc += point_term<COPIES>(encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), sc[i], tab, lane4, bad);
       acc %= PLK_GROUP_ORDER;
     }
   }
   acc %= PLK_GROUP_ORDER;
 
   const uint32_t wave = threadIdx.x / PLK_WAVE;
-  const uint32_t s = wave_sum(acc);
+  const uint32_t s = plk_wave_sum(acc);
   const uint64_t anybad = __ballot(bad);
   if ((threadIdx.x & (PLK_WAVE - 1)) == 0) {
     wsum[wave] = s;
@@ -412,12 +422,13 @@ int env_int(const char* name) {
 }
 }  // namespace
 
-void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* gpt) {
-  static int env_threads = -1, env_blocks = -1, env_g = -1;
+void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* gpt, int* copies) {
+  static int env_threads = -1, env_blocks = -1, env_g = -1, env_c = -1;
   if (env_threads < 0) {
     env_threads = env_int("PLK_MSM_THREADS");
     env_blocks = env_int("PLK_MSM_MAX_BLOCKS");
     env_g = env_int("PLK_MSM_G");
+    env_c = env_int("PLK_MSM_COPIES");
   }
   const uint64_t groups = n >> 4;
   int th = groups >= 64ull * 1024 ? 512 : 256;
@@ -436,27 +447,41 @@ void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* gpt
   // share a CU; +1.5-2 % on the headline over one group; PLK_MSM_G overrides)
   const int gmax = (env_g == 1 || env_g == 2 || env_g == 4) ? env_g : 2;
   while (g < gmax && (uint64_t)(2 * g) <= per_thread) g *= 2;
+  // table copies: eight keep the gathers nearly conflict-free (a single 2^22-point MSM: lookups
+  // 0.2 us shorter than with one copy, tools/msm_single_lab.hip) and the fill is off the
+  // critical path (its words are loaded before the points); PLK_MSM_COPIES=1 for tuning
+  int c = 8;
+  if (env_c == 1 || env_c == 8) c = env_c;
   *threads = th;
   *blocks = (int)b;
   if (gpt) *gpt = g;
+  if (copies) *copies = c;
 }
 
 namespace {
-template <bool A, int T>
+template <bool A, int T, int C>
 void go_g(int g, dim3 grid, hipStream_t st, const uint8_t* p, uint64_t ps, const uint8_t* s, uint64_t ss, uint64_t n,
           PlkMsmResult* r) {
-  if (!A || g == 1)
-    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 1>), grid, dim3(T), 0, st, p, ps, s, ss, n, r);
+  if (!A) g = 1;
+  const uint64_t span = (uint64_t)grid.x * T * g;
+  const uint32_t full = (uint32_t)((n >> 4) / span);
+  if (g == 1)
+    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 1, C>), grid, dim3(T), 0, st, p, ps, s, ss, n, full, r);
   else if (g == 2)
-    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 2>), grid, dim3(T), 0, st, p, ps, s, ss, n, r);
+    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 2, C>), grid, dim3(T), 0, st, p, ps, s, ss, n, full, r);
   else
-    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 4>), grid, dim3(T), 0, st, p, ps, s, ss, n, r);
+    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 4, C>), grid, dim3(T), 0, st, p, ps, s, ss, n, full, r);
 }
 template <int T>
-void go_t(bool aligned, int g, dim3 grid, hipStream_t st, const uint8_t* p, uint64_t ps, const uint8_t* s, uint64_t ss,
-          uint64_t n, PlkMsmResult* r) {
-  if (aligned) go_g<true, T>(g, grid, st, p, ps, s, ss, n, r);
-  else go_g<false, T>(g, grid, st, p, ps, s, ss, n, r);
+void go_t(bool aligned, int g, int c, dim3 grid, hipStream_t st, const uint8_t* p, uint64_t ps, const uint8_t* s,
+          uint64_t ss, uint64_t n, PlkMsmResult* r) {
+  if (aligned) {
+    if (c == 1) go_g<true, T, 1>(g, grid, st, p, ps, s, ss, n, r);
+    else go_g<true, T, 8>(g, grid, st, p, ps, s, ss, n, r);
+  } else {
+    if (c == 1) go_g<false, T, 1>(g, grid, st, p, ps, s, ss, n, r);
+    else go_g<false, T, 8>(g, grid, st, p, ps, s, ss, n, r);
+  }
 }
 }  // namespace
 
@@ -467,14 +492,14 @@ int plk_msm_batch_launch(const uint8_t* d_pts, uint64_t pstride, const uint8_t* 
     plk_set_error("plk_msm batch %d too large", batch);
     return PLK_ERR_RANGE;
   }
-  int threads, blocks, g;
-  plk_msm_geometry(n, batch, &threads, &blocks, &g);
+  int threads, blocks, g, c;
+  plk_msm_geometry(n, batch, &threads, &blocks, &g, &c);
   const bool aligned = ((uintptr_t)d_pts % 16 == 0) && ((uintptr_t)d_sc % 16 == 0) &&
                        (batch == 1 || (pstride % 16 == 0 && sstride % 16 == 0));
   const dim3 grid(blocks, batch);
-  if (threads == 1024) go_t<1024>(aligned, g, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
-  else if (threads == 512) go_t<512>(aligned, g, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
-  else go_t<256>(aligned, g, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
+  if (threads == 1024) go_t<1024>(aligned, g, c, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
+  else if (threads == 512) go_t<512>(aligned, g, c, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
+  else go_t<256>(aligned, g, c, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }

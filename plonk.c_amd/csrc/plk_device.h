@@ -10,6 +10,18 @@
 
 #define PLK_WAVE 64
 
+// Sum over the 64 lanes of a wave (every lane active), wave-uniform result: DPP row rotations
+// leave each 16-lane row's sum in all its lanes, then the four row sums are read out as
+// scalars.  No LDS round trips (__shfl_xor is ds_bpermute: ~6 dependent LDS latencies).
+__device__ __forceinline__ uint32_t plk_wave_sum(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);   // row_ror:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);   // row_ror:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xF, 0xF, false);   // row_ror:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xF, 0xF, false);   // row_ror:1
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
 // ----------------------------------------------------------------------------------------
 // BabyBear Montgomery arithmetic, R = 2^32.  Values are kept fully reduced in [0, p).
 // ----------------------------------------------------------------------------------------

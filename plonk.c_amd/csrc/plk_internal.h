@@ -29,7 +29,7 @@ void plk_set_error(const char* fmt, ...);
 
 // msm.hip
 int plk_msm_upload_tables(const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101);
-void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* groups_per_thread);
+void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* groups_per_thread, int* copies);
 int plk_msm_batch_launch(const uint8_t* d_pts, uint64_t pstride, const uint8_t* d_sc, uint64_t sstride, uint64_t n,
                          int batch, PlkMsmResult* d_res, hipStream_t st);
 int plk_msm_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsmResult* d_res, hipStream_t st);

@@ -32,6 +32,9 @@ def summarise(db, sub=None):
 
 
 if __name__ == "__main__":
+    width = 60
+    if "--wide" in sys.argv:
+        width = 110
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     out_json = None
     if "--json" in sys.argv:
@@ -41,8 +44,8 @@ if __name__ == "__main__":
     sub = args[1] if len(args) > 1 else None
     rows = summarise(db, sub)
     for r in rows:
-        print("%-60s grid=%-14s blk=%-5d calls=%-6d avg=%9.3f us  med=%9.3f  min=%9.3f" % (
-            r["kernel"][:60], "%dx%d" % tuple(r["grid"]), r["block"], r["calls"], r["avg_us"],
+        print("%-*s grid=%-14s blk=%-5d calls=%-6d avg=%9.3f us  med=%9.3f  min=%9.3f" % (
+            width, r["kernel"][:width], "%dx%d" % tuple(r["grid"]), r["block"], r["calls"], r["avg_us"],
             r["median_us"], r["min_us"]))
     if out_json:
         with open(out_json, "w") as f:
