@@ -118,6 +118,15 @@ def test_poly_large_digests(oracle):
             assert oracle.poly_mul(a, b) == out
 
 
+def test_poly_c3_size_digests(oracle):
+    """the independent NTT checker agrees with the reference at config C3's size"""
+    for c in load_golden("poly_mul_big.json")["large"]:
+        a, b = gen.poly_inputs(c["seed"], c["la"], c["lb"])
+        out = oracle.poly_mul_ntt(a, b)
+        assert len(out) == c["len"]
+        assert gen.digest(np.frombuffer(out, np.uint8)) == c["sha256"]
+
+
 def test_poly_survey_digests(oracle):
     for c in load_golden("poly_mul.json")["survey_xorshift"]:
         a, b = oracle.gen_survey_poly(c["n"])

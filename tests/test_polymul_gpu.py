@@ -25,6 +25,18 @@ def test_golden_large_digests(hip, idx):
     assert gen.digest(np.frombuffer(out, np.uint8)) == c["sha256"]
 
 
+@pytest.mark.parametrize("idx", range(3))
+def test_golden_c3_size_digests(hip, idx):
+    """Config C3 at its own size: reference digests of 2^18 x 2^18, 2^19 x 2^19 (the
+    2^20-coefficient product) and a ragged shape around it (tests/golden/poly_mul_big.json,
+    recorded from oracle/_ref by make_golden.py poly_big)."""
+    c = load_golden("poly_mul_big.json")["large"][idx]
+    a, b = gen.poly_inputs(c["seed"], c["la"], c["lb"])
+    out = hip.poly_mul(a, b)
+    assert len(out) == c["len"]
+    assert gen.digest(np.frombuffer(out, np.uint8)) == c["sha256"]
+
+
 def test_survey_digests(hip, oracle):
     for c in load_golden("poly_mul.json")["survey_xorshift"]:
         a, b = oracle.gen_survey_poly(c["n"])
