@@ -2,17 +2,25 @@
 """Benchmark of the PLONK hot path on MI355X (BASELINE.json metric).
 
 Headline (`value`): G1-MSM Mpoint/s -- the KZG commitment MSM srs_eval_at_s
-(reference src/srs.h:53-68) over 2^22 points per GPU (config "2^22-point G1 MSM"), inputs
-resident in HBM, rotated over > 512 MiB of distinct input sets so no step is served from the
-256 MiB Infinity Cache.  One step = one complete MSM (3 B point + 1 B scalar per point) to a
-finished G1.  With N GPUs every rank owns a 2^22-point shard of one N*2^22-point MSM
-(weak scaling, point-range sharding); the K partial discrete logs of the timed steps are
-summed with ONE RCCL all-reduce and mapped to points inside the timed region.
+(reference src/srs.h:53-68) over 2^22-point MSMs (config "2^22-point G1 MSM"), inputs resident
+in HBM, rotated over > 512 MiB of distinct input sets so no step is served from the 256 MiB
+Infinity Cache.  A step = one batched launch of --msm-batch complete MSMs (3 B point + 1 B scalar
+per point) finished to G1s.
 
-Also reported (rank 0, `components`): the 2^16-point MSM (config C2), the 2^20 forward NTT
-(config C3, Gelem/s), poly_mul 2^19 x 2^19, and the reference CPU path timed on this host.
+Multi-GPU (one process per GPU, torch.distributed over RCCL): by default STRONG scaling, the
+config SURVEY §8 d3 names -- every 2^22-point MSM is split into contiguous point ranges
+(plonkhip.dist.shard_range), rank r reads only its range, and the partial discrete logs of all
+K steps are finished by plonkhip.dist.finish_sharded: ONE RCCL all-reduce SUM + the log -> point
+map (+ the gathered serial fold for MSMs with irregular encodings).  --weak: every rank owns a
+2^22-point shard of an N * 2^22-point MSM instead.  After timing, rank 0 recomputes the first
+MSM on one GPU and (strong, 2^22) the sharded path runs the reference golden input
+tests/golden/msm.json large[7]; both results are reported.
 
-    python bench.py [--gpus N --steps K --warmup W --log2n 22]
+Also reported (rank 0, `components`): one 2^22 MSM per launch, the 2^16-point MSM (config C2),
+the 2^20 forward NTT (config C3) and poly_mul 2^19 x 2^19 with their rooflines, the 2^20-gate
+prove (C5), and the reference CPU path timed on this host (MSM, schoolbook poly_mul, toy prove).
+
+    python bench.py [--gpus N --steps K --warmup W --log2n 22 --weak]
 """
 import argparse
 import json
@@ -25,6 +33,14 @@ sys.path.insert(0, os.path.join(ROOT, "plonk.c_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
 MSM_BYTES_PER_POINT = 4  # 3 B G1 + 1 B HF read once
+NTT_BYTES_PER_ELEM = 8   # u32 read + write once
+
+
+def roofline_obj(alg_bytes, ms, what):
+    """HBM roofline of a component: algorithmic bytes / measured device time vs the spec peak"""
+    gbs = alg_bytes / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "alg_bytes": int(alg_bytes), "alg_bytes_def": what}
 
 
 def parse():
@@ -42,23 +58,42 @@ def parse():
     ap.add_argument("--no-components", action="store_true")
     ap.add_argument("--profile-only", action="store_true",
                     help="just launch the timed MSM loop (for rocprofv3 runs)")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: every rank owns a full 2^log2n-point shard (default: strong, each "
+                         "2^log2n-point MSM split over the ranks)")
     return ap.parse_args()
 
 
-def make_msm_sets(torch, n, sets, dev, seed):
-    """Synthetic SRS points kG (k uniform in [1,16], G = (1,2)) and HF scalars in [0,16]."""
-    kg = torch.tensor([[1, 2, 0], [68, 74, 0], [26, 45, 0], [65, 98, 0], [12, 32, 0], [32, 42, 0],
-                       [91, 35, 0], [18, 49, 0], [18, 52, 0], [91, 66, 0], [32, 59, 0],
-                       [12, 69, 0], [65, 3, 0], [26, 56, 0], [68, 27, 0], [1, 99, 0]],
-                      dtype=torch.uint8, device=dev)
+KG16 = [[1, 2, 0], [68, 74, 0], [26, 45, 0], [65, 98, 0], [12, 32, 0], [32, 42, 0], [91, 35, 0], [18, 49, 0],
+        [18, 52, 0], [91, 66, 0], [32, 59, 0], [12, 69, 0], [65, 3, 0], [26, 56, 0], [68, 27, 0], [1, 99, 0]]
+
+
+def make_msm_set(torch, n, dev, seed):
+    """One synthetic MSM input: SRS points kG (k uniform in [1,16], G = (1,2)) and HF scalars in
+    [0,16], from a device generator seeded per set (any rank can rebuild any set)."""
+    kg = torch.tensor(KG16, dtype=torch.uint8, device=dev)
     g = torch.Generator(device=dev).manual_seed(seed)
-    pts = torch.empty((sets, 3 * n), dtype=torch.uint8, device=dev)
-    sc = torch.empty((sets, n), dtype=torch.uint8, device=dev)
-    for s in range(sets):
-        k = torch.randint(0, 16, (n,), generator=g, device=dev)
-        pts[s] = kg[k].reshape(-1)
-        sc[s] = torch.randint(0, 17, (n,), generator=g, device=dev, dtype=torch.int16).to(torch.uint8)
+    k = torch.randint(0, 16, (n,), generator=g, device=dev)
+    pts = kg[k].reshape(-1)
+    sc = torch.randint(0, 17, (n,), generator=g, device=dev, dtype=torch.int16).to(torch.uint8)
     return pts, sc
+
+
+def make_shard_sets(torch, n, lo, hi, sets, dev, seed_of):
+    """Rows s = this rank's point range [lo, hi) of input set s (seed seed_of(s))."""
+    m = hi - lo
+    pts = torch.empty((sets, 3 * m), dtype=torch.uint8, device=dev)
+    sc = torch.empty((sets, m), dtype=torch.uint8, device=dev)
+    for s in range(sets):
+        p, c = make_msm_set(torch, n, dev, seed_of(s))
+        pts[s] = p[3 * lo:3 * hi]
+        sc[s] = c[lo:hi]
+    return pts, sc
+
+
+def make_msm_sets(torch, n, sets, dev, seed):
+    """`sets` full n-point inputs (rows), seeds seed + s."""
+    return make_shard_sets(torch, n, 0, n, sets, dev, lambda s: seed + s)
 
 
 def event_avg_ms(torch, st, fn, reps, rounds=3):
@@ -137,6 +172,102 @@ def cpu_baseline(pts_np, sc_np, budget_s, gpu_g1):
             "seconds_per_msm": round(dt, 4), "matches_gpu": out == gpu_g1}
 
 
+def kernel_source_hash():
+    """SHA-256 (16 hex) of the MSM kernel's sources: a PMC record is used only for this code."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("msm.hip", "plk_device.h", "plk_internal.h"):
+        with open(os.path.join(ROOT, "plonk.c_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(log2n, batch, m):
+    """roofline.traffic: HBM bytes per launch from the committed PMC pass
+    (profiles/msm_pmc_latest.json, tools/pmc_summary.py), only when it was measured for this
+    launch shape AND this kernel source; otherwise None."""
+    path = os.path.join(ROOT, "profiles", "msm_pmc_latest.json")
+    try:
+        with open(path) as f:
+            j = json.load(f)
+    except (OSError, ValueError):
+        return None, "msm_dlog_kernel"
+    kname = j.get("kernel", "msm_dlog_kernel").split("(")[0].replace("void ", "")
+    ok = (j.get("log2n") == log2n and j.get("msm_batch") == batch and m == 1 << log2n and
+          j.get("source_sha16") == kernel_source_hash())
+    return (j.get("hbm_bytes_per_launch") if ok else None), kname
+
+
+def one_msm_log(torch, hip, pts, sc, n, dev, st):
+    """discrete log of one MSM over a full input (single GPU)"""
+    rec = torch.zeros(hip.MSM_RESULT_BYTES, dtype=torch.uint8, device=dev)
+    hip.msm_g1_dev(pts, sc, n, rec, st)
+    torch.cuda.synchronize()
+    return int(rec[hip.MSM_LOG_OFFSET:hip.MSM_LOG_OFFSET + 4].view(torch.int32).item())
+
+
+def single_msm_component(torch, hip, pts, sc, m, sets, dev):
+    """ONE m-point MSM per launch (the literal north-star case), launches back to back from a
+    HIP graph (host out of the loop), cold input sets; frac against the HBM spec peak."""
+    r1 = torch.zeros((64, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
+    gr = graph_avg_ms(torch, lambda i, s: hip.msm_g1_dev(pts[i % sets], sc[i % sets], m, r1[i % 64], s), 64)
+    if gr is None:
+        st = torch.cuda.current_stream()
+        gr = event_avg_ms(torch, st, lambda i: hip.msm_g1_dev(pts[i % sets], sc[i % sets], m, r1[i % 64], st), 64)
+    avg, med = gr
+    gbs = MSM_BYTES_PER_POINT * m / (avg * 1e-3) / 1e9
+    return {"device_us_per_msm": round(avg * 1e3, 2), "median_us": round(med * 1e3, 2),
+            "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "alg_bytes": MSM_BYTES_PER_POINT * m,
+            "note": "unbatched: one launch per MSM, 64 launches replayed back to back as a HIP graph (includes "
+                    "the dependent-launch boundary); rocprofv3 kernel duration in profiles/"}
+
+
+def cpu_other_baselines(hip):
+    """The reference's other hot paths on this host (oracle/_ref: the unmodified reference
+    headers, gcc -O2, one thread), bounded samples: schoolbook poly_mul (src/poly.h:106-122) at
+    2^14 x 2^14 and 2^15 x 2^15 with the O(la lb) extrapolation to config C3's 2^19 x 2^19, and the
+    toy prove of src/plonk-test.c (src/plonk.h:223) next to the same proof through the drop-in
+    build whose hot ops run in libplonkhip."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import gen
+    from pyoracle import Reference
+    if not Reference.available():
+        return {"note": "oracle/_ref absent on this host"}
+    R = Reference()
+    out = {}
+    for k in (14, 15):
+        a, b = gen.poly_inputs(0xC0DE + k, 1 << k, 1 << k)
+        t0 = time.perf_counter()
+        R.poly_mul(a, b)
+        dt = time.perf_counter() - t0
+        out["poly_mul_2^%dx2^%d" % (k, k)] = {"s": round(dt, 4), "GMAC_s": round((1 << 2 * k) / dt / 1e9, 3)}
+    rate = out["poly_mul_2^15x2^15"]["GMAC_s"] * 1e9
+    out["poly_mul_2^19x2^19_extrapolated_s"] = round((1 << 38) / rate, 1)
+    with open(os.path.join(ROOT, "tests", "golden", "prove.json")) as f:
+        p = json.load(f)["proofs"][0]
+    args = (p["gates"], p["copies"], p["wires"], p["chal"], p["rand"], p["secret"], p["srs_n"], p["srs_mode"])
+    reps = 2000
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        proof = R.prove4(*args)
+    ref_us = (time.perf_counter() - t0) / reps * 1e6
+    out["toy_prove_4_gates"] = {"reference_cpu_us": round(ref_us, 2), "matches_golden": proof.hex() == p["proof"]}
+    dropin = os.path.join(ROOT, "oracle", "_ref", "libplonkref_dropin.so")
+    if os.path.exists(dropin):
+        D = Reference(dropin)
+        D.prove4(*args)
+        t0 = time.perf_counter()
+        for _ in range(50):
+            dproof = D.prove4(*args)
+        out["toy_prove_4_gates"]["dropin_gpu_us"] = round((time.perf_counter() - t0) / 50 * 1e6, 1)
+        out["toy_prove_4_gates"]["dropin_matches_golden"] = dproof.hex() == p["proof"]
+    out["note"] = ("reference compiled from its own headers (oracle/_ref, gcc -O2), 1 thread; the toy prove is "
+                   "latency-bound on the GPU (about 26 host<->device round trips of tiny ops)")
+    return out
+
+
 def components(torch, hip, dev, st):
     out = {}
     # C2: 2^16-point MSM -- device-resident kernel time and host-buffer call (PCIe incl.)
@@ -168,18 +299,20 @@ def components(torch, hip, dev, st):
     eag, _ = event_avg_ms(torch, st, lambda i: hip.ntt_dev(bufs[i % 4], k, False, st), 50)
     gr = graph_avg_ms(torch, lambda i, s: hip.ntt_dev(bufs[i % 4], k, False, s), 50)
     avg, med = gr if gr else (eag, eag)
-    out["ntt_2^20_forward"] = {"ms": round(avg, 4), "eager_ms": round(eag, 4), "Gelem_s": round((1 << k) / (avg * 1e-3) / 1e9, 2),
-                               "passes": 2, "alg_bytes": 2 * 4 * (1 << k) * 2,
-                               "GB_s_alg": round(2 * 8 * (1 << k) / (avg * 1e-3) / 1e9, 1)}
+    alg = NTT_BYTES_PER_ELEM * (1 << k)
+    out["ntt_2^20_forward"] = {"ms": round(avg, 4), "eager_ms": round(eag, 4),
+                               "Gelem_s": round((1 << k) / (avg * 1e-3) / 1e9, 2), "passes": 2,
+                               "roofline": roofline_obj(alg, avg, "SURVEY 8(d): u32 read + write once per element")}
     # the same transform, 8 independent arrays sharing each pass's launch (plk_ntt_batch_dev)
     nb = 8
     bb_ = [torch.randint(0, 2013265921, (nb, 1 << k), dtype=torch.int64, device=dev).to(torch.int32)
            for _ in range(2)]
-    avg, med = event_avg_ms(torch, st, lambda i: hip.ntt_batch_dev(bb_[i % 2], k, nb, False, st), 20)
+    gr = graph_avg_ms(torch, lambda i, s: hip.ntt_batch_dev(bb_[i % 2], k, nb, False, s), 20)
+    avg, med = gr if gr else event_avg_ms(torch, st, lambda i: hip.ntt_batch_dev(bb_[i % 2], k, nb, False, st), 20)
     out["ntt_2^20_forward_batch8"] = {"ms_per_launch": round(avg, 4),
                                       "Gelem_s": round(nb * (1 << k) / (avg * 1e-3) / 1e9, 2),
-                                      "GB_s_alg": round(nb * 2 * 8 * (1 << k) / (avg * 1e-3) / 1e9, 1)}
-    # poly_mul 2^19 x 2^19 -> 2^20 - 1 coefficients (device-resident, 3 launches)
+                                      "roofline": roofline_obj(nb * alg, avg, "8 transforms per launch")}
+    # poly_mul 2^19 x 2^19 -> 2^20 - 1 coefficients (device-resident)
     la = lb = 1 << 19
     a = torch.randint(0, 17, (la,), dtype=torch.int16, device=dev).to(torch.uint8)
     b = torch.randint(0, 17, (lb,), dtype=torch.int16, device=dev).to(torch.uint8)
@@ -187,8 +320,11 @@ def components(torch, hip, dev, st):
     nz = torch.zeros(4, dtype=torch.int32, device=dev)
     work = torch.zeros(hip.poly_mul_workspace(la, lb), dtype=torch.uint8, device=dev)
     hip.poly_mul_dev(a, la, b, lb, o, nz, work, st)
-    avg, med = event_avg_ms(torch, st, lambda i: hip.poly_mul_dev(a, la, b, lb, o, nz, work, st), 30)
-    out["poly_mul_2^19x2^19"] = {"ms": round(avg, 4), "Gcoeff_s_out": round((la + lb - 1) / (avg * 1e-3) / 1e9, 2)}
+    gr = graph_avg_ms(torch, lambda i, s: hip.poly_mul_dev(a, la, b, lb, o, nz, work, s), 30)
+    avg, med = gr if gr else event_avg_ms(torch, st, lambda i: hip.poly_mul_dev(a, la, b, lb, o, nz, work, st), 30)
+    out["poly_mul_2^19x2^19"] = {"ms": round(avg, 4), "Gcoeff_s_out": round((la + lb - 1) / (avg * 1e-3) / 1e9, 2),
+                                 "roofline": roofline_obj(la + lb + (la + lb - 1), avg,
+                                                          "SURVEY 8(d): la + lb + (la + lb - 1) bytes of HF")}
     out["prove_2^20_gates"] = prove_component(torch, hip, dev, 20)
     return out
 
@@ -244,47 +380,64 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; PLK_DIST_BACKEND=gloo (and more ranks than GPUs) only to rehearse
+    # the multi-rank path on a one-GPU box -- the driver's runs use RCCL ("nccl")
+    backend = os.environ.get("PLK_DIST_BACKEND", "nccl")
+    gpu = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    hip.init(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+    dev = torch.device("cuda", gpu)
+    hip.init(gpu)
     st = torch.cuda.current_stream()
 
-    n = 1 << args.log2n
+    from plonkhip.dist import finish_sharded, g1_bytes, gpu_ops, shard_range
+
+    n = 1 << args.log2n                      # points per MSM
+    strong = world > 1 and not args.weak
+    lo, hi = shard_range(n, rank, world) if strong else (0, n)
+    m = hi - lo                              # points this rank reads per MSM
     B = max(1, args.msm_batch)
-    sets = max(2 * B, -(-args.rotate_mib * (1 << 20) // (MSM_BYTES_PER_POINT * n)))
-    sets = -(-sets // B) * B                       # whole launches never wrap the rotation
-    pts, sc = make_msm_sets(torch, n, sets, dev, 1234 + rank)
-    K, W = args.steps, args.warmup            # steps of B MSMs (one batched launch each)
+    sets = max(2 * B, -(-args.rotate_mib * (1 << 20) // (MSM_BYTES_PER_POINT * m)))
+    sets = -(-sets // B) * B                 # whole launches never wrap the rotation
+    # strong: every rank builds the SAME input sets and keeps its range; weak: rank r's sets are
+    # its own shards of N * 2^log2n-point MSMs
+    seed_of = (lambda s: 1234 + s) if strong or world == 1 else (lambda s, r=rank: 1234 + 100003 * r + s)
+    pts, sc = make_shard_sets(torch, n, lo, hi, sets, dev, seed_of)
+    ops = gpu_ops(hip, st)
+    K, W = args.steps, args.warmup          # steps of B MSMs (one batched launch each)
     res = torch.zeros(((W + K) * B, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
-    outs = torch.zeros((K * B, 4), dtype=torch.uint8, device=dev)
 
     def launch(first, count):
-        """MSMs first .. first+count-1 (one result record each), B per launch; MSM i reads
+        """MSMs first .. first+count-1 (result record i = res[i]), B per launch; MSM i reads
         input set i mod sets."""
         i = first
         while i < first + count:
             b = min(B, first + count - i, sets - i % sets)
             s0 = i % sets
-            hip.msm_g1_batch_dev(pts[s0], 3 * n, sc[s0], n, n, b, res[i], st)
+            ops.launch(pts[s0], 3 * m, sc[s0], m, m, b, res[i:])
             i += b
 
-    launch(0, W * B)
+    def shard_of(j):                         # MSM W*B + j of the timed region
+        s0 = (W * B + j) % sets
+        return pts[s0], sc[s0]
+
+    launch(0, max(W, 1) * B)                 # (records are re-armed by every launch)
+    # the finish path once on the warmup records: torch loads its elementwise kernels lazily
+    # (tens of ms on first use), which must not land in the timed region
+    finish_sharded(ops.records_to_partials(res[:max(W, 1) * B]), n, ops, lambda j: (pts[j % sets], sc[j % sets]))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     launch(W * B, K * B)
-    logs = res[W * B:].view(torch.int32)[:, hip.MSM_LOG_OFFSET // 4].contiguous()
-    if world > 1:
-        dist.all_reduce(logs, op=dist.ReduceOp.SUM)
-    hip.msm_finalize_dev(logs, K * B, 1, outs, st)
+    partials = ops.records_to_partials(res[W * B:])
+    g1t, folded = finish_sharded(partials, n, ops, shard_of)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -294,11 +447,41 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    irregular = int(res[:, hip.MSM_IRREGULAR_OFFSET:hip.MSM_IRREGULAR_OFFSET + 4].view(torch.int32).sum().item())
     if args.profile_only:
         if world > 1:
             dist.destroy_process_group()
         return
+
+    # ---- correctness of the timed results (outside the timed region)
+    g1s = g1_bytes(g1t[:1])
+    check = {}
+    first_set = W * B % sets
+    if rank == 0:
+        # the first timed MSM recomputed on this GPU alone from its full input (every shard)
+        if world == 1 or strong:
+            fp, fs = make_msm_set(torch, n, dev, seed_of(first_set))
+            full_logs = [one_msm_log(torch, hip, fp, fs, n, dev, st)]
+        else:
+            full_logs = []
+            for r in range(world):
+                fp, fs = make_msm_set(torch, n, dev, 1234 + 100003 * r + first_set)
+                full_logs.append(one_msm_log(torch, hip, fp, fs, n, dev, st))
+        want = g1_bytes(ops.exp(torch.tensor([sum(full_logs) % 102], dtype=torch.int32, device=dev)))[0]
+        check["first_msm_single_gpu_recompute"] = want == g1s[0]
+    if strong and args.log2n == 22:
+        # the reference's own answer for a 2^22-point input, through the same sharded path
+        sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+        import gen
+        with open(os.path.join(ROOT, "tests", "golden", "msm.json")) as f:
+            gold = json.load(f)["large"][7]
+        gp, gs = gen.msm_inputs(gold["seed"], gold["n"], gold["kind"])
+        sp = torch.from_numpy(gp[lo:hi].reshape(-1).copy()).to(dev)
+        ss = torch.from_numpy(gs[lo:hi].copy()).to(dev)
+        rec = torch.zeros((1, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
+        ops.launch(sp, 0, ss, 0, hi - lo, 1, rec)
+        got, _ = finish_sharded(ops.records_to_partials(rec), n, ops, lambda j: (sp, ss))
+        check["golden_2^22_reference"] = g1_bytes(got)[0].hex() == gold["out"]
+    irregular = int(partials[:, 1].sum().item())
 
     # Kernel-level timing for the roofline, on the stream the kernel runs on: one event pair
     # around L back-to-back launches of B MSMs (a pair around every launch would add its
@@ -312,7 +495,7 @@ def main():
     def one(j):
         s0 = (base + j * B) % sets
         s0 -= s0 % B
-        hip.msm_g1_batch_dev(pts[s0], 3 * n, sc[s0], n, n, B, res2[0], st)
+        ops.launch(pts[s0], 3 * m, sc[s0], m, m, B, res2)
 
     one(0)                       # device busy before the start event (see event_avg_ms)
     e0.record(st)
@@ -321,21 +504,12 @@ def main():
     e1.record(st)
     torch.cuda.synchronize()
     avg_ms = e0.elapsed_time(e1) / L
-    alg = MSM_BYTES_PER_POINT * n * B
+    alg = MSM_BYTES_PER_POINT * m * B
     achieved = alg / (avg_ms * 1e-3) / 1e9
-    traffic, kname = None, "msm_dlog_kernel"
-    pmc = os.path.join(ROOT, "profiles", "msm_pmc_latest.json")
-    if os.path.exists(pmc):
-        try:
-            with open(pmc) as f:
-                j = json.load(f)
-            if j.get("log2n") == args.log2n and j.get("msm_batch") == B:
-                traffic = j.get("hbm_bytes_per_launch")
-                kname = j.get("kernel", kname).split("(")[0].replace("void ", "")
-        except (OSError, ValueError):
-            traffic = None
+    traffic, kname = pmc_traffic(args.log2n, B, m)
 
-    value = world * n * B * K / elapsed / 1e6
+    total_points = (n if strong or world == 1 else world * n) * B * K
+    value = total_points / elapsed / 1e6
     line = {
         "metric": "G1-MSM Mpoint/s + NTT Gelem/s; end-to-end prove ms at 2^20 gates",
         "value": round(value, 1),
@@ -345,46 +519,48 @@ def main():
         "warmup": W,
         "ms_per_step": round(elapsed / K * 1e3, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: SRS points kG (k uniform 1..16), HF scalars uniform 0..16, %d distinct "
-                "input sets (%d MiB) rotated so every step reads cold data, resident in HBM"
-                % (sets, sets * MSM_BYTES_PER_POINT * n >> 20),
-        "config": {"workload": "%d x 2^%d-point G1 MSMs (srs_eval_at_s) per GPU per step: one batched "
-                               "launch over %d distinct input sets; point-range sharded over %d GPU(s), one "
-                               "RCCL all-reduce of the partial logs of all K steps" % (B, args.log2n, B, world),
-                   "points_per_gpu": n, "msms_per_step": B, "msms_per_launch": B, "parallelism": "dp%d" % world},
+                "input sets (%d MiB per GPU) rotated so every step reads cold data, resident in HBM"
+                % (sets, sets * MSM_BYTES_PER_POINT * m >> 20),
+        "config": {"workload": "%d x 2^%d-point G1 MSMs (srs_eval_at_s) per step, one batched launch per GPU over %d "
+                               "distinct input sets; %s; ONE RCCL all-reduce of the partial logs of all K steps "
+                               "(plonkhip.dist.finish_sharded)" % (
+                                   B, args.log2n, B,
+                                   "each MSM point-range sharded over %d GPU(s) (%d points per GPU)" % (world, m)
+                                   if strong or world == 1 else
+                                   "every GPU owns a 2^%d-point shard of %d-GPU MSMs" % (args.log2n, world)),
+                   "points_per_msm": n if strong or world == 1 else world * n, "points_per_gpu": m,
+                   "msms_per_step": B, "msms_per_launch": B, "parallelism": "dp%d" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": kname,
                      "launch_ms_avg": round(avg_ms, 5), "alg_bytes_per_launch": alg,
                      "timing": "hipEvent pair around %d back-to-back launches on the kernel's "
                                "stream, opened after one primer launch is queued" % L},
+        "checks": check,
         "irregular_inputs": irregular,
+        "serial_fold_fallbacks": folded,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         torch.cuda.synchronize()
-        gpu_g1 = bytes(res[0, hip.MSM_G1_OFFSET:hip.MSM_G1_OFFSET + 3].cpu().numpy())
-        line["cpu_baseline"] = cpu_baseline(pts[0].cpu().numpy(), sc[0].cpu().numpy(),
-                                            args.cpu_seconds, gpu_g1)
+        line["cpu_baseline"] = cpu_baseline(pts[first_set].cpu().numpy(), sc[first_set].cpu().numpy(),
+                                            args.cpu_seconds, g1s[0])
     if rank == 0 and not args.no_components:
         comp = components(torch, hip, dev, st)
-        r1 = torch.zeros((64, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
-        avg1, med1 = event_avg_ms(torch, st, lambda i: hip.msm_g1_dev(pts[i % sets], sc[i % sets], n,
-                                                                       r1[i % 64], st), 64)
-        comp["msm_2^%d_one_per_launch" % args.log2n] = {
-            "device_us_per_msm": round(avg1 * 1e3, 2), "median_us": round(med1 * 1e3, 2),
-            "GB_s": round(MSM_BYTES_PER_POINT * n / (avg1 * 1e-3) / 1e9, 1),
-            "note": "unbatched: one launch per MSM, back-to-back on one stream"}
+        comp["msm_2^%d_one_per_launch" % args.log2n] = single_msm_component(torch, hip, pts, sc, m, sets, dev)
         B8 = 8
         r8 = torch.zeros((B8, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
         avg8, med8 = event_avg_ms(torch, st, lambda i: hip.msm_g1_batch_dev(
-            pts[(i * B8) % sets], 3 * n, sc[(i * B8) % sets], n, n, B8, r8[0], st), 16)
+            pts[(i * B8) % sets], 3 * m, sc[(i * B8) % sets], m, m, B8, r8[0], st), 16)
         comp["msm_2^%d_8_per_launch" % args.log2n] = {
             "device_us_per_launch": round(avg8 * 1e3, 2),
-            "GB_s": round(MSM_BYTES_PER_POINT * n * B8 / (avg8 * 1e-3) / 1e9, 1),
+            "GB_s": round(MSM_BYTES_PER_POINT * m * B8 / (avg8 * 1e-3) / 1e9, 1),
             "note": "8 MSMs per launch (the prover's commitments are 9 per launch)"}
+        if world == 1 and not args.no_cpu_baseline:
+            comp["cpu_reference_other"] = cpu_other_baselines(hip)
         line["components"] = comp
     if world > 1 and not args.no_components:
         # C5 at N GPUs: replicas only (the prover's NTT work stays on one GPU) --

@@ -136,6 +136,51 @@ int plk_ntt_dev(uint32_t *d_data, int log_n, int inverse, void *stream);
  * share each pass's launch (the prover's products run the same way). */
 int plk_ntt_batch_dev(uint32_t *d_data, int log_n, int batch, int inverse, void *stream);
 
+/* ---- the ops around the hot path ---------------------------------
+ * Byte-exact restatements of the reference's host ops on the GPU, for every byte value
+ * (non-canonical HF bytes included: the kernels fall back to the reference's serial loop on the
+ * device where the parallel form would differ).  The drop-in headers call them. */
+
+/* Replaces poly_eval (src/poly.h:265-272): Horner at x, *y = the reference's HF byte. */
+int plk_poly_eval(const uint8_t *p, size_t len, uint8_t x, uint8_t *y);
+/* n evaluations in one launch (the prover's ~40 evaluations, src/plonk.h:345-347, 527-533,
+ * 567, 574; the grand-product loop src/plonk.h:326-359): ys[i] = poly_eval(polys[i], xs[i]). */
+int plk_poly_eval_batch(const uint8_t *const *polys, const size_t *lens, const uint8_t *xs, int n,
+                        uint8_t *ys);
+/* device form: d_polys = host array of n device pointers; d_tick = plk_poly_eval_workspace(n)
+ * bytes of device memory, zeroed once (every launch leaves it zeroed again). */
+size_t plk_poly_eval_workspace(int n);
+int plk_poly_eval_batch_dev(const uint8_t *const *d_polys, const size_t *lens, const uint8_t *xs, int n,
+                            uint8_t *d_ys, void *d_tick, void *stream);
+
+/* Replaces poly_divide (src/poly.h:124-177): num = quot * den + rem.
+ *   quot: max(nl - dl + 1, 1) bytes, rem: min(dl - 1, nl) bytes (may be NULL when that is 0);
+ *   *quot_len / *rem_len = lengths after the reference's trim (rem_len 0 when dl == 1).
+ * Divisors x^m * lead + d0 (Z_H = x^n - 1, x - z, constants) run as parallel chain scans; any
+ * other divisor, and non-canonical numerator bytes, run the reference's loop on the device.
+ * A zero divisor is PLK_ERR_ARG ("Division by zero polynomial in poly_divide"); a divisor lead
+ * byte >= 17 is PLK_ERR_RANGE (the reference reads hf_inverses out of bounds). */
+int plk_poly_divide(const uint8_t *num, size_t nl, const uint8_t *den, size_t dl, uint8_t *quot, size_t *quot_len,
+                    uint8_t *rem, size_t *rem_len);
+/* device form: den stays a HOST array (classified on the host, copied into d_work when the
+ * serial loop needs it); d_lens[0..1] receive the index + 1 of the last non-zero quotient /
+ * remainder byte (0: all zero) over the untrimmed lengths above; d_work:
+ * plk_poly_divide_workspace(nl, dl) bytes. */
+size_t plk_poly_divide_workspace(size_t nl, size_t dl);
+int plk_poly_divide_dev(const uint8_t *d_num, size_t nl, const uint8_t *den, size_t dl, uint8_t *d_quot,
+                        uint8_t *d_rem, uint32_t *d_lens, void *d_work, void *stream);
+
+/* Replaces matrix_mul (src/matrix.h:79-96): out[m x n] = a[m x k] b[k x n], row-major bytes,
+ * sums by hf_add of hf_mul products. */
+int plk_matrix_mul(const uint8_t *a, size_t m, size_t k, const uint8_t *b, size_t n, uint8_t *out);
+/* Replaces matrix_inv (src/matrix.h:149-176, Gauss-Jordan src/matrix.h:100-147) as plonk_new
+ * uses it for the Vandermonde inverse h_pows_inv (src/plonk.h:105-113): the same pivoting, so
+ * the same bytes for singular matrices too.  Entries must be GF(17) values (< 17). */
+int plk_matrix_inv(const uint8_t *mat, size_t n, uint8_t *out);
+/* interpolate_at_h (src/plonk.h:162-195): out = h_pows_inv (n x n) * values, trimmed as
+ * poly_new; out holds n bytes. */
+int plk_interpolate(const uint8_t *h_pows_inv, const uint8_t *values, size_t n, uint8_t *out, size_t *out_len);
+
 /* ---- device-resident prover (replaces plonk_new / plonk_prove / plonk_free,
  * src/plonk.h:53-139, 223-656, 120-139) ---------------------------------------------------
  * plk_prover_create uploads the SRS and Z_H once (the PLONK struct of plonk_new); the

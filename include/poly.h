@@ -2,8 +2,9 @@
  * Same guard, POLY layout, names and semantics (constructor trims trailing zeros, results
  * are freshly malloc'ed and freed with poly_free).  poly_mul -- the prover's hot
  * polynomial operation (17 calls per proof) -- runs on the GPU through plk_poly_mul
- * (exact BabyBear NTT / direct convolution, include/plonkhip.h).  The other operations are
- * O(n) or O(n * small) host code, restated from scratch. */
+ * (exact NTT / direct convolution, include/plonkhip.h), and so do poly_divide and poly_eval
+ * (plk_poly_divide, plk_poly_eval).  The other operations are O(n)
+ * coefficient copies and scalings, host code restated from scratch. */
 #ifndef POLY_H
 #define POLY_H
 
@@ -86,7 +87,9 @@ static inline POLY poly_mul(const POLY *a, const POLY *b) {
   return r;
 }
 
-/* long division num = quot * den + rem (src/poly.h:124-177) */
+/* long division num = quot * den + rem (src/poly.h:124-177) on the GPU (plk_poly_divide:
+ * parallel chain scans for x^m-type divisors such as Z_H and x - z, the reference's loop on the
+ * device otherwise) */
 static inline void poly_divide(const POLY *num, const POLY *den, POLY *quot, POLY *rem) {
   if (poly_is_zero(den)) {
     fprintf(stderr, "Division by zero polynomial in poly_divide\n");
@@ -95,19 +98,17 @@ static inline void poly_divide(const POLY *num, const POLY *den, POLY *quot, POL
   size_t nl = num->len, dl = den->len;
   HF *q = (HF *)poly_xalloc_(nl, "poly_divide");
   HF *r = (HF *)poly_xalloc_(nl, "poly_divide");
-  memcpy(r, num->coeffs, nl);
-  HF lead_inv = hf_inv(den->coeffs[dl - 1]);
-  for (ssize_t i = (ssize_t)nl - 1; i >= (ssize_t)(dl - 1); i--) {
-    HF c = hf_mul(r[i], lead_inv);
-    q[i - (dl - 1)] = c;
-    for (ssize_t j = 0; j < (ssize_t)dl; j++) r[i - j] = hf_sub(r[i - j], hf_mul(c, den->coeffs[dl - 1 - j]));
+  size_t ql = 0, rl = 0;
+  int rc = plk_poly_divide((const uint8_t *)num->coeffs, nl, (const uint8_t *)den->coeffs, dl, (uint8_t *)q, &ql,
+                           (uint8_t *)r, &rl);
+  if (rc != PLK_OK) {
+    fprintf(stderr, "poly_divide failed on the GPU (libplonkhip error %d): %s\n", rc, plk_last_error());
+    exit(EXIT_FAILURE);
   }
-  size_t ql = nl >= dl ? nl - dl + 1 : 1;
-  size_t rl = dl - 1 > nl ? nl : dl - 1;
-  *quot = poly_new(q, ql);
-  *rem = poly_new(r, rl);
-  free(q);
-  free(r);
+  quot->coeffs = q;   /* already trimmed to ql / rl; the tails of the buffers are unused */
+  quot->len = ql;
+  rem->coeffs = r;
+  rem->len = rl;
 }
 
 static inline POLY poly_scale(const POLY *p, HF s) {
@@ -150,10 +151,14 @@ static inline void poly_free(POLY *p) {
   p->len = 0;
 }
 
-/* Horner */
+/* Horner (src/poly.h:265-272) on the GPU (plk_poly_eval: exact for every byte value) */
 static inline HF poly_eval(const POLY *p, HF x) {
-  HF y = hf_zero();
-  for (size_t i = p->len; i-- > 0;) y = hf_add(hf_mul(y, x), p->coeffs[i]);
+  HF y = {0};
+  int rc = plk_poly_eval((const uint8_t *)p->coeffs, p->len, x.value, &y.value);
+  if (rc != PLK_OK) {
+    fprintf(stderr, "poly_eval failed on the GPU (libplonkhip error %d): %s\n", rc, plk_last_error());
+    exit(EXIT_FAILURE);
+  }
   return y;
 }
 

@@ -322,6 +322,55 @@ uint8_t orc_poly_eval(const uint8_t *p, size_t len, uint8_t x) {
   return y;
 }
 
+/* matrix_mul (src/matrix.h:79-96): row-major bytes, sum = hf_add(sum, hf_mul(a, b)) */
+static uint8_t h_add(uint8_t a, uint8_t b) { uint8_t s = (uint8_t)(a + b); if (s >= P_HF) s -= P_HF; return s; }
+
+void orc_matrix_mul(const uint8_t *a, size_t m, size_t k, const uint8_t *b, size_t n, uint8_t *out) {
+  for (size_t i = 0; i < m; i++)
+    for (size_t j = 0; j < n; j++) {
+      uint8_t s = 0;
+      for (size_t t = 0; t < k; t++) s = h_add(s, h_mul(a[i * k + t], b[t * n + j]));
+      out[i * n + j] = s;
+    }
+}
+
+/* matrix_inv (src/matrix.h:149-176): Gauss-Jordan on [M | I] (src/matrix.h:100-147) --
+ * the first non-zero pivot at or below row r in column `lead` (moving right when a column is
+ * all zero), row swap, normalisation by hf_div, elimination of every other row. */
+void orc_matrix_inv(const uint8_t *a, size_t n, uint8_t *out) {
+  const size_t c = 2 * n;
+  uint8_t *g = calloc(n * c + 1, 1);
+  for (size_t i = 0; i < n; i++) {
+    memcpy(g + i * c, a + i * n, n);
+    g[i * c + n + i] = 1;
+  }
+  size_t lead = 0;
+  for (size_t r = 0; r < n; r++) {
+    if (c <= lead) break;
+    size_t i = r;
+    int stop = 0;
+    while (g[i * c + lead] == 0) {
+      if (++i == n) {
+        i = r;
+        if (++lead == c) { stop = 1; break; }
+      }
+    }
+    if (stop) break;
+    if (i != r)
+      for (size_t k = 0; k < c; k++) { uint8_t t = g[i * c + k]; g[i * c + k] = g[r * c + k]; g[r * c + k] = t; }
+    const uint8_t div = g[r * c + lead];
+    if (div) for (size_t k = 0; k < c; k++) g[r * c + k] = h_mul(g[r * c + k], hf_inv_tab[div % P_HF]);
+    for (size_t ii = 0; ii < n; ii++) {
+      if (ii == r) continue;
+      const uint8_t mult = g[ii * c + lead];
+      for (size_t k = 0; k < c; k++) g[ii * c + k] = h_sub(g[ii * c + k], h_mul(g[r * c + k], mult));
+    }
+    lead++;
+  }
+  for (size_t i = 0; i < n; i++) memcpy(out + i * n, g + i * c + n, n);
+  free(g);
+}
+
 /* ---------------- seeded generators shared with SURVEY.md §8c ---------------- */
 static uint64_t xs_next(uint64_t *s) {
   uint64_t x = *s;

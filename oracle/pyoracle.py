@@ -40,6 +40,8 @@ class _Lib:
             ("msm" if prefix == "ref_" else "msm_fold", None, [_u8p, _u8p, C.c_size_t, _u8p]),
             ("poly_mul", C.c_size_t, [_u8p, C.c_size_t, _u8p, C.c_size_t, _u8p]),
             ("poly_eval", C.c_uint8, [_u8p, C.c_size_t, C.c_uint8]),
+            ("matrix_mul", None, [_u8p, C.c_size_t, C.c_size_t, _u8p, C.c_size_t, _u8p]),
+            ("matrix_inv", None, [_u8p, C.c_size_t, _u8p]),
         ]:
             f = getattr(L, prefix + name)
             f.restype = res
@@ -47,6 +49,18 @@ class _Lib:
 
     def fn(self, name):
         return getattr(self.lib, self.p + name)
+
+    def matrix_mul(self, a, m, k, b, n):
+        a, b = _u8(a), _u8(b)
+        out = np.zeros(max(m * n, 1), np.uint8)
+        self.fn("matrix_mul")(_ptr(a), m, k, _ptr(b), n, _ptr(out))
+        return bytes(out[:m * n])
+
+    def matrix_inv(self, a, n):
+        a = _u8(a)
+        out = np.zeros(max(n * n, 1), np.uint8)
+        self.fn("matrix_inv")(_ptr(a), n, _ptr(out))
+        return bytes(out[:n * n])
 
     def g1_add(self, a, b):
         out = np.zeros(3, np.uint8)

@@ -15,6 +15,8 @@
  *   ref_poly_mul      -> poly_mul                                       src/poly.h:106-122
  *   ref_poly_divide   -> poly_divide                                    src/poly.h:124-177
  *   ref_poly_eval     -> poly_eval                                      src/poly.h:265-272
+ *   ref_matrix_mul    -> matrix_mul                                     src/matrix.h:79-96
+ *   ref_matrix_inv    -> matrix_inv (Gauss-Jordan)                      src/matrix.h:100-176
  *   ref_interpolate4  -> plonk_new + interpolate_at_h                   src/plonk.h:53,162
  *   ref_prove4        -> srs_create + plonk_new + plonk_prove           src/srs.h:18, src/plonk.h:53,223
  *   ref_plonk4_data   -> srs_create + plonk_new: h, k1_h, k2_h, h_pows_inv, z_h_x, g1s
@@ -93,6 +95,23 @@ uint8_t ref_poly_eval(const uint8_t *p, size_t len, uint8_t x) {
   POLY P = {(HF *)p, len};
   HF X = {x};
   return poly_eval(&P, X).value;
+}
+
+void ref_matrix_mul(const uint8_t *a, size_t m, size_t k, const uint8_t *b, size_t n, uint8_t *out) {
+  MATRIX A = matrix_new((HF *)a, m, k), B = matrix_new((HF *)b, k, n);
+  MATRIX R = matrix_mul(&A, &B);
+  memcpy(out, R.v, m * n);
+  matrix_free(&A);
+  matrix_free(&B);
+  matrix_free(&R);
+}
+
+void ref_matrix_inv(const uint8_t *a, size_t n, uint8_t *out) {
+  MATRIX A = matrix_new((HF *)a, n, n);
+  MATRIX R = matrix_inv(&A);
+  memcpy(out, R.v, n * n);
+  matrix_free(&A);
+  matrix_free(&R);
 }
 
 /* interpolate_at_h over the reference's 4-element H (plonk-test.c setup: secret 2, n 6). */

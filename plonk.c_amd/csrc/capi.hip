@@ -16,17 +16,29 @@ namespace {
 thread_local char g_err[512] = "";
 
 struct Ctx {
-  std::mutex mu;
+  std::mutex mu;            // guards everything below; never destroyed (plk_shutdown resets fields)
   bool ready = false;
   int device = -1;
+  int live_provers = 0;     // plk_prover_t objects alive: they use the NTT tables
   hipStream_t st = nullptr;
   uint8_t gen[3] = {0, 0, 0};
-  // MSM staging
+  // MSM staging (host-buffer plk_msm_g1)
   uint8_t* d_pts = nullptr;
   size_t cap_pts = 0;
   uint8_t* d_sc = nullptr;
   size_t cap_sc = 0;
   PlkMsmResult* d_res = nullptr;
+  // SRS upload cache (layer 4): the device copy of the last point array, keyed by the
+  // caller's pointer; reused when the first 3n bytes still equal the host mirror (memcmp: exact,
+  // no hash collisions).  srs_eval_at_s passes the same srs->g1s on every commitment of a proof
+  // (src/plonk.h:299-301, 379, 522-524, 620-621) with vs->len <= srs->len points.
+  const uint8_t* srs_key = nullptr;
+  size_t srs_cached = 0;    // bytes valid in d_pts / h_srs
+  uint8_t* h_srs = nullptr; // host mirror of the cached bytes
+  size_t cap_h_srs = 0;
+  // pinned staging for host -> device copies
+  uint8_t* h_stage = nullptr;
+  size_t cap_stage = 0;
   // poly_mul staging
   uint8_t* d_a = nullptr;
   size_t cap_a = 0;
@@ -37,6 +49,9 @@ struct Ctx {
   uint32_t* d_nz = nullptr;
   void* d_work = nullptr;
   size_t cap_work = 0;
+  // small-op staging (poly_divide / poly_eval / interpolate): one device arena
+  uint8_t* d_ops = nullptr;
+  size_t cap_ops = 0;
 } g;
 
 // ---- E(F101) tables, built from the group law on canonical points ----------------------
@@ -136,16 +151,71 @@ int grow(T** p, size_t* cap, size_t need) {
   return PLK_OK;
 }
 
+int grow_host(uint8_t** p, size_t* cap, size_t need, bool pinned) {
+  if (*cap >= need && *p) return PLK_OK;
+  size_t n = *cap ? *cap : 4096;
+  while (n < need) n *= 2;
+  if (*p) {
+    if (pinned) (void)hipHostFree(*p);
+    else free(*p);
+  }
+  *p = nullptr;
+  *cap = 0;
+  if (pinned) {
+    if (hipHostMalloc((void**)p, n, hipHostMallocDefault) != hipSuccess) *p = nullptr;
+  } else {
+    *p = (uint8_t*)malloc(n);
+  }
+  if (!*p) {
+    plk_set_error("host allocation of %zu bytes failed", n);
+    return PLK_ERR_NOMEM;
+  }
+  *cap = n;
+  return PLK_OK;
+}
+
+// Host -> device through the pinned staging buffer in chunks (the caller's pageable memory is
+// copied into pinned memory while the previous chunk's DMA runs).  Synchronous on g.st.
+int upload(uint8_t* dst, const uint8_t* src, size_t bytes) {
+  constexpr size_t CHUNK = 4u << 20;
+  if (!bytes) return PLK_OK;
+  int rc = grow_host(&g.h_stage, &g.cap_stage, 2 * CHUNK, true);
+  if (rc) return rc;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  PLK_HIP(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
+  PLK_HIP(hipEventCreateWithFlags(&done[1], hipEventDisableTiming));
+  for (size_t off = 0, k = 0; off < bytes; off += CHUNK, k ^= 1) {
+    const size_t len = bytes - off < CHUNK ? bytes - off : CHUNK;
+    uint8_t* h = g.h_stage + k * CHUNK;
+    if (off >= 2 * CHUNK) PLK_HIP(hipEventSynchronize(done[k]));   // this half's previous DMA
+    memcpy(h, src + off, len);
+    PLK_HIP(hipMemcpyAsync(dst + off, h, len, hipMemcpyHostToDevice, g.st));
+    PLK_HIP(hipEventRecord(done[k], g.st));
+  }
+  PLK_HIP(hipStreamSynchronize(g.st));
+  (void)hipEventDestroy(done[0]);
+  (void)hipEventDestroy(done[1]);
+  return PLK_OK;
+}
+
 int init_locked(int device) {
-  if (g.ready) return PLK_OK;
+  if (g.ready) {
+    if (device >= 0 && device != g.device) {
+      plk_set_error("libplonkhip is initialised on device %d; plk_init(%d) refused (plk_shutdown first)",
+                    g.device, device);
+      return PLK_ERR_ARG;
+    }
+    return PLK_OK;
+  }
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
     plk_set_error("no HIP device available (libplonkhip has no CPU fallback)");
     return PLK_ERR_NODEV;
   }
-  if (device < 0) {
+  if (device < 0) {   // implicit: $PLK_DEVICE, else the calling thread's current device
     const char* e = getenv("PLK_DEVICE");
-    device = e ? atoi(e) : 0;
+    if (e) device = atoi(e);
+    else if (hipGetDevice(&device) != hipSuccess) device = 0;
   }
   if (device >= count) {
     plk_set_error("device %d out of range (%d devices)", device, count);
@@ -164,10 +234,42 @@ int init_locked(int device) {
   return PLK_OK;
 }
 
-int ensure(void) {
-  if (g.ready) return hipSetDevice(g.device) == hipSuccess ? PLK_OK : PLK_ERR_HIP;
-  return init_locked(-1);
+// Host-buffer entry points hold g.mu for the whole call and run on g.device (set for the
+// call's thread).  Device entry points take the lock only to initialise, and then require
+// the calling thread's current device to be the library's: their stream and buffers belong to
+// that device, and the tables (dlog, NTT twiddles) exist only there.
+int ensure_locked(void) {
+  int rc = init_locked(-1);
+  if (rc) return rc;
+  return hipSetDevice(g.device) == hipSuccess ? PLK_OK : PLK_ERR_HIP;
 }
+
+int ensure_dev(void) {
+  int dev = -1;
+  {
+    std::lock_guard<std::mutex> lk(g.mu);
+    int rc = init_locked(-1);
+    if (rc) return rc;
+    dev = g.device;
+  }
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess) return PLK_ERR_HIP;
+  if (cur != dev) {
+    plk_set_error("libplonkhip runs on device %d but the calling thread's current device is %d", dev, cur);
+    return PLK_ERR_ARG;
+  }
+  return PLK_OK;
+}
+
+// Bump-carves the small-op device arena (poly_eval / poly_divide / matrix host calls).
+struct Arena {
+  size_t off = 0;
+  size_t take(size_t b) {
+    const size_t o = off;
+    off += (b + 255) & ~(size_t)255;
+    return o;
+  }
+};
 
 // Device entry points run on exactly the stream they are given; NULL is HIP's null stream
 // (torch's default stream also has handle 0).  g.st is used only by the host-buffer calls.
@@ -180,6 +282,20 @@ void plk_set_error(const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof g_err, fmt, ap);
   va_end(ap);
+}
+
+// device provers (prove.hip) hold the context: plk_shutdown keeps the tables while any is alive
+int plk_ctx_retain(void) {
+  int rc = ensure_dev();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g.mu);
+  g.live_provers++;
+  return PLK_OK;
+}
+
+void plk_ctx_release(void) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (g.live_provers > 0) g.live_provers--;
 }
 
 extern "C" {
@@ -201,20 +317,39 @@ int plk_init(int device) {
 void plk_shutdown(void) {
   std::lock_guard<std::mutex> lk(g.mu);
   if (!g.ready) return;
+  if (g.live_provers > 0) {   // their kernels read the NTT tables: keep everything
+    plk_set_error("plk_shutdown: %d prover(s) still alive; nothing released", g.live_provers);
+    return;
+  }
+  (void)hipSetDevice(g.device);
   (void)hipStreamSynchronize(g.st);
   (void)hipFree(g.d_pts); (void)hipFree(g.d_sc); (void)hipFree(g.d_res);
   (void)hipFree(g.d_a); (void)hipFree(g.d_b); (void)hipFree(g.d_out); (void)hipFree(g.d_nz); (void)hipFree(g.d_work);
+  (void)hipFree(g.d_ops);
+  if (g.h_stage) (void)hipHostFree(g.h_stage);
+  free(g.h_srs);
   plk_ntt_free_tables();
   (void)hipStreamDestroy(g.st);
-  const int dev = g.device;
-  g.~Ctx();
-  new (&g) Ctx();
-  (void)dev;
+  // reset field by field: the mutex (held here) stays as it is
+  g.ready = false;
+  g.device = -1;
+  g.st = nullptr;
+  g.d_pts = g.d_sc = g.d_a = g.d_b = g.d_out = g.d_ops = nullptr;
+  g.cap_pts = g.cap_sc = g.cap_a = g.cap_b = g.cap_out = g.cap_work = g.cap_ops = 0;
+  g.d_res = nullptr;
+  g.d_nz = nullptr;
+  g.d_work = nullptr;
+  g.srs_key = nullptr;
+  g.srs_cached = 0;
+  g.h_srs = nullptr;
+  g.cap_h_srs = 0;
+  g.h_stage = nullptr;
+  g.cap_stage = 0;
 }
 
 int plk_dlog_generator(uint8_t out[3]) {
   std::lock_guard<std::mutex> lk(g.mu);
-  int rc = ensure();
+  int rc = ensure_locked();
   if (rc) return rc;
   memcpy(out, g.gen, 3);
   return PLK_OK;
@@ -224,13 +359,26 @@ int plk_msm_g1(const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t 
   if ((!points || !scalars) && n) { plk_set_error("plk_msm_g1: NULL input"); return PLK_ERR_ARG; }
   if (!out) { plk_set_error("plk_msm_g1: NULL out"); return PLK_ERR_ARG; }
   std::lock_guard<std::mutex> lk(g.mu);
-  int rc = ensure();
+  int rc = ensure_locked();
   if (rc) return rc;
-  if ((rc = grow(&g.d_pts, &g.cap_pts, 3 * n + 16)) || (rc = grow(&g.d_sc, &g.cap_sc, n + 16))) return rc;
-  if (n) {
-    PLK_HIP(hipMemcpyAsync(g.d_pts, points, 3 * n, hipMemcpyHostToDevice, g.st));
-    PLK_HIP(hipMemcpyAsync(g.d_sc, scalars, n, hipMemcpyHostToDevice, g.st));
+  if ((rc = grow(&g.d_sc, &g.cap_sc, n + 16))) return rc;
+  const size_t pb = 3 * n;
+  const bool hit = n && points == g.srs_key && pb <= g.srs_cached && memcmp(points, g.h_srs, pb) == 0;
+  if (!hit && n) {
+    // keep the device copy of the longer of (cached, new) when the new bytes extend it
+    if (pb > g.cap_pts) {
+      g.srs_key = nullptr;
+      g.srs_cached = 0;
+      if ((rc = grow(&g.d_pts, &g.cap_pts, pb + 16))) return rc;
+    }
+    if ((rc = grow_host(&g.h_srs, &g.cap_h_srs, pb + 16, false))) return rc;
+    g.srs_key = nullptr;   // invalid until the upload completed
+    if ((rc = upload(g.d_pts, points, pb))) return rc;
+    memcpy(g.h_srs, points, pb);
+    g.srs_key = points;
+    g.srs_cached = pb;
   }
+  if ((rc = upload(g.d_sc, scalars, n))) return rc;
   if ((rc = plk_msm_launch(g.d_pts, g.d_sc, n, g.d_res, g.st))) return rc;
   PlkMsmResult h;
   PLK_HIP(hipMemcpyAsync(&h, g.d_res, sizeof h, hipMemcpyDeviceToHost, g.st));
@@ -256,7 +404,7 @@ int plk_poly_mul(const uint8_t* a, size_t la, const uint8_t* b, size_t lb, uint8
   }
   if (!a || !b || !out) { plk_set_error("plk_poly_mul: NULL buffer"); return PLK_ERR_ARG; }
   std::lock_guard<std::mutex> lk(g.mu);
-  int rc = ensure();
+  int rc = ensure_locked();
   if (rc) return rc;
   const size_t rl = la + lb - 1;
   const size_t ws = plk_poly_mul_workspace_bytes(la, lb);
@@ -264,8 +412,7 @@ int plk_poly_mul(const uint8_t* a, size_t la, const uint8_t* b, size_t lb, uint8
       (rc = grow(&g.d_out, &g.cap_out, rl + 16)))
     return rc;
   if (ws && (rc = grow((uint8_t**)&g.d_work, &g.cap_work, ws))) return rc;
-  PLK_HIP(hipMemcpyAsync(g.d_a, a, la, hipMemcpyHostToDevice, g.st));
-  PLK_HIP(hipMemcpyAsync(g.d_b, b, lb, hipMemcpyHostToDevice, g.st));
+  if ((rc = upload(g.d_a, a, la)) || (rc = upload(g.d_b, b, lb))) return rc;
   if ((rc = plk_poly_mul_launch(g.d_a, la, g.d_b, lb, g.d_out, g.d_nz, g.d_work, g.st))) return rc;
   uint32_t nz = 0;
   PLK_HIP(hipMemcpyAsync(out, g.d_out, rl, hipMemcpyDeviceToHost, g.st));
@@ -277,8 +424,7 @@ int plk_poly_mul(const uint8_t* a, size_t la, const uint8_t* b, size_t lb, uint8
 
 // ---- device-resident ------------------------------------------------------------------
 int plk_msm_result_init(plk_msm_result_t* d_res, void* stream) {
-  std::lock_guard<std::mutex> lk(g.mu);
-  int rc = ensure();
+  int rc = ensure_dev();
   if (rc) return rc;
   PLK_HIP(hipMemsetAsync(d_res, 0, sizeof(plk_msm_result_t), pick(stream)));
   return PLK_OK;
@@ -286,33 +432,33 @@ int plk_msm_result_init(plk_msm_result_t* d_res, void* stream) {
 
 int plk_msm_g1_dev(const uint8_t* d_points, const uint8_t* d_scalars, size_t n, plk_msm_result_t* d_res,
                    void* stream) {
-  int rc = ensure();
+  int rc = ensure_dev();
   if (rc) return rc;
   return plk_msm_launch(d_points, d_scalars, n, d_res, pick(stream));
 }
 
 int plk_msm_g1_batch_dev(const uint8_t* d_points, size_t points_stride, const uint8_t* d_scalars,
                          size_t scalars_stride, size_t n, int batch, plk_msm_result_t* d_res, void* stream) {
-  int rc = ensure();
+  int rc = ensure_dev();
   if (rc) return rc;
   return plk_msm_batch_launch(d_points, points_stride, d_scalars, scalars_stride, n, batch, d_res, pick(stream));
 }
 
 int plk_msm_g1_serial_dev(const uint8_t* d_points, const uint8_t* d_scalars, size_t n, plk_msm_result_t* d_res,
                           void* stream) {
-  int rc = ensure();
+  int rc = ensure_dev();
   if (rc) return rc;
   return plk_msm_serial_launch(d_points, d_scalars, n, d_res, pick(stream));
 }
 
 int plk_msm_combine_dev(const uint32_t* d_logs, int count, uint8_t* d_out3, void* stream) {
-  int rc = ensure();
+  int rc = ensure_dev();
   if (rc) return rc;
   return plk_msm_combine_launch(d_logs, count, d_out3, pick(stream));
 }
 
 int plk_msm_finalize_dev(const uint32_t* d_logs, int batch, int stride, uint8_t* d_out4, void* stream) {
-  int rc = ensure();
+  int rc = ensure_dev();
   if (rc) return rc;
   return plk_msm_finalize_launch(d_logs, batch, stride, d_out4, pick(stream));
 }
@@ -321,7 +467,7 @@ size_t plk_poly_mul_workspace(size_t la, size_t lb) { return plk_poly_mul_worksp
 
 int plk_poly_mul_dev(const uint8_t* d_a, size_t la, const uint8_t* d_b, size_t lb, uint8_t* d_out,
                      uint32_t* d_out_nz, void* d_work, void* stream) {
-  int rc = ensure();
+  int rc = ensure_dev();
   if (rc) return rc;
   return plk_poly_mul_launch(d_a, la, d_b, lb, d_out, d_out_nz, d_work, pick(stream));
 }
@@ -342,7 +488,7 @@ size_t plk_poly_mul_batch_workspace(const plk_polymul_job_t* jobs, int n) {
 }
 
 int plk_poly_mul_batch_dev(const plk_polymul_job_t* jobs, int n, void* d_work, size_t work_bytes, void* stream) {
-  int rc = ensure();
+  int rc = ensure_dev();
   if (rc) return rc;
   if (!jobs || n < 1 || n > 64) {
     plk_set_error("plk_poly_mul_batch_dev: %d jobs (1..64)", n);
@@ -360,19 +506,203 @@ int plk_poly_mul_batch_dev(const plk_polymul_job_t* jobs, int n, void* d_work, s
 }
 
 int plk_ntt_dev(uint32_t* d_data, int log_n, int inverse, void* stream) {
-  int rc = ensure();
+  int rc = ensure_dev();
   if (rc) return rc;
   return plk_ntt_launch(d_data, log_n, 1, inverse, pick(stream));
 }
 
 int plk_ntt_batch_dev(uint32_t* d_data, int log_n, int batch, int inverse, void* stream) {
-  int rc = ensure();
+  int rc = ensure_dev();
   if (rc) return rc;
   if (!d_data || batch < 1) {
     plk_set_error("plk_ntt_batch_dev: null data or batch %d", batch);
     return PLK_ERR_ARG;
   }
   return plk_ntt_launch(d_data, log_n, batch, inverse, pick(stream));
+}
+
+// ---- the ops around the hot path -----------------------------------------
+size_t plk_poly_eval_workspace(int n) { return (size_t)128 * (n > 0 ? n : 1); }
+
+int plk_poly_eval_batch_dev(const uint8_t* const* d_polys, const size_t* lens, const uint8_t* xs, int n,
+                            uint8_t* d_ys, void* d_tick, void* stream) {
+  int rc = ensure_dev();
+  if (rc) return rc;
+  if (!d_polys || !lens || !xs || !d_ys || !d_tick || n < 1) {
+    plk_set_error("plk_poly_eval_batch_dev: NULL argument or n = %d", n);
+    return PLK_ERR_ARG;
+  }
+  for (int b = 0; b < n; b += PLK_EVAL_MAX_JOBS) {
+    const int m = n - b < PLK_EVAL_MAX_JOBS ? n - b : PLK_EVAL_MAX_JOBS;
+    uint64_t l64[PLK_EVAL_MAX_JOBS];
+    for (int i = 0; i < m; i++) l64[i] = lens[b + i];
+    if ((rc = plk_poly_eval_batch_launch(d_polys + b, l64, xs + b, m, d_ys + b,
+                                         (uint8_t*)d_tick + (size_t)128 * b, pick(stream))))
+      return rc;
+  }
+  return PLK_OK;
+}
+
+int plk_poly_eval_batch(const uint8_t* const* polys, const size_t* lens, const uint8_t* xs, int n, uint8_t* ys) {
+  if (!polys || !lens || !xs || !ys || n < 1) {
+    plk_set_error("plk_poly_eval_batch: NULL argument or n = %d", n);
+    return PLK_ERR_ARG;
+  }
+  std::lock_guard<std::mutex> lk(g.mu);
+  int rc = ensure_locked();
+  if (rc) return rc;
+  Arena A;
+  std::vector<size_t> off(n);
+  for (int i = 0; i < n; i++) off[i] = A.take(lens[i] + 16);
+  const size_t o_y = A.take(n), o_tick = A.take(plk_poly_eval_workspace(n));
+  if ((rc = grow(&g.d_ops, &g.cap_ops, A.off))) return rc;
+  std::vector<const uint8_t*> dp(n);
+  for (int i = 0; i < n; i++) {
+    if (lens[i] && !polys[i]) {
+      plk_set_error("plk_poly_eval_batch: NULL polynomial %d", i);
+      return PLK_ERR_ARG;
+    }
+    if (lens[i] && (rc = upload(g.d_ops + off[i], polys[i], lens[i]))) return rc;
+    dp[i] = g.d_ops + off[i];
+  }
+  PLK_HIP(hipMemsetAsync(g.d_ops + o_tick, 0, plk_poly_eval_workspace(n), g.st));
+  for (int b = 0; b < n; b += PLK_EVAL_MAX_JOBS) {
+    const int m = n - b < PLK_EVAL_MAX_JOBS ? n - b : PLK_EVAL_MAX_JOBS;
+    uint64_t l64[PLK_EVAL_MAX_JOBS];
+    for (int i = 0; i < m; i++) l64[i] = lens[b + i];
+    if ((rc = plk_poly_eval_batch_launch(dp.data() + b, l64, xs + b, m, g.d_ops + o_y + b,
+                                         g.d_ops + o_tick + (size_t)128 * b, g.st)))
+      return rc;
+  }
+  PLK_HIP(hipMemcpyAsync(ys, g.d_ops + o_y, n, hipMemcpyDeviceToHost, g.st));
+  PLK_HIP(hipStreamSynchronize(g.st));
+  return PLK_OK;
+}
+
+int plk_poly_eval(const uint8_t* p, size_t len, uint8_t x, uint8_t* y) {
+  const uint8_t* ps[1] = {p};
+  const size_t ls[1] = {len};
+  return plk_poly_eval_batch(ps, ls, &x, 1, y);
+}
+
+size_t plk_poly_divide_workspace(size_t nl, size_t dl) { return plk_poly_divide_workspace_bytes(nl, dl); }
+
+int plk_poly_divide_dev(const uint8_t* d_num, size_t nl, const uint8_t* den, size_t dl, uint8_t* d_quot,
+                        uint8_t* d_rem, uint32_t* d_lens, void* d_work, void* stream) {
+  int rc = ensure_dev();
+  if (rc) return rc;
+  if (!d_quot || !d_lens || !d_work || (dl > 1 && nl && !d_rem)) {
+    plk_set_error("plk_poly_divide_dev: NULL buffer");
+    return PLK_ERR_ARG;
+  }
+  return plk_poly_divide_launch(d_num, nl, den, dl, d_quot, d_rem, d_lens, d_work, pick(stream));
+}
+
+int plk_poly_divide(const uint8_t* num, size_t nl, const uint8_t* den, size_t dl, uint8_t* quot, size_t* quot_len,
+                    uint8_t* rem, size_t* rem_len) {
+  if (!quot || !quot_len || !rem_len || (nl && !num)) {
+    plk_set_error("plk_poly_divide: NULL argument");
+    return PLK_ERR_ARG;
+  }
+  std::lock_guard<std::mutex> lk(g.mu);
+  int rc = ensure_locked();
+  if (rc) return rc;
+  const size_t ql = nl >= dl ? nl - dl + 1 : 1;
+  const size_t rl = dl ? (dl - 1 < nl ? dl - 1 : nl) : 0;
+  if (rl && !rem) {
+    plk_set_error("plk_poly_divide: NULL remainder buffer");
+    return PLK_ERR_ARG;
+  }
+  Arena A;
+  const size_t o_num = A.take(nl + 16), o_q = A.take(nl + 16), o_r = A.take(nl + 16), o_len = A.take(16),
+               o_w = A.take(plk_poly_divide_workspace_bytes(nl, dl));
+  if ((rc = grow(&g.d_ops, &g.cap_ops, A.off))) return rc;
+  uint8_t* d = g.d_ops;
+  if ((rc = upload(d + o_num, num, nl))) return rc;
+  if ((rc = plk_poly_divide_launch(d + o_num, nl, den, dl, d + o_q, d + o_r, (uint32_t*)(d + o_len), d + o_w, g.st)))
+    return rc;
+  uint32_t lens[2] = {0, 0};
+  PLK_HIP(hipMemcpyAsync(quot, d + o_q, ql, hipMemcpyDeviceToHost, g.st));
+  if (rl) PLK_HIP(hipMemcpyAsync(rem, d + o_r, rl, hipMemcpyDeviceToHost, g.st));
+  PLK_HIP(hipMemcpyAsync(lens, d + o_len, 8, hipMemcpyDeviceToHost, g.st));
+  PLK_HIP(hipStreamSynchronize(g.st));
+  // poly_new's trim keeps one coefficient (src/poly.h:21-24); a zero-length remainder stays empty
+  *quot_len = lens[0] ? lens[0] : 1;
+  *rem_len = rl ? (lens[1] ? lens[1] : 1) : 0;
+  return PLK_OK;
+}
+
+int plk_matrix_mul(const uint8_t* a, size_t m, size_t k, const uint8_t* b, size_t n, uint8_t* out) {
+  if ((m * k && !a) || (k * n && !b) || (m * n && !out)) {
+    plk_set_error("plk_matrix_mul: NULL argument");
+    return PLK_ERR_ARG;
+  }
+  if (!m || !n) return PLK_OK;
+  std::lock_guard<std::mutex> lk(g.mu);
+  int rc = ensure_locked();
+  if (rc) return rc;
+  Arena A;
+  const size_t o_a = A.take(m * k), o_b = A.take(k * n), o_o = A.take(m * n);
+  if ((rc = grow(&g.d_ops, &g.cap_ops, A.off))) return rc;
+  uint8_t* d = g.d_ops;
+  if ((rc = upload(d + o_a, a, m * k)) || (rc = upload(d + o_b, b, k * n))) return rc;
+  if ((rc = plk_matrix_mul_launch(d + o_a, m, k, d + o_b, n, d + o_o, g.st))) return rc;
+  PLK_HIP(hipMemcpyAsync(out, d + o_o, m * n, hipMemcpyDeviceToHost, g.st));
+  PLK_HIP(hipStreamSynchronize(g.st));
+  return PLK_OK;
+}
+
+int plk_matrix_inv(const uint8_t* mat, size_t n, uint8_t* out) {
+  if (n && (!mat || !out)) {
+    plk_set_error("plk_matrix_inv: NULL argument");
+    return PLK_ERR_ARG;
+  }
+  for (size_t i = 0; i < n * n; i++)
+    if (mat[i] >= 17) {   // hf_div of a raw pivot reads hf_inverses out of bounds in the reference
+      plk_set_error("plk_matrix_inv: entry %zu = %u is not a GF(17) value (reference behaviour undefined)", i,
+                    (unsigned)mat[i]);
+      return PLK_ERR_RANGE;
+    }
+  if (!n) return PLK_OK;
+  std::lock_guard<std::mutex> lk(g.mu);
+  int rc = ensure_locked();
+  if (rc) return rc;
+  Arena A;
+  const size_t o_m = A.take(n * n), o_aug = A.take(2 * n * n), o_o = A.take(n * n);
+  if ((rc = grow(&g.d_ops, &g.cap_ops, A.off))) return rc;
+  uint8_t* d = g.d_ops;
+  if ((rc = upload(d + o_m, mat, n * n))) return rc;
+  if ((rc = plk_matrix_inv_launch(d + o_m, n, d + o_aug, d + o_o, g.st))) return rc;
+  PLK_HIP(hipMemcpyAsync(out, d + o_o, n * n, hipMemcpyDeviceToHost, g.st));
+  PLK_HIP(hipStreamSynchronize(g.st));
+  return PLK_OK;
+}
+
+int plk_interpolate(const uint8_t* h_pows_inv, const uint8_t* values, size_t n, uint8_t* out, size_t* out_len) {
+  if (!out_len || (n && (!h_pows_inv || !values || !out))) {
+    plk_set_error("plk_interpolate: NULL argument");
+    return PLK_ERR_ARG;
+  }
+  if (!n) {
+    *out_len = 0;
+    return PLK_OK;
+  }
+  std::lock_guard<std::mutex> lk(g.mu);
+  int rc = ensure_locked();
+  if (rc) return rc;
+  Arena A;
+  const size_t o_m = A.take(n * n), o_v = A.take(n), o_o = A.take(n), o_len = A.take(16);
+  if ((rc = grow(&g.d_ops, &g.cap_ops, A.off))) return rc;
+  uint8_t* d = g.d_ops;
+  if ((rc = upload(d + o_m, h_pows_inv, n * n)) || (rc = upload(d + o_v, values, n))) return rc;
+  if ((rc = plk_matrix_mul_launch(d + o_m, n, n, d + o_v, 1, d + o_o, g.st))) return rc;
+  if ((rc = plk_trim_launch(d + o_o, n, (uint32_t*)(d + o_len), g.st))) return rc;
+  uint32_t nz = 0;
+  PLK_HIP(hipMemcpyAsync(out, d + o_o, n, hipMemcpyDeviceToHost, g.st));
+  PLK_HIP(hipMemcpyAsync(&nz, d + o_len, 4, hipMemcpyDeviceToHost, g.st));
+  PLK_HIP(hipStreamSynchronize(g.st));
+  *out_len = nz ? nz : 1;
+  return PLK_OK;
 }
 
 }  // extern "C"

@@ -343,6 +343,12 @@ __global__ __launch_bounds__(1024) void trim_kernel(const uint8_t* __restrict__ 
   if (threadIdx.x == 0) *nz = 0;
 }
 
+int plk_trim_launch(const uint8_t* d, uint64_t len, uint32_t* d_nz, hipStream_t st) {
+  hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d, len, d_nz);
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
 // Direct convolution when one operand is short: out[i] = sum_j a[j] b[i-j] mod 17 over the
 // short operand s (length ls <= 32, staged in LDS), the long one read coalesced.
 __global__ __launch_bounds__(256) void polymul_direct_kernel(const uint8_t* lg, uint64_t llg, const uint8_t* sh,
@@ -644,11 +650,17 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
 // the caller reports length 1).
 int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
                         uint32_t* d_nz, void* d_work, hipStream_t st) {
-  if (la == 0 || lb == 0) return PLK_ERR_ARG;
+  if (la == 0 || lb == 0) {
+    plk_set_error("poly_mul: empty operand (la %llu, lb %llu)", (unsigned long long)la, (unsigned long long)lb);
+    return PLK_ERR_ARG;
+  }
   const uint64_t rl = la + lb - 1;
   const uint64_t mn = la < lb ? la : lb;
-  if (mn * 256 >= bb::P) return PLK_ERR_RANGE;
-  if (rl >= (1ull << 32)) return PLK_ERR_RANGE;
+  if (mn * 256 >= bb::P || rl >= (1ull << 32)) {
+    plk_set_error("poly_mul: %llu x %llu outside the exact range (min(la, lb) * 256 < %u, la + lb - 1 < 2^32)",
+                  (unsigned long long)la, (unsigned long long)lb, bb::P);
+    return PLK_ERR_RANGE;
+  }
   if (mn <= PLK_DIRECT_MAX) {
     const uint8_t* lg = la >= lb ? d_a : d_b;
     const uint8_t* sh = la >= lb ? d_b : d_a;
@@ -663,7 +675,11 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
   }
   uint64_t e = 0;
   const int k = product_plan(la, lb, &e);
-  if (k > bb::TWO_ADICITY) return PLK_ERR_RANGE;
+  if (k > bb::TWO_ADICITY) {
+    plk_set_error("poly_mul: %llu x %llu needs a 2^%d transform (max 2^%d)", (unsigned long long)la,
+                  (unsigned long long)lb, k, bb::TWO_ADICITY);
+    return PLK_ERR_RANGE;
+  }
   const uint32_t ninv = bb::hpow(1ull << k, bb::P - 2);   // normal form on purpose
   if (k <= PLK_SMALL_LOG) {   // (never wrapped: product_plan only wraps above 2^(SMALL_LOG+1))
     const size_t lds = (size_t)4 * (2 * col_stride(1 << k) + 2 * (1 << k));
@@ -672,7 +688,11 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
     PLK_HIP(hipGetLastError());
     return PLK_OK;
   }
-  if (!d_work) return PLK_ERR_ARG;
+  if (!d_work) {
+    plk_set_error("poly_mul: %llu x %llu needs a workspace (plk_poly_mul_workspace)", (unsigned long long)la,
+                  (unsigned long long)lb);
+    return PLK_ERR_ARG;
+  }
   const PlkPolyMulJob job{d_a, la, d_b, lb, d_out};
   int rc = ntt_group(&job, 1, k, e ? &e : nullptr, d_work, st);
   if (rc) return rc;
@@ -695,7 +715,10 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
   for (int i = 0; i < nj; i++) {
     const PlkPolyMulJob& j = jobs[i];
     ks[i] = -1;
-    if (j.la == 0 || j.lb == 0) return PLK_ERR_ARG;
+    if (j.la == 0 || j.lb == 0) {
+      plk_set_error("poly_mul batch: job %d has an empty operand", i);
+      return PLK_ERR_ARG;
+    }
     const uint64_t mn = j.la < j.lb ? j.la : j.lb;
     const int k = product_plan(j.la, j.lb, &es[i]);
     if (j.acc && !(mn > PLK_DIRECT_MAX && k > PLK_SMALL_LOG)) {
@@ -707,7 +730,11 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
       return PLK_ERR_ARG;
     }
     if (mn > PLK_DIRECT_MAX && k > PLK_SMALL_LOG) {
-      if (mn * 256 >= bb::P || k > bb::TWO_ADICITY) return PLK_ERR_RANGE;
+      if (mn * 256 >= bb::P || k > bb::TWO_ADICITY) {
+        plk_set_error("poly_mul batch: job %d (%llu x %llu) outside the exact range", i, (unsigned long long)j.la,
+                      (unsigned long long)j.lb);
+        return PLK_ERR_RANGE;
+      }
       ks[i] = k;
       continue;
     }
@@ -757,7 +784,10 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
 // or inverse (DIT, bit-reversed -> natural, NOT scaled by N^-1).  Same passes as poly_mul.
 // batch independent arrays at d + b 2^k share each pass's launch (up to 12 per launch).
 int plk_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st) {
-  if (k < 1 || k > bb::TWO_ADICITY || batch < 1) return PLK_ERR_RANGE;
+  if (k < 1 || k > bb::TWO_ADICITY || batch < 1) {
+    plk_set_error("ntt: log_n %d (1..%d), batch %d", k, bb::TWO_ADICITY, batch);
+    return PLK_ERR_RANGE;
+  }
   if (plk_wave_ntt_supported(k)) return plk_wave_ntt_launch(d, k, batch, inverse, st);
   // k <= 12: one workgroup-tile pass (lo = 0, a single tile holds the whole array)
   const Tw tw = inverse ? tw_inv() : tw_fwd();

@@ -17,6 +17,8 @@ static_assert(offsetof(plk_msm_result_t, log) == 8 && offsetof(plk_msm_result_t,
 #define PLK_DIRECT_MAX 32      // poly_mul with min(la, lb) <= 32: direct convolution
 
 void plk_set_error(const char* fmt, ...);
+int plk_ctx_retain(void);    // a device prover is alive (capi.hip): plk_shutdown keeps the tables
+void plk_ctx_release(void);
 
 #define PLK_HIP(call)                                                                    \
   do {                                                                                   \
@@ -99,3 +101,16 @@ int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, int field, u
 int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st);
 int plk_wave_init_coltabs(void);    // after plk_ntt_init_tables' root tables
 void plk_wave_free_coltabs(void);
+
+// polyops.hip: poly_eval / poly_divide / matrix ops
+#define PLK_EVAL_MAX_JOBS 32
+int plk_poly_eval_batch_launch(const uint8_t* const* polys, const uint64_t* lens, const uint8_t* xs, int nj,
+                               uint8_t* d_y, void* d_tick, hipStream_t st);
+size_t plk_poly_divide_workspace_bytes(uint64_t nl, uint64_t dl);
+int plk_poly_divide_launch(const uint8_t* d_num, uint64_t nl, const uint8_t* den, uint64_t dl, uint8_t* d_q,
+                           uint8_t* d_rem, uint32_t* d_lens, void* d_work, hipStream_t st);
+int plk_matrix_mul_launch(const uint8_t* d_a, uint64_t m, uint64_t k, const uint8_t* d_b, uint64_t n, uint8_t* d_out,
+                          hipStream_t st);
+int plk_matrix_inv_launch(const uint8_t* d_mat, uint64_t n, uint8_t* d_aug, uint8_t* d_out, hipStream_t st);
+// ntt.hip: index + 1 of the last non-zero byte of d[0, len) (0 if none) into *d_nz
+int plk_trim_launch(const uint8_t* d, uint64_t len, uint32_t* d_nz, hipStream_t st);

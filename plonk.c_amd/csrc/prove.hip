@@ -1356,7 +1356,7 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
     plk_set_error("plk_prover_create: n, z_h and srs are required");
     return PLK_ERR_ARG;
   }
-  int rc = plk_init(-1);
+  int rc = plk_ctx_retain();
   if (rc) return rc;
   plk_prover* P = new plk_prover();
   P->n = d->n;
@@ -1364,7 +1364,12 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   // Z_H: trimmed as poly_z returns it; classify
   size_t zl = d->z_h_len;
   while (zl > 1 && d->z_h[zl - 1] == 0) zl--;
-  if (zl == 1 && d->z_h[0] == 0) { delete P; plk_set_error("Division by zero polynomial in poly_divide"); return PLK_ERR_ARG; }
+  if (zl == 1 && d->z_h[0] == 0) {
+    delete P;
+    plk_ctx_release();
+    plk_set_error("Division by zero polynomial in poly_divide");
+    return PLK_ERR_ARG;
+  }
   P->zh_len = zl;
   P->zh_lead = d->z_h[zl - 1] % HFP;
   P->zh_c = d->z_h[0] % HFP;
@@ -1418,6 +1423,7 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   if (hipMalloc((void**)&P->mem, P->mem_bytes) != hipSuccess) {
     plk_set_error("plk_prover_create: hipMalloc(%zu) failed", P->mem_bytes);
     delete P;
+    plk_ctx_release();
     return PLK_ERR_NOMEM;
   }
   if (hipHostMalloc((void**)&P->h_res, 64 + 4 * NSTAT, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -1479,6 +1485,7 @@ void plk_prover_destroy(plk_prover_t* P) {
   if (P->h_res) (void)hipHostFree(P->h_res);
   if (P->st) (void)hipStreamDestroy(P->st);
   delete P;
+  plk_ctx_release();
 }
 
 size_t plk_prover_device_bytes(const plk_prover_t* P) { return P ? P->mem_bytes : 0; }

@@ -51,6 +51,16 @@ SIGNATURES = {
     "plk_poly_mul_batch_dev": (C.c_int, [_vp, C.c_int, _vp, _sz, _vp]),
     "plk_ntt_dev": (C.c_int, [_vp, C.c_int, C.c_int, _vp]),
     "plk_ntt_batch_dev": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, _vp]),
+    "plk_poly_eval": (C.c_int, [_u8p, _sz, C.c_uint8, _u8p]),
+    "plk_poly_eval_batch": (C.c_int, [C.POINTER(_u8p), C.POINTER(_sz), _u8p, C.c_int, _u8p]),
+    "plk_poly_eval_workspace": (_sz, [C.c_int]),
+    "plk_poly_eval_batch_dev": (C.c_int, [C.POINTER(_vp), C.POINTER(_sz), _u8p, C.c_int, _vp, _vp, _vp]),
+    "plk_poly_divide": (C.c_int, [_u8p, _sz, _u8p, _sz, _u8p, C.POINTER(_sz), _u8p, C.POINTER(_sz)]),
+    "plk_poly_divide_workspace": (_sz, [_sz, _sz]),
+    "plk_poly_divide_dev": (C.c_int, [_vp, _sz, _u8p, _sz, _vp, _vp, _vp, _vp, _vp]),
+    "plk_matrix_mul": (C.c_int, [_u8p, _sz, _sz, _u8p, _sz, _u8p]),
+    "plk_matrix_inv": (C.c_int, [_u8p, _sz, _u8p]),
+    "plk_interpolate": (C.c_int, [_u8p, _u8p, _sz, _u8p, C.POINTER(_sz)]),
     "plk_prover_create": (C.c_int, [_vp, C.POINTER(_vp)]),
     "plk_prover_destroy": (None, [_vp]),
     "plk_prover_device_bytes": (_sz, [_vp]),
@@ -172,6 +182,61 @@ def poly_mul(a, b):
     return bytes(out[:n.value])
 
 
+def poly_eval(p, x):
+    """Horner at x exactly as src/poly.h:265-272 (raw HF bytes included)."""
+    p = _u8(p).reshape(-1)
+    y = np.zeros(1, np.uint8)
+    _check("plk_poly_eval", lib().plk_poly_eval(_p(p), p.size, int(x) & 0xFF, _p(y)))
+    return int(y[0])
+
+
+def poly_eval_batch(polys, xs):
+    arrs = [_u8(p).reshape(-1) for p in polys]
+    n = len(arrs)
+    ptrs = (_u8p * n)(*[_p(a) for a in arrs])
+    lens = (_sz * n)(*[a.size for a in arrs])
+    xa = _u8(xs).reshape(-1)
+    ys = np.zeros(n, np.uint8)
+    _check("plk_poly_eval_batch", lib().plk_poly_eval_batch(ptrs, lens, _p(xa), n, _p(ys)))
+    return [int(v) for v in ys]
+
+
+def poly_divide(num, den):
+    """(quot, rem) bytes, trimmed as src/poly.h:124-177 returns them."""
+    num = _u8(num).reshape(-1)
+    den = _u8(den).reshape(-1)
+    q = np.zeros(max(num.size, 1), np.uint8)
+    r = np.zeros(max(num.size, 1), np.uint8)
+    ql, rl = _sz(0), _sz(0)
+    _check("plk_poly_divide", lib().plk_poly_divide(_p(num), num.size, _p(den), den.size, _p(q), C.byref(ql),
+                                                    _p(r), C.byref(rl)))
+    return bytes(q[:ql.value]), bytes(r[:rl.value])
+
+
+def matrix_mul(a, m, k, b, n):
+    a = _u8(a).reshape(-1)
+    b = _u8(b).reshape(-1)
+    out = np.zeros(max(m * n, 1), np.uint8)
+    _check("plk_matrix_mul", lib().plk_matrix_mul(_p(a), m, k, _p(b), n, _p(out)))
+    return bytes(out[:m * n])
+
+
+def matrix_inv(mat, n):
+    mat = _u8(mat).reshape(-1)
+    out = np.zeros(max(n * n, 1), np.uint8)
+    _check("plk_matrix_inv", lib().plk_matrix_inv(_p(mat), n, _p(out)))
+    return bytes(out[:n * n])
+
+
+def interpolate(h_pows_inv, values):
+    v = _u8(values).reshape(-1)
+    m = _u8(h_pows_inv).reshape(-1)
+    out = np.zeros(max(v.size, 1), np.uint8)
+    ol = _sz(0)
+    _check("plk_interpolate", lib().plk_interpolate(_p(m), _p(v), v.size, _p(out), C.byref(ol)))
+    return bytes(out[:ol.value])
+
+
 # ---------------------------------------------------------------- device entry points
 def _ptr(t):
     if t is None:
@@ -251,6 +316,31 @@ def poly_mul_batch_dev(jobs, work, work_bytes, stream=None):
     arr = _jobs(jobs)
     _check("plk_poly_mul_batch_dev", lib().plk_poly_mul_batch_dev(arr, len(jobs), _ptr(work), int(work_bytes),
                                                                   _stream(stream)))
+
+
+def poly_eval_workspace(n):
+    return int(lib().plk_poly_eval_workspace(int(n)))
+
+
+def poly_eval_batch_dev(polys, lens, xs, ys, tick, stream=None):
+    """polys: device tensors (or raw pointers); tick: zeroed device workspace."""
+    n = len(polys)
+    ptrs = (_vp * n)(*[_ptr(p) for p in polys])
+    ls = (_sz * n)(*[int(v) for v in lens])
+    xa = _u8(xs).reshape(-1)
+    _check("plk_poly_eval_batch_dev", lib().plk_poly_eval_batch_dev(ptrs, ls, _p(xa), n, _ptr(ys), _ptr(tick),
+                                                                    _stream(stream)))
+
+
+def poly_divide_workspace(nl, dl):
+    return int(lib().plk_poly_divide_workspace(int(nl), int(dl)))
+
+
+def poly_divide_dev(num, nl, den, quot, rem, lens, work, stream=None):
+    """den: HOST bytes (classified on the host)."""
+    d = _u8(den).reshape(-1)
+    _check("plk_poly_divide_dev", lib().plk_poly_divide_dev(_ptr(num), int(nl), _p(d), d.size, _ptr(quot),
+                                                            _ptr(rem), _ptr(lens), _ptr(work), _stream(stream)))
 
 
 def ntt_dev(data, log_n, inverse=False, stream=None):

@@ -115,4 +115,5 @@ def test_reference_plonk_test_compiles_against_dropin(tmp_path):
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     nm = subprocess.run(["nm", str(tmp_path / "plonk-test")], capture_output=True, text=True).stdout
-    assert "U plk_poly_mul" in nm and "U plk_msm_g1" in nm
+    for sym in ("plk_poly_mul", "plk_msm_g1", "plk_poly_divide", "plk_poly_eval", "plk_matrix_inv", "plk_matrix_mul"):
+        assert "U " + sym in nm, sym

@@ -1,6 +1,8 @@
-"""Point-range sharded MSM over world_size 2 with gloo on CPU: shards + one SUM all-reduce of
-partial logs must reproduce the single-device result bit for bit (the partials come from
-the oracle here; on the GPU box they come from libplonkhip)."""
+"""Point-range sharded MSM over gloo on CPU (world 2 and 3): `plonkhip.dist.sharded_msm` -- the
+exact function bench.py runs over RCCL -- must reproduce the single-device serial fold bit for
+bit (reference srs_eval_at_s, src/srs.h:53-68), including MSMs whose irregular encodings force
+the gathered serial fold.  The per-shard partials come from the oracle here; on the GPU box they
+come from libplonkhip (`plonkhip.dist.gpu_ops`)."""
 import os
 import socket
 
@@ -19,49 +21,102 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, batch, q):
+def _inputs(n, batch, irregular_at):
+    out = []
+    for b in range(batch):
+        pts, sc = gen.msm_inputs(100 + b, n, "full")
+        pts = pts.copy()
+        if b in irregular_at:                     # an off-curve point inside the given index
+            pts[irregular_at[b]] = (5, 5, 0)
+        out.append((pts, sc))
+    return out
+
+
+class OracleOps:
+    """sharded_msm's compute, from the CPU oracle (test infrastructure)."""
+
+    def __init__(self, orc):
+        self.orc = orc
+
+    def partials(self, shard_points, shard_scalars):
+        import torch
+        rows = []
+        for p, s in zip(shard_points, shard_scalars):
+            log, _ = self.orc.msm_dlog(p.numpy(), s.numpy())
+            rows.append([0, 1] if log is None else [log, 0])
+        return torch.tensor(rows, dtype=torch.int32)
+
+    def exp(self, logs):
+        import torch
+        return torch.tensor([list(self.orc.dlog_exp(int(v))) + [0] for v in logs], dtype=torch.uint8)
+
+    def fold(self, points, scalars):
+        return self.orc.msm(points.numpy(), scalars.numpy())
+
+
+def _worker(rank, world, port, n, batch, irregular_at, q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(here)
-    for p in (os.path.join(root, "plonk.c_amd"), os.path.join(root, "oracle"), os.path.join(here, "golden")):
+    for p in (os.path.join(root, "plonk.c_amd"), os.path.join(root, "oracle"), here, os.path.join(here, "golden")):
         sys.path.insert(0, p)
+    import torch
     import torch.distributed as dist
 
-    import gen as g
-    from plonkhip.dist import sharded_msm_logs
+    from plonkhip.dist import g1_bytes, shard_range, sharded_msm
     from pyoracle import Oracle
+    from test_dist_cpu import OracleOps, _inputs
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    orc = Oracle()
-    inputs = [g.msm_inputs(100 + b, n, "full") for b in range(batch)]
-
-    def partial(lo, hi, b):
-        pts, sc = inputs[b]
-        return orc.msm_dlog(pts[lo:hi], sc[lo:hi])[0]
-
-    logs = sharded_msm_logs(n, rank, world, partial, batch=batch)
-    q.put((rank, [orc.dlog_exp(int(v)).hex() for v in logs]))
+    lo, hi = shard_range(n, rank, world)
+    sp, ss = [], []
+    for pts, sc in _inputs(n, batch, irregular_at):
+        sp.append(torch.from_numpy(pts[lo:hi].reshape(-1).copy()))
+        ss.append(torch.from_numpy(sc[lo:hi].copy()))
+    out, folded = sharded_msm(sp, ss, n, OracleOps(Oracle()))
+    q.put((rank, [o.hex() for o in g1_bytes(out)], folded))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _run(world, n, batch, irregular_at):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, batch, irregular_at, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, out, folded = q.get(timeout=120)
+        got[r] = (out, folded)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_msm_matches_single_device(oracle, world):
     n, batch = 10007, 3
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, batch, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    got = dict(q.get(timeout=120) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    want = [oracle.msm(*gen.msm_inputs(100 + b, n, "full")).hex() for b in range(batch)]
+    got = _run(world, n, batch, {})
+    want = [oracle.msm(p, s).hex() for p, s in _inputs(n, batch, {})]
     for r in range(world):
-        assert got[r] == want
+        assert got[r] == (want, 0)
+
+
+def test_irregular_point_in_a_later_shard(oracle):
+    """an off-curve point in rank 1's shard of MSM 1 (and in rank 0's of MSM 2): those MSMs take
+    the gathered serial fold and still equal the reference fold; MSM 0 stays on the log path"""
+    from plonkhip.dist import shard_range
+    n, batch, world = 4099, 3, 2
+    lo1, _ = shard_range(n, 1, world)
+    irregular_at = {1: lo1 + 17, 2: 3}
+    got = _run(world, n, batch, irregular_at)
+    want = [oracle.msm(p, s).hex() for p, s in _inputs(n, batch, irregular_at)]
+    for r in range(world):
+        assert got[r] == (want, 2)
 
 
 def test_shard_ranges_cover_exactly():

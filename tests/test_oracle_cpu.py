@@ -167,3 +167,26 @@ def test_poly_mul_ntt_beyond_two_adicity(oracle):
     want = (full % 17).astype(np.uint8).tobytes().rstrip(b"\x00") or b"\x00"
     ok = got == want
     assert ok
+
+
+def test_polyops_goldens(oracle):
+    """the oracle's poly_divide / poly_eval / matrix restatements vs the reference's outputs
+    (tests/golden/polyops.json)"""
+    from make_golden import big_division_inputs
+    g = load_golden("polyops.json")
+    for c in g["divide"]:
+        q, r = oracle.poly_divide(bytes.fromhex(c["num"]), bytes.fromhex(c["den"]))
+        assert (q.hex(), r.hex()) == (c["q"], c["r"]), c["note"]
+    for c in g["divide_big"]:
+        if c["nl"] * (2 if c["kind"] != "binomial" else 1) > 1 << 21 and c["kind"] == "general":
+            continue
+        a, b = big_division_inputs(c["seed"], c["nl"], c["kind"], c["param"])
+        q, r = oracle.poly_divide(a, b)
+        assert gen.digest(np.frombuffer(q, np.uint8)) == c["q_sha256"]
+        assert gen.digest(np.frombuffer(r, np.uint8)) == c["r_sha256"]
+    for c in g["eval"]:
+        assert oracle.poly_eval(bytes.fromhex(c["p"]), c["x"]) == c["y"], c["note"]
+    for c in g["matrix_inv"]:
+        assert oracle.matrix_inv(bytes.fromhex(c["m"]), c["n"]).hex() == c["inv"], c["note"]
+    for c in g["matrix_mul"]:
+        assert oracle.matrix_mul(bytes.fromhex(c["a"]), c["m"], c["k"], bytes.fromhex(c["b"]), c["n"]).hex() == c["out"]

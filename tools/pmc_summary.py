@@ -12,9 +12,12 @@ runs with --pmc only (no --sys-trace / --runtime-trace), its own process.
 grid_y == BATCH, i.e. BATCH MSMs of 2^LOG2N points per launch).
 """
 import json
+import os
 import sqlite3
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def summarise(db, sub="msm_dlog_kernel"):
@@ -50,8 +53,10 @@ if __name__ == "__main__":
         match = [r for r in rows if r["grid"][1] == batch]
         if match:
             r = match[0]
+            from bench import kernel_source_hash
             with open(path, "w") as f:
                 json.dump({"log2n": log2n, "msm_batch": batch, "kernel": r["kernel"],
+                           "source_sha16": kernel_source_hash(),
                            "grid": r["grid"], "block": r["block"], "dispatches": r["dispatches"],
                            "fetch_size_kib_avg": r["fetch_size_kib_avg"],
                            "hbm_bytes_per_launch": r["hbm_read_bytes_est"],
