@@ -290,6 +290,25 @@ def components(torch, hip, dev, st):
                        "note": "one launch per MSM, back-to-back on one stream: device time from 64 launches "
                                "replayed as a HIP graph%s; eager_us_per_call = one Python call per launch "
                                "(host-rate bound)" % ("" if gr else " (capture unavailable: eager)")}
+    # the drop-in's srs_eval_at_s path (plk_msm_g1, host buffers): 2^20 points, the SRS bytes
+    # unchanged between calls (device copy reused after a memcmp) vs a fresh SRS array each call
+    n20 = 1 << 20
+    p20, s20 = make_msm_sets(torch, n20, 1, dev, 99)
+    ph20, sh20 = p20[0].cpu().numpy(), s20[0].cpu().numpy()
+    hip.msm_g1(ph20, sh20)
+    t0 = time.perf_counter()
+    for _ in range(10):
+        hip.msm_g1(ph20, sh20)
+    cached_us = (time.perf_counter() - t0) / 10 * 1e6
+    copies = [ph20.copy() for _ in range(10)]
+    t0 = time.perf_counter()
+    for c in copies:
+        hip.msm_g1(c, sh20)
+    fresh_us = (time.perf_counter() - t0) / 10 * 1e6
+    out["msm_2^20_host_call"] = {"srs_cached_us": round(cached_us, 1), "srs_uploaded_us": round(fresh_us, 1),
+                                 "note": "plk_msm_g1 (what the drop-in srs_eval_at_s calls), host buffers, PCIe "
+                                         "included; cached = same SRS pointer and bytes (reference: 9 commitments "
+                                         "per proof over one SRS, src/plonk.h:299-301,379,522-524,620-621)"}
     # C3: forward NTT 2^20 over BabyBear (Montgomery u32, in place, 2 passes)
     k = 20
     bufs = [torch.randint(0, 2013265921, (1 << k,), dtype=torch.int64, device=dev).to(torch.int32)
