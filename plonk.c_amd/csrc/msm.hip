@@ -350,22 +350,69 @@ __device__ RawPt r_addp(RawPt a, RawPt b) {
 }
 }  // namespace
 
-__global__ void msm_serial_fold_kernel(const uint8_t* __restrict__ pts, const uint8_t* __restrict__ sc,
-                                       uint64_t n, PlkMsmResult* res) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  RawPt acc{0, 0, 1};
-  for (uint64_t i = 0; i < n; i++) {
+// The reference's fold for inputs with irregular encodings, exactly.  For canonical points the
+// raw formulas ARE the group law, so the fold's prefix up to the first irregular
+// point equals EXP[sum c_i LOG(P_i)]: one block sums that prefix in parallel (discrete logs
+// through the LDS table, 16 points per thread per chunk, stopping at the chunk that holds the
+// first irregular point), then one thread continues the raw fold from that point to the end.
+constexpr int FOLD_T = 1024, FOLD_E = 16;
+__global__ __launch_bounds__(FOLD_T) void msm_serial_fold_kernel(const uint8_t* __restrict__ pts,
+                                                                 const uint8_t* __restrict__ sc, uint64_t n,
+                                                                 PlkMsmResult* res) {
+  __shared__ uint32_t tab[TAB_ENTRIES];
+  __shared__ uint32_t wsum[FOLD_T / PLK_WAVE];
+  __shared__ unsigned long long s_first;
+  if (blockIdx.x != 0) return;
+  for (int i = threadIdx.x; i < TAB_ENTRIES; i += FOLD_T) tab[i] = c_ytab[i];
+  if (threadIdx.x == 0) s_first = ~0ull;
+  __syncthreads();
+  uint32_t acc = 0;
+  uint64_t first = ~0ull;
+  for (uint64_t base = 0; base < n && first == ~0ull; base += (uint64_t)FOLD_T * FOLD_E) {
+    uint32_t lg[FOLD_E];
+    unsigned long long mine = ~0ull;
+#pragma unroll
+    for (int k = 0; k < FOLD_E; k++) {
+      const uint64_t i = base + (uint64_t)k * FOLD_T + threadIdx.x;
+      lg[k] = 0;
+      if (i < n) {
+        bool bad = false;
+        const uint32_t t = point_term<1>(encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), sc[i], tab, 0u, bad);
+        lg[k] = t;
+        if (bad && i < mine) mine = i;
+      }
+    }
+    if (mine != ~0ull) atomicMin(&s_first, mine);
+    __syncthreads();
+    first = s_first;                    // uniform: the first irregular index so far (or none)
+#pragma unroll
+    for (int k = 0; k < FOLD_E; k++) {
+      const uint64_t i = base + (uint64_t)k * FOLD_T + threadIdx.x;
+      if (i < first) acc += lg[k];      // (i < n: lg = 0 past the end)
+    }
+    acc %= PLK_GROUP_ORDER;
+    __syncthreads();
+  }
+  const uint32_t ws = plk_wave_sum(acc);
+  if ((threadIdx.x & (PLK_WAVE - 1)) == 0) wsum[threadIdx.x / PLK_WAVE] = ws;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  uint32_t tot = 0;
+  for (int w = 0; w < FOLD_T / PLK_WAVE; w++) tot += wsum[w];
+  const uint32_t lg0 = tot % PLK_GROUP_ORDER;
+  RawPt a{c_exp[4 * lg0], c_exp[4 * lg0 + 1], c_exp[4 * lg0 + 2]};   // the fold over [0, first)
+  for (uint64_t i = first; i < n; i++) {
     RawPt run{pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
     RawPt term{0, 0, 1};
     for (uint32_t k = sc[i]; k; k >>= 1) {
       if (k & 1) term = r_addp(term, run);
       run = r_double(run);
     }
-    acc = r_addp(acc, term);
+    a = r_addp(a, term);
   }
-  res->g1[0] = (uint8_t)acc.x;
-  res->g1[1] = (uint8_t)acc.y;
-  res->g1[2] = (uint8_t)acc.inf;
+  res->g1[0] = (uint8_t)a.x;
+  res->g1[1] = (uint8_t)a.y;
+  res->g1[2] = (uint8_t)a.inf;
   res->g1[3] = 0;
 }
 
@@ -510,7 +557,7 @@ int plk_msm_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsm
 
 int plk_msm_serial_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsmResult* d_res,
                           hipStream_t st) {
-  hipLaunchKernelGGL(msm_serial_fold_kernel, dim3(1), dim3(64), 0, st, d_pts, d_sc, n, d_res);
+  hipLaunchKernelGGL(msm_serial_fold_kernel, dim3(1), dim3(FOLD_T), 0, st, d_pts, d_sc, n, d_res);
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }

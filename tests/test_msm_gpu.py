@@ -81,6 +81,21 @@ def test_irregular_late_in_large_input(hip, oracle):
     assert hip.msm_g1(pts, sc) == oracle.msm(pts, sc)
 
 
+@pytest.mark.parametrize("where", ["first", "chunk_edge", "last"])
+def test_irregular_in_2_22_points(hip, oracle, where):
+    """one irregular point in a 2^22-point input: the prefix before it is summed in parallel,
+    the raw fold runs from it (reference fold, src/srs.h:59-66); before, every point of the
+    input went through one GPU lane"""
+    c = load_golden("msm.json")["large"][7]
+    pts, sc = gen.msm_inputs(c["seed"], c["n"], c["kind"])
+    pts = pts.copy()
+    idx = {"first": 0, "chunk_edge": 16384 * 3 - 1, "last": c["n"] - 1}[where]
+    pts[idx] = (5, 5, 0)
+    sc = sc.copy()
+    sc[idx] = 3
+    assert hip.msm_g1(pts, sc) == oracle.msm(pts, sc)
+
+
 def test_srs_eval_degree_check(hip):
     pts = np.tile(np.array([1, 2, 0], np.uint8), 4)
     with pytest.raises(ValueError):
