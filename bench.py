@@ -248,23 +248,25 @@ def cpu_other_baselines(hip):
     with open(os.path.join(ROOT, "tests", "golden", "prove.json")) as f:
         p = json.load(f)["proofs"][0]
     args = (p["gates"], p["copies"], p["wires"], p["chal"], p["rand"], p["secret"], p["srs_n"], p["srs_mode"])
-    reps = 2000
+    reps = 20000
     t0 = time.perf_counter()
     for _ in range(reps):
-        proof = R.prove4(*args)
+        proof = R.prove4_inproc(*args)
     ref_us = (time.perf_counter() - t0) / reps * 1e6
     out["toy_prove_4_gates"] = {"reference_cpu_us": round(ref_us, 2), "matches_golden": proof.hex() == p["proof"]}
     dropin = os.path.join(ROOT, "oracle", "_ref", "libplonkref_dropin.so")
     if os.path.exists(dropin):
         D = Reference(dropin)
-        D.prove4(*args)
+        D.prove4_inproc(*args)
         t0 = time.perf_counter()
         for _ in range(50):
-            dproof = D.prove4(*args)
+            dproof = D.prove4_inproc(*args)
         out["toy_prove_4_gates"]["dropin_gpu_us"] = round((time.perf_counter() - t0) / 50 * 1e6, 1)
         out["toy_prove_4_gates"]["dropin_matches_golden"] = dproof.hex() == p["proof"]
-    out["note"] = ("reference compiled from its own headers (oracle/_ref, gcc -O2), 1 thread; the toy prove is "
-                   "latency-bound on the GPU (about 26 host<->device round trips of tiny ops)")
+    out["note"] = ("reference compiled from its own headers (oracle/_ref, gcc -O2), 1 thread, in-process; the toy "
+                   "prove = srs_create + plonk_new + plonk_prove of src/plonk-test.c, whose drop-in build sends its "
+                   "poly_mul / MSM / poly_divide / poly_eval / matrix ops to the GPU one tiny call at a time "
+                   "(latency-bound: ~100 host<->device round trips)")
     return out
 
 

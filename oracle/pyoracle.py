@@ -230,6 +230,16 @@ class Reference(_Lib):
         n = self.lib.ref_interpolate4(_ptr(_u8(values)), _ptr(out))
         return bytes(out[:n])
 
+    def prove4_inproc(self, gates, copies, wires, chal, rnd, secret=2, srs_n=6, srs_mode=0):
+        """in-process prove (no fork): valid instances only (timing)"""
+        f = self.lib.ref_prove4_inproc
+        f.restype = None
+        f.argtypes = [_u8p, _u8p, _u8p, _u8p, _u8p, C.c_uint8, C.c_size_t, C.c_int, _u8p]
+        out = np.zeros(34, np.uint8)
+        f(_ptr(_u8(gates)), _ptr(_u8(copies)), _ptr(_u8(wires)), _ptr(_u8(chal)), _ptr(_u8(rnd)), secret, srs_n,
+          srs_mode, _ptr(out))
+        return bytes(out)
+
     def prove4(self, gates, copies, wires, chal, rnd, secret=2, srs_n=6, srs_mode=0):
         out = np.zeros(34, np.uint8)
         rc = self.lib.ref_prove4(_ptr(_u8(gates)), _ptr(_u8(copies)), _ptr(_u8(wires)),

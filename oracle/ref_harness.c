@@ -213,6 +213,14 @@ static void prove4_body(const uint8_t *gates, const uint8_t *copies, const uint8
   }
 }
 
+/* in-process (no fork): for timing instances the reference accepts (bench.py's CPU baseline
+ * of the toy circuit: srs_create + plonk_new + plonk_prove, as src/plonk-test.c does) */
+void ref_prove4_inproc(const uint8_t *gates, const uint8_t *copies, const uint8_t *wires,
+                       const uint8_t *chal, const uint8_t *rnd, uint8_t secret, size_t srs_n,
+                       int srs_mode, uint8_t *out) {
+  prove4_body(gates, copies, wires, chal, rnd, secret, srs_n, srs_mode, out);
+}
+
 int ref_prove4(const uint8_t *gates, const uint8_t *copies, const uint8_t *wires,
                const uint8_t *chal, const uint8_t *rnd, uint8_t secret, size_t srs_n,
                int srs_mode, uint8_t *out) {

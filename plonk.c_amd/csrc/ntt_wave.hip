@@ -618,6 +618,9 @@ int wave_plan(int k, int TB, int* Ms) {
 }
 
 // column tables [field][k] (field 0 BabyBear, 1 F29) for the 2-pass plans, k = 13 .. 23
+#ifndef PLK_NTT_COLT_MIN_K
+#define PLK_NTT_COLT_MIN_K 13   // smallest transform using a column table (tuning: larger = lo * hi products)
+#endif
 constexpr int COLT_MIN_K = 13, COLT_MAX_K = 23;
 uint32_t* g_col[2][COLT_MAX_K + 1] = {};
 
@@ -629,7 +632,7 @@ template <class F>
 WTw fwd_wtw(int k) {
   const bool f29 = F::ADIC == f29::TWO_ADICITY;
   WTw w = to_wtw(f29 ? plk_ntt_tables29() : plk_ntt_tables(), false);
-  w.col = (k >= COLT_MIN_K && k <= COLT_MAX_K) ? g_col[f29 ? 1 : 0][k] : nullptr;
+  w.col = (k >= PLK_NTT_COLT_MIN_K && k >= COLT_MIN_K && k <= COLT_MAX_K) ? g_col[f29 ? 1 : 0][k] : nullptr;
   return w;
 }
 
