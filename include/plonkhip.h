@@ -63,7 +63,7 @@ int plk_poly_mul(const uint8_t *a, size_t la, const uint8_t *b, size_t lb, uint8
 
 /* ---- device-resident entry points (bench, multi-GPU, pipelines) ---------------------- */
 
-/* Result record of one MSM, 1152 bytes of device memory.  Zero it once
+/* Result record of one MSM, 2176 bytes of device memory.  Zero it once
  * (plk_msm_result_init); every launch leaves its internal words at zero again, so a record
  * can be reused by the next launch on the same stream.  The arrival words of the blocks of
  * one launch live on separate 128-byte lines (serialised device-scope atomics on one line
@@ -75,8 +75,8 @@ typedef struct {
                           run plk_msm_g1_serial_dev for the reference's exact raw fold */
   uint8_t g1[4];       /* {x, y, infinite, 0} */
   uint32_t pad[27];
-  uint64_t shard[8][16]; /* internal: per-XCD arrival words shard[s][0]: [31:0] sum,
-                            [47:32] ticket, [63:48] bad; one 128-byte line each */
+  uint64_t shard[16][16]; /* internal: arrival words shard[s][0] (two per XCD): [31:0] sum,
+                             [47:32] ticket, [63:48] bad; one 128-byte line each */
 } plk_msm_result_t;
 
 int plk_msm_result_init(plk_msm_result_t *d_res, void *stream);

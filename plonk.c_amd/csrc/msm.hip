@@ -36,7 +36,7 @@
 #endif
 
 __constant__ uint32_t c_ytab[512];             // E[idx], see above
-__constant__ uint8_t c_exp[PLK_GROUP_ORDER * 4];  // EXP[k] = {x, y, inf, 0}
+__constant__ __attribute__((aligned(16))) uint8_t c_exp[PLK_GROUP_ORDER * 4];  // EXP[k] = {x, y, inf, 0}
 __constant__ uint8_t c_inv101[PLK_GF_P];       // a^-1 mod 101 (0 -> 0), for the raw fold
 
 namespace {
@@ -154,6 +154,50 @@ __device__ __forceinline__ uint32_t group_sum(const Group& g, const uint32_t* ta
   return part;                                   // <= 16 * 101 * 255
 }
 
+// Half a group (8 points, 24 B of points + 8 B of scalars) for one thread: the single-MSM
+// form, where every thread has exactly one unit of work and the launch is ONE resident round.
+// The terms are computed after the last word of the half arrives, so halving the work per
+// thread (twice the waves) halves what the last-arriving waves still compute after the stream
+// ends: a single 2^22-point MSM 0.2-0.3 us shorter (tools/msm_single_lab2.hip).
+struct Half {
+  uint2 a0, a1, a2, s;
+};
+__device__ __forceinline__ Half load_half(const uint8_t* pts, const uint8_t* sc, uint64_t u) {
+  const uint2* pp = reinterpret_cast<const uint2*>(pts + 24 * u);   // 8-byte aligned: 48 (u/2) + 24 (u&1)
+  Half h;
+  h.a0 = pp[0];
+  asm volatile("" ::: "memory");
+  h.a1 = pp[1];
+  asm volatile("" ::: "memory");
+  h.a2 = pp[2];
+  asm volatile("" ::: "memory");
+  h.s = *reinterpret_cast<const uint2*>(sc + 8 * u);
+  return h;
+}
+template <int C, int J>
+__device__ __forceinline__ uint32_t half_d(const uint32_t (&w)[12], const uint32_t* tab, uint32_t lane4) {
+  const uint32_t k = point_bytes<J>(w);
+  const uint32_t idx = (k >> 16) & 0x1FFu;
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + ((idx << copy_shift<C>()) | lane4)) - k;
+}
+// d = E - k per point (the log in byte 0 when canonical, >= 256 otherwise); the eight logs are
+// packed two bytes at a time and multiplied by the scalar bytes with v_dot4_u32_u8.
+template <int C>
+__device__ __forceinline__ uint32_t half_sum(const Half& h, const uint32_t* tab, uint32_t lane4, bool& bad) {
+  const uint32_t w[12] = {h.a0.x, h.a0.y, h.a1.x, h.a1.y, h.a2.x, h.a2.y, 0u, 0u, 0u, 0u, 0u, 0u};
+  const uint32_t d0 = half_d<C, 0>(w, tab, lane4), d1 = half_d<C, 1>(w, tab, lane4);
+  const uint32_t d2 = half_d<C, 2>(w, tab, lane4), d3 = half_d<C, 3>(w, tab, lane4);
+  const uint32_t d4 = half_d<C, 4>(w, tab, lane4), d5 = half_d<C, 5>(w, tab, lane4);
+  const uint32_t d6 = half_d<C, 6>(w, tab, lane4), d7 = half_d<C, 7>(w, tab, lane4);
+  bad |= (d0 | d1 | d2 | d3 | d4 | d5 | d6 | d7) >= 256u;
+  // perm selector 0x0C0C0400: byte 0 of the second operand, byte 0 of the first, zeros above
+  const uint32_t lo = __builtin_amdgcn_perm(__builtin_amdgcn_perm(d3, d2, 0x0C0C0400u),
+                                            __builtin_amdgcn_perm(d1, d0, 0x0C0C0400u), 0x05040100u);
+  const uint32_t hi = __builtin_amdgcn_perm(__builtin_amdgcn_perm(d7, d6, 0x0C0C0400u),
+                                            __builtin_amdgcn_perm(d5, d4, 0x0C0C0400u), 0x05040100u);
+  return __builtin_amdgcn_udot4(hi, h.s.y, __builtin_amdgcn_udot4(lo, h.s.x, 0u, false), false);   // <= 8*101*255
+}
+
 }  // namespace
 
 // One launch = a batch of gridDim.y MSMs of n points each (points/scalars of MSM b at
@@ -171,11 +215,12 @@ __device__ __forceinline__ uint32_t group_sum(const Group& g, const uint32_t* ta
 // no fence or re-read needed), re-arms the shard word and adds the shard total to
 // res[b].top the same way; the last shard's finisher writes log / irregular / g1 and
 // re-arms top.  Every word is zero again when the launch ends.
-template <bool ALIGNED, int NT, int G, int COPIES>
+template <bool ALIGNED, int NT, int G, int COPIES, bool HALF>
 __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, uint64_t pstride,
                                                       const uint8_t* sc_base, uint64_t sstride,
                                                       uint64_t n, uint32_t full, PlkMsmResult* res_base) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[TAB_ENTRIES * COPIES];
+  __shared__ uint32_t etab[PLK_GROUP_ORDER];   // EXP words {x, y, inf, 0} for the last finisher
   __shared__ uint32_t wsum[NT / PLK_WAVE];
   __shared__ uint32_t wbad[NT / PLK_WAVE];
   const uint8_t* pts = pts_base + (uint64_t)blockIdx.y * pstride;
@@ -189,9 +234,33 @@ __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, u
   bool bad = false;
   TableFill<NT, COPIES> fill;
   fill.load();                                  // table words first ...
+  // ... with the EXP table (staged in LDS: the last finisher's point lookup is then not a
+  // dependent global load at the very end of the launch, -0.15..0.3 us per single MSM)
+  const uint32_t ev = threadIdx.x < PLK_GROUP_ORDER ? reinterpret_cast<const uint32_t*>(c_exp)[threadIdx.x] : 0u;
 
   const uint64_t ngroups = n >> 4;
-  if (ALIGNED) {
+  if (HALF) {
+    // one resident round of half groups (8 points per thread, units of 24 B + 8 B); `full` is
+    // unused: a thread takes units tid, tid + stride, ... (at most one in the launches that
+    // use this form, see plk_msm_geometry)
+    const uint64_t nunits = ngroups * 2;
+    uint64_t u = tid;
+    Half h{};
+    asm volatile("" ::: "memory");
+    if (u < nunits) h = load_half(pts, sc, u);
+    if (!(PLK_MSM_DIAG & 1)) {
+      fill.store(tab);
+      if (threadIdx.x < PLK_GROUP_ORDER) etab[threadIdx.x] = ev;
+      __syncthreads();
+    }
+    if (u < nunits) acc = half_sum<COPIES>(h, tab, lane4, bad) % PLK_GROUP_ORDER;
+    for (u += stride; u < nunits; u += stride) acc += half_sum<COPIES>(load_half(pts, sc, u), tab, lane4, bad) % PLK_GROUP_ORDER;
+    const uint64_t base = ngroups << 4;
+    if (blockIdx.x == 0 && base + threadIdx.x < n) {
+      const uint64_t i = base + threadIdx.x;
+      acc += point_term<COPIES>(encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), sc[i], tab, lane4, bad);
+    }
+  } else if (ALIGNED) {
     // 16 points per thread-step: 48 B of points (3 x dwordx4) + 16 B of scalars (1 x dwordx4)
     const uint4* p4 = reinterpret_cast<const uint4*>(pts);
     const uint4* s4 = reinterpret_cast<const uint4*>(sc);
@@ -216,6 +285,7 @@ __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, u
       }
       if (!(PLK_MSM_DIAG & 1)) {
         fill.store(tab);                              // ... LDS fill waits for the table words only
+        if (threadIdx.x < PLK_GROUP_ORDER) etab[threadIdx.x] = ev;
         __syncthreads();
       }
       uint32_t part = 0;
@@ -225,6 +295,7 @@ __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, u
       g += span;
     } else if (!(PLK_MSM_DIAG & 1)) {
       fill.store(tab);
+      if (threadIdx.x < PLK_GROUP_ORDER) etab[threadIdx.x] = ev;
       __syncthreads();
     }
     for (uint32_t it = 1; it < full; it++, g += span) {
@@ -254,6 +325,7 @@ __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, u
     }
   } else {
     fill.store(tab);
+    if (threadIdx.x < PLK_GROUP_ORDER) etab[threadIdx.x] = ev;
     __syncthreads();
     for (uint64_t i = tid; i < n; i += stride) {
       acc += point_term<COPIES>(encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), sc[i], tab, lane4, bad);
@@ -305,10 +377,7 @@ __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, u
   const uint32_t lg = (uint32_t)(tot & 0xFFFFFFFFull) % PLK_GROUP_ORDER;
   res->log = lg;
   res->irregular = (uint32_t)(tot >> 48);
-  res->g1[0] = c_exp[4 * lg + 0];
-  res->g1[1] = c_exp[4 * lg + 1];
-  res->g1[2] = c_exp[4 * lg + 2];
-  res->g1[3] = 0;
+  *reinterpret_cast<uint32_t*>(res->g1) = etab[lg];
   atomicExch(&res->top, 0ull);
 }
 
@@ -469,13 +538,15 @@ int env_int(const char* name) {
 }
 }  // namespace
 
-void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* gpt, int* copies) {
-  static int env_threads = -1, env_blocks = -1, env_g = -1, env_c = -1;
+void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* gpt, int* copies, int* half) {
+  static int env_threads = -1, env_blocks = -1, env_g = -1, env_c = -1, env_half = -1;
   if (env_threads < 0) {
     env_threads = env_int("PLK_MSM_THREADS");
     env_blocks = env_int("PLK_MSM_MAX_BLOCKS");
     env_g = env_int("PLK_MSM_G");
     env_c = env_int("PLK_MSM_COPIES");
+    const char* e = getenv("PLK_MSM_HALF");
+    env_half = e ? atoi(e) : 1;
   }
   const uint64_t groups = n >> 4;
   int th = groups >= 64ull * 1024 ? 512 : 256;
@@ -499,10 +570,20 @@ void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* gpt
   // critical path (its words are loaded before the points); PLK_MSM_COPIES=1 for tuning
   int c = 8;
   if (env_c == 1 || env_c == 8) c = env_c;
+  // a single MSM whose threads have at most one group each (one resident round): half groups
+  // on twice the blocks, one table copy (lab: the smaller fill wins there, 0.05-0.2 us)
+  int hf = 0;
+  if (env_half && batch == 1 && groups <= b * (uint64_t)th && 2 * b <= 8ull * 65535ull) {
+    hf = 1;
+    b *= 2;
+    g = 1;
+    c = env_c == 8 ? 8 : 1;
+  }
   *threads = th;
   *blocks = (int)b;
   if (gpt) *gpt = g;
   if (copies) *copies = c;
+  if (half) *half = hf;
 }
 
 namespace {
@@ -513,16 +594,19 @@ void go_g(int g, dim3 grid, hipStream_t st, const uint8_t* p, uint64_t ps, const
   const uint64_t span = (uint64_t)grid.x * T * g;
   const uint32_t full = (uint32_t)((n >> 4) / span);
   if (g == 1)
-    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 1, C>), grid, dim3(T), 0, st, p, ps, s, ss, n, full, r);
+    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 1, C, false>), grid, dim3(T), 0, st, p, ps, s, ss, n, full, r);
   else if (g == 2)
-    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 2, C>), grid, dim3(T), 0, st, p, ps, s, ss, n, full, r);
+    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 2, C, false>), grid, dim3(T), 0, st, p, ps, s, ss, n, full, r);
   else
-    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 4, C>), grid, dim3(T), 0, st, p, ps, s, ss, n, full, r);
+    hipLaunchKernelGGL((msm_dlog_kernel<A, T, 4, C, false>), grid, dim3(T), 0, st, p, ps, s, ss, n, full, r);
 }
 template <int T>
-void go_t(bool aligned, int g, int c, dim3 grid, hipStream_t st, const uint8_t* p, uint64_t ps, const uint8_t* s,
-          uint64_t ss, uint64_t n, PlkMsmResult* r) {
-  if (aligned) {
+void go_t(bool aligned, int g, int c, int half, dim3 grid, hipStream_t st, const uint8_t* p, uint64_t ps,
+          const uint8_t* s, uint64_t ss, uint64_t n, PlkMsmResult* r) {
+  if (aligned && half) {
+    if (c == 1) hipLaunchKernelGGL((msm_dlog_kernel<true, T, 1, 1, true>), grid, dim3(T), 0, st, p, ps, s, ss, n, 0u, r);
+    else hipLaunchKernelGGL((msm_dlog_kernel<true, T, 1, 8, true>), grid, dim3(T), 0, st, p, ps, s, ss, n, 0u, r);
+  } else if (aligned) {
     if (c == 1) go_g<true, T, 1>(g, grid, st, p, ps, s, ss, n, r);
     else go_g<true, T, 8>(g, grid, st, p, ps, s, ss, n, r);
   } else {
@@ -539,14 +623,18 @@ int plk_msm_batch_launch(const uint8_t* d_pts, uint64_t pstride, const uint8_t* 
     plk_set_error("plk_msm batch %d too large", batch);
     return PLK_ERR_RANGE;
   }
-  int threads, blocks, g, c;
-  plk_msm_geometry(n, batch, &threads, &blocks, &g, &c);
+  int threads, blocks, g, c, half;
+  plk_msm_geometry(n, batch, &threads, &blocks, &g, &c, &half);
   const bool aligned = ((uintptr_t)d_pts % 16 == 0) && ((uintptr_t)d_sc % 16 == 0) &&
                        (batch == 1 || (pstride % 16 == 0 && sstride % 16 == 0));
+  if (!aligned && half) {   // the byte-wise form: the plain plan
+    half = 0;
+    blocks /= 2;
+  }
   const dim3 grid(blocks, batch);
-  if (threads == 1024) go_t<1024>(aligned, g, c, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
-  else if (threads == 512) go_t<512>(aligned, g, c, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
-  else go_t<256>(aligned, g, c, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
+  if (threads == 1024) go_t<1024>(aligned, g, c, half, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
+  else if (threads == 512) go_t<512>(aligned, g, c, half, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
+  else go_t<256>(aligned, g, c, half, grid, st, d_pts, pstride, d_sc, sstride, n, d_res);
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }

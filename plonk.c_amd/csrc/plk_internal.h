@@ -6,11 +6,11 @@
 #include "../../include/plonkhip.h"
 
 typedef plk_msm_result_t PlkMsmResult;
-static_assert(sizeof(plk_msm_result_t) == 1152, "MSM result record is 1152 bytes");
+static_assert(sizeof(plk_msm_result_t) == 2176, "MSM result record is 2176 bytes");
 static_assert(offsetof(plk_msm_result_t, log) == 8 && offsetof(plk_msm_result_t, irregular) == 12 &&
                   offsetof(plk_msm_result_t, g1) == 16 && offsetof(plk_msm_result_t, shard) == 128,
               "offsets used by plonkhip/__init__.py");
-#define PLK_MSM_SHARDS 8      // ticket shards per MSM record (one per XCD)
+#define PLK_MSM_SHARDS 16     // ticket shards per MSM record (two per XCD)
 
 #define PLK_NTT_SMALL_LOG 13   // universal small twiddle table covers tiles up to 2^13 rows
 #define PLK_SMALL_LOG 12       // poly_mul with N <= 2^12: one workgroup does everything
@@ -31,7 +31,8 @@ void plk_ctx_release(void);
 
 // msm.hip
 int plk_msm_upload_tables(const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101);
-void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* groups_per_thread, int* copies);
+void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* groups_per_thread, int* copies,
+                      int* half);
 int plk_msm_batch_launch(const uint8_t* d_pts, uint64_t pstride, const uint8_t* d_sc, uint64_t sstride, uint64_t n,
                          int batch, PlkMsmResult* d_res, hipStream_t st);
 int plk_msm_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsmResult* d_res, hipStream_t st);

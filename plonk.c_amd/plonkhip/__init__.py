@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("PLK_LIB") or os.path.join(PKG_DIR, "libplonkhip.so") 
 HEADER_PATH = os.path.join(REPO_DIR, "include", "plonkhip.h")
 
 PLK_OK, PLK_ERR_HIP, PLK_ERR_ARG, PLK_ERR_RANGE, PLK_ERR_NODEV, PLK_ERR_NOMEM = range(6)
-MSM_RESULT_BYTES = 1152
+MSM_RESULT_BYTES = 2176
 MSM_LOG_OFFSET, MSM_IRREGULAR_OFFSET, MSM_G1_OFFSET = 8, 12, 16
 
 _u8p = C.POINTER(C.c_uint8)

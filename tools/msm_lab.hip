@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
     const int B = batches[bi];
     const int L = B == 40 ? 8 : (B == 8 ? 20 : 80);
     int th, bl, g;
-    plk_msm_geometry(n, B, &th, &bl, &g, nullptr);
+    plk_msm_geometry(n, B, &th, &bl, &g, nullptr, nullptr);
     float best = 1e30f;
     for (int rep = 0; rep < 3; rep++) {
       CK(hipEventRecord(a, st));

@@ -325,17 +325,43 @@ int main(int argc, char** argv) {
 #define LIB(NT, G, C, B)                                                                       \
   vs.push_back({"lib<" #NT "," #G "," #C "> x" #B, [=](int s) {                               \
                   int th, bl, g, c;                                                          \
-                  plk_msm_geometry(n, B, &th, &bl, &g, &c);                                  \
-                  hipLaunchKernelGGL((msm_dlog_kernel<true, NT, G, C>), dim3(bl, B), dim3(NT), 0, st, \
+                  plk_msm_geometry(n, B, &th, &bl, &g, &c, nullptr);                                 \
+                  hipLaunchKernelGGL((msm_dlog_kernel<true, NT, G, C, false>), dim3(bl, B), dim3(NT), 0, st, \
                                      pts + 3 * n * s, 3 * n, sc + n * s, n, n,                \
                                      (uint32_t)((n >> 4) / ((uint64_t)bl * NT * G)), lres);   \
                 }, B})
 #define LIBG(NT, G, C, BL)                                                                     \
   vs.push_back({"lib<" #NT "," #G "," #C "> grid " #BL, [=](int s) {                         \
-                  hipLaunchKernelGGL((msm_dlog_kernel<true, NT, G, C>), dim3(BL, 1), dim3(NT), 0, st, \
+                  hipLaunchKernelGGL((msm_dlog_kernel<true, NT, G, C, false>), dim3(BL, 1), dim3(NT), 0, st, \
                                      pts + 3 * n * s, 3 * n, sc + n * s, n, n,                \
                                      (uint32_t)((n >> 4) / ((uint64_t)BL * NT * G)), lres);   \
                 }, 1})
+  const int set = argc > 5 ? atoi(argv[5]) : 0;
+  if (set == 1) {   // geometry and cost-ladder exploration
+    raw("empty_256x256", k_empty<256>, 256, 256);
+    raw("empty_512x256", k_empty<512>, 512, 256);
+    raw("empty_1024x256", k_empty<1024>, 1024, 256);
+    raw("empty_512x512", k_empty<512>, 512, 512);
+    raw("readg_256_g4_x256", k_readg<256, 4>, 256, (int)(ng / 1024));
+    raw("readg_256_g8_x128", k_readg<256, 8>, 256, (int)(ng / 2048));
+    raw("readg_512_g2_x256", k_readg<512, 2>, 512, (int)(ng / 1024));
+    raw("readg_512_g4_x128", k_readg<512, 4>, 512, (int)(ng / 2048));
+    raw("readg_1024_g1_x256", k_readg<1024, 1>, 1024, (int)(ng / 1024));
+    raw("readg_512_g1_x512", k_readg<512, 1>, 512, (int)(ng / 512));
+    raw("L0_512_c1", k_ladder<512, 1, 0, 1>, 512, (int)(ng / 512));
+    raw("L1_512_c1", k_ladder<512, 1, 1, 1>, 512, (int)(ng / 512));
+    raw("L2_512_c1", k_ladder<512, 1, 2, 1>, 512, (int)(ng / 512));
+    raw("L3_512_c1", k_ladder<512, 1, 3, 1>, 512, (int)(ng / 512));
+    raw("L4_512_c1", k_ladder<512, 1, 4, 1>, 512, (int)(ng / 512));
+    raw("L5_512_c1", k_ladder<512, 1, 5, 1>, 512, (int)(ng / 512));
+    raw("L6_512_c1", k_ladder<512, 1, 6, 1>, 512, (int)(ng / 512));
+    raw("L0_256_g4_c1", k_ladder<256, 1, 0, 4>, 256, (int)(ng / 1024));
+    raw("L1_256_g4_c1", k_ladder<256, 1, 1, 4>, 256, (int)(ng / 1024));
+    raw("L2_256_g4_c1", k_ladder<256, 1, 2, 4>, 256, (int)(ng / 1024));
+    raw("L3_256_g4_c1", k_ladder<256, 1, 3, 4>, 256, (int)(ng / 1024));
+    raw("L6_256_g4_c1", k_ladder<256, 1, 6, 4>, 256, (int)(ng / 1024));
+  }
+  if (set == 0) {
   raw("empty_512x512", k_empty<512>, 512, (int)(ng / 512));
   raw("ladder0_read", k_ladder<512, 1, 0>, 512, (int)(ng / 512));
   raw("ladder6_g1_c8", k_ladder<512, 8, 6, 1>, 512, (int)(ng / 512));
@@ -347,6 +373,7 @@ int main(int argc, char** argv) {
   LIBG(1024, 1, 8, 256);
   LIB(512, 2, 8, 40);
   LIB(512, 2, 1, 40);
+  }
   const int rounds = argc > 4 ? atoi(argv[4]) : 1;
   for (int round = 0; round < rounds; round++)
   for (const V& v : vs) {
