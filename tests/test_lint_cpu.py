@@ -1,0 +1,37 @@
+"""Source guard for a gfx950 compiler miscompile (ROCm 7.2 clang 22, pinned by tools/swar_probe.hip).
+
+The AMDGPU dot4 combine rewrites an add chain of products c_t * (w_t & 0x00FF00FF) -- two byte
+lanes per 32-bit word (SWAR) -- into v_dot4_u32_u8 over byte 0 only, silently dropping the upper
+lane's terms (probe: 1,973,430 of 4,194,304 bytes wrong; the same arithmetic with the masked word
+made opaque by an empty asm is exact).  Products of genuine single bytes (x & 0xFF), which every
+kept kernel uses, are what the instruction computes and stay exact.  This test keeps multi-byte
+lane masks out of multiplicative expressions in the device sources."""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "plonk.c_amd", "csrc")
+
+# a hex constant with 0xFF bytes separated by zero bytes (0x00FF00FF, 0xFF00FF): byte lanes.  Contiguous
+# masks (0xFF, 0xFFFF, 0xFFFF0000) select one field and do not match.
+LANE_MASK = re.compile(r"0x0*ff(?:00)+ff(?:00|ff)*u?\b", re.IGNORECASE)
+
+
+def test_no_swar_lane_masks_in_products():
+    hits = []
+    for name in sorted(os.listdir(CSRC)):
+        if not name.endswith((".hip", ".h")):
+            continue
+        with open(os.path.join(CSRC, name)) as f:
+            for no, line in enumerate(f, 1):
+                code = line.split("//")[0]
+                if LANE_MASK.search(code) and "*" in code:
+                    hits.append("%s:%d: %s" % (name, no, line.strip()))
+    assert not hits, "SWAR lane mask in a product (see tools/swar_probe.hip):\n" + "\n".join(hits)
+
+
+def test_lane_mask_pattern():
+    assert LANE_MASK.search("lo += c * (w & 0x00FF00FFu);")
+    assert LANE_MASK.search("x * (y & 0xff00ff)")
+    assert not LANE_MASK.search("(d & 0xFFu) * c")
+    assert not LANE_MASK.search("v & 0xFFFFu")

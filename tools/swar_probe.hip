@@ -75,6 +75,26 @@ __global__ void probe(int form, const uint32_t* words, const uint8_t* cfs, uint8
   else lincomb(form, w, cf, out + 4 * (size_t)i);
 }
 
+// form 4, in a kernel of its own (adding it to probe() changes how the forms above compile):
+// form 1 with the masked words made opaque to the instruction combiner
+__global__ void probe_opaque(const uint32_t* words, const uint8_t* cfs, uint8_t* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t lo = 0, hi = 0;
+  for (int t = 0; t < NT; t++) {
+    const uint32_t w = words[(size_t)i * NT + t];
+    uint32_t ml = w & 0x00FF00FFu, mh = (w >> 8) & 0x00FF00FFu;
+    asm volatile("" : "+v"(ml), "+v"(mh));
+    const uint32_t c = cfs[(size_t)i * NT + t];
+    lo += c * ml;
+    hi += c * mh;
+  }
+  out[4 * (size_t)i + 0] = (uint8_t)((lo & 0xFFFFu) % 17u);
+  out[4 * (size_t)i + 1] = (uint8_t)((hi & 0xFFFFu) % 17u);
+  out[4 * (size_t)i + 2] = (uint8_t)((lo >> 16) % 17u);
+  out[4 * (size_t)i + 3] = (uint8_t)((hi >> 16) % 17u);
+}
+
 int main() {
   const int n = 1 << 20;
   uint32_t* hw = (uint32_t*)malloc(sizeof(uint32_t) * n * NT);
@@ -96,9 +116,10 @@ int main() {
   CK(hipMemcpy(dw, hw, sizeof(uint32_t) * n * NT, hipMemcpyHostToDevice));
   CK(hipMemcpy(dc, hc, n * NT, hipMemcpyHostToDevice));
   int bad_total = 0;
-  for (int form = 0; form < 4; form++) {
+  for (int form = 0; form < 5; form++) {
     CK(hipMemset(dout, 0xAB, 4 * (size_t)n));
-    hipLaunchKernelGGL(probe, dim3(n / 256), dim3(256), 0, 0, form, dw, dc, dout, n);
+    if (form == 4) hipLaunchKernelGGL(probe_opaque, dim3(n / 256), dim3(256), 0, 0, dw, dc, dout, n);
+    else hipLaunchKernelGGL(probe, dim3(n / 256), dim3(256), 0, 0, form, dw, dc, dout, n);
     CK(hipGetLastError());
     CK(hipMemcpy(ho, dout, 4 * (size_t)n, hipMemcpyDeviceToHost));
     int bad = 0;
