@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Compute roofline of the NTT kernels: butterflies per launch / duration / the measured
+butterfly peak (tools/bfly_peak.hip: the engine's own butterfly formulas in registers, no memory,
+full occupancy -- the integer-VALU roof of this arithmetic on this chip).
+
+    python tools/ntt_roofline.py <run_results.db> <bfly_peak.json> [--prove | --all] [--json out]
+
+--prove: the kernels of the LAST prove call of the trace (tools/prove_bench.py; calls end with
+trim_pack_kernel); --all (default): every wt_* dispatch, aggregated per (kernel, grid).
+
+Butterflies counted (the algorithmic work, radix-2 count):
+  wt_fwd/wt_inv_kernel<TB, R, M, ...>: blocks x 2^(TB-1) x M  (blocks = grid_x / workgroup x grid_y;
+      the high passes' one column multiply per element is NOT counted, so the fraction is a lower
+      bound; sum-group members skipped by the inverse pass are counted, an upper bound there)
+  wt_center_kernel<TB, R, F>: (job, tile) items x 2^(TB-1) x TB x 3 (two forward transforms and one
+      inverse per item); the items are the next inverse pass's blocks (same batch)
+Peak: F29 / BabyBear DIF for forward passes, DIT for inverse, (2 DIF + 1 DIT) / 3 for the center."""
+import json
+import re
+import sqlite3
+import sys
+from collections import defaultdict
+
+PAT = re.compile(r"wt_(fwd|inv|center)_kernel<(\d+), (\d+)(?:, (\d+))?.*?(F29|FBB)")
+
+
+def parse(name):
+    m = PAT.search(name.replace("(anonymous namespace)::", ""))
+    if not m:
+        return None
+    kind, tb, _r, mm, field = m.groups()
+    return kind, int(tb), int(mm) if mm else int(tb), field
+
+
+def peak(kind, field, pk):
+    f = "f29" if field == "F29" else "bb"
+    dif, dit = pk[f + "_dif_Gbfly_s"] * 1e9, pk[f + "_dit_Gbfly_s"] * 1e9
+    if kind == "fwd":
+        return dif
+    if kind == "inv":
+        return dit
+    return 3.0 / (2.0 / dif + 1.0 / dit)
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    db, pk_path = args[0], args[1]
+    out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
+    with open(pk_path) as f:
+        pk = json.loads([l for l in f if l.startswith("{")][0])
+    rows = list(sqlite3.connect(db).execute(
+        "select name, grid_x, grid_y, workgroup_x, duration, start from kernels order by start"))
+    if "--prove" in sys.argv:
+        idx = [i for i, r in enumerate(rows) if "trim_pack" in r[0]]
+        rows = rows[idx[-2] + 1:idx[-1] + 1]
+    disp = []
+    for i, (name, gx, gy, wx, dur, _) in enumerate(rows):
+        p = parse(name)
+        if not p:
+            continue
+        kind, tb, mm, field = p
+        if kind == "center":
+            nxt = next((r for r in rows[i + 1:] if parse(r[0]) and parse(r[0])[0] == "inv"), None)
+            if nxt is None:
+                continue
+            items = (nxt[1] // nxt[3]) * nxt[2]
+            bfly = items * (1 << (tb - 1)) * tb * 3
+        else:
+            bfly = (gx // wx) * gy * (1 << (tb - 1)) * mm
+        disp.append((name.replace("(anonymous namespace)::", "").split("(")[0], gx, gy, kind, field, bfly, dur / 1e3))
+    agg = defaultdict(lambda: [0, 0, 0.0, None, None])
+    for name, gx, gy, kind, field, bfly, us in disp:
+        a = agg[(name, gx, gy)]
+        a[0] += 1
+        a[1] += bfly
+        a[2] += us
+        a[3], a[4] = kind, field
+    res = []
+    print("# butterfly roofline (peak: %s)" % pk_path)
+    print("%-58s %-14s %5s %10s %12s %10s %6s" % ("kernel", "grid", "calls", "avg_us", "Mbfly/launch", "Gbfly/s", "frac"))
+    tot_b = tot_t = tot_peak_t = 0.0
+    for (name, gx, gy), (calls, bfly, us, kind, field) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
+        rate = bfly / (us * 1e-6)
+        pkr = peak(kind, field, pk)
+        frac = rate / pkr
+        tot_b += bfly
+        tot_t += us
+        tot_peak_t += bfly / pkr * 1e6
+        res.append({"kernel": name, "grid": [gx, gy], "calls": calls, "avg_us": round(us / calls, 2),
+                    "bfly_per_launch": bfly // calls, "Gbfly_s": round(rate / 1e9, 1),
+                    "peak_Gbfly_s": round(pkr / 1e9, 1), "frac": round(frac, 3)})
+        print("%-58s %-14s %5d %10.2f %12.2f %10.1f %6.3f" % (name[:58], "(%d,%d)" % (gx, gy), calls, us / calls,
+                                                          bfly / calls / 1e6, rate / 1e9, frac))
+    if tot_t:
+        print("all NTT kernels: %.1f us, butterfly-roof time %.1f us -> frac %.3f" % (tot_t, tot_peak_t,
+                                                                                  tot_peak_t / tot_t))
+    if out_json:
+        with open(out_json, "w") as f:
+            json.dump({"peak": pk, "kernels": res, "total_us": round(tot_t, 1),
+                       "roof_us": round(tot_peak_t, 1), "frac": round(tot_peak_t / tot_t, 3) if tot_t else None},
+                      f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
