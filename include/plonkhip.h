@@ -57,7 +57,10 @@ int plk_msm_g1(const uint8_t *points, const uint8_t *scalars, size_t n, uint8_t 
 /* Replaces the body of poly_mul (src/poly.h:106-122):
  *   out[0 .. la+lb-1) = a * b over GF(17); *out_len = length after the reference's
  *   trailing-zero trim (src/poly.h:20-38), >= 1.  out must hold la+lb-1 bytes.
- *   la == 0 or lb == 0 mirrors the reference: *out_len = (la+lb-1 > 0), out[0] = 0. */
+ *   la == 0 or lb == 0 mirrors the reference: *out_len = (la+lb-1 > 0), out[0] = 0.
+ *   Any shape with la + lb - 1 < 2^32: products beyond one transform's exact range
+ *   (min(la, lb) >= 7,864,320 or more than 2^27 output coefficients) run as in-range piece
+ *   products accumulated mod 17 (the _dev form then needs plk_poly_mul_workspace bytes). */
 int plk_poly_mul(const uint8_t *a, size_t la, const uint8_t *b, size_t lb, uint8_t *out,
                  size_t *out_len);
 

@@ -29,6 +29,7 @@
 #include "plk_device.h"
 #include "plk_internal.h"
 
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -540,8 +541,34 @@ bool plk_poly_mul_summable(uint64_t la, uint64_t lb) {
   return la && lb && mn > PLK_DIRECT_MAX && product_plan(la, lb, nullptr) > PLK_SMALL_LOG;
 }
 
+// Products outside one transform's exact range (min(la, lb) * 256 >= the BabyBear prime, i.e.
+// min >= 7,864,320, or a transform above 2^27 points) -- sizes the reference computes with its
+// schoolbook loop -- run BLOCKED: the longer operand in pieces of PLK_BLK_L, the shorter in
+// pieces of PLK_BLK_S coefficients, every piece product an in-range F29 product of a 2^26-point
+// transform, accumulated mod 17 into the zeroed output at the pieces' offset sum.
+// PLK_POLY_BLOCK=L,S (host env) forces the blocked path with smaller pieces (tests).
+static uint64_t PLK_BLK_S = 3670016;                    // F29's exact range: 128 S < p
+static uint64_t PLK_BLK_L = (1ull << 26) - 3670016 + 1;  // L + S - 1 = 2^26 (no wrap)
+static bool g_blk_forced = false;
+static void blk_env() {   // read on every call (tests switch it within one process)
+  const char* e = getenv("PLK_POLY_BLOCK");
+  unsigned long long l = 0, s = 0;
+  g_blk_forced = e && sscanf(e, "%llu,%llu", &l, &s) == 2 && l >= 33 && s >= 33 && s <= 3670016 &&
+                 l <= (1ull << 26) - 3670016 + 1;
+  PLK_BLK_L = g_blk_forced ? l : (1ull << 26) - 3670016 + 1;
+  PLK_BLK_S = g_blk_forced ? s : 3670016;
+}
+static bool blocked_shape(uint64_t la, uint64_t lb) {
+  blk_env();
+  const uint64_t mn = la < lb ? la : lb, mx = la < lb ? lb : la;
+  if (g_blk_forced) return mn > PLK_BLK_S || mx > PLK_BLK_L;
+  return mn * 256 >= bb::P || product_plan(la, lb, nullptr) > bb::TWO_ADICITY;
+}
+static size_t blocked_ws(uint64_t la, uint64_t lb);
+
 size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb) {
   if (la == 0 || lb == 0) return 0;
+  if (blocked_shape(la, lb)) return blocked_ws(la, lb);
   const int k = product_plan(la, lb, nullptr);
   if ((la < lb ? la : lb) <= PLK_DIRECT_MAX || k <= PLK_SMALL_LOG) return 0;
   return (size_t)2 * 4 * (1ull << k);
@@ -646,6 +673,53 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
   return plk_wave_poly_mul_batch_launch(w, m, k, use29 ? 1 : 0, ninv, st);
 }
 
+// out[off + t] = (out[off + t] + part[t]) mod 17, t < len (a piece product of the blocked path)
+__global__ __launch_bounds__(256) void acc17_kernel(uint8_t* __restrict__ out, const uint8_t* __restrict__ part,
+                                                    uint64_t len) {
+  for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < len; t += (uint64_t)gridDim.x * 256)
+    out[t] = (uint8_t)((out[t] + part[t]) % 17u);
+}
+
+static uint64_t align256(uint64_t v) { return (v + 255) & ~255ull; }
+// workspace of the blocked path: one piece product's bytes + the largest piece's own workspace
+static size_t blocked_ws(uint64_t la, uint64_t lb) {
+  const uint64_t mn = la < lb ? la : lb, mx = la < lb ? lb : la;
+  const uint64_t pl = mx < PLK_BLK_L ? mx : PLK_BLK_L, ps = mn < PLK_BLK_S ? mn : PLK_BLK_S;
+  return (size_t)align256(pl + ps - 1) + plk_poly_mul_workspace_bytes(pl, ps);
+}
+
+int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
+                        uint32_t* d_nz, void* d_work, hipStream_t st);
+static int blocked_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
+                          uint32_t* d_nz, void* d_work, hipStream_t st) {
+  if (!d_work) {
+    plk_set_error("poly_mul: %llu x %llu needs a workspace (plk_poly_mul_workspace)", (unsigned long long)la,
+                  (unsigned long long)lb);
+    return PLK_ERR_ARG;
+  }
+  const bool aL = la >= lb;
+  const uint8_t* L = aL ? d_a : d_b;
+  const uint8_t* S = aL ? d_b : d_a;
+  const uint64_t lL = aL ? la : lb, lS = aL ? lb : la, rl = la + lb - 1;
+  const uint64_t pl = lL < PLK_BLK_L ? lL : PLK_BLK_L, ps = lS < PLK_BLK_S ? lS : PLK_BLK_S;
+  uint8_t* part = (uint8_t*)d_work;
+  void* pwork = part + align256(pl + ps - 1);
+  PLK_HIP(hipMemsetAsync(d_out, 0, rl, st));
+  for (uint64_t i = 0; i < lL; i += PLK_BLK_L)
+    for (uint64_t j = 0; j < lS; j += PLK_BLK_S) {
+      const uint64_t li = lL - i < PLK_BLK_L ? lL - i : PLK_BLK_L, lj = lS - j < PLK_BLK_S ? lS - j : PLK_BLK_S;
+      int rc = plk_poly_mul_launch(L + i, li, S + j, lj, part, nullptr, pwork, st);
+      if (rc) return rc;
+      const uint64_t len = li + lj - 1, blocks = (len + 255) / 256;
+      hipLaunchKernelGGL(acc17_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, st,
+                         d_out + i + j, part, len);
+      PLK_HIP(hipGetLastError());
+    }
+  if (d_nz) hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d_out, rl, d_nz);
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
 // d_out must hold la+lb-1 bytes; *d_nz (if not NULL) receives the trimmed length (0 means "all zero" ->
 // the caller reports length 1).
 int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
@@ -656,11 +730,12 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
   }
   const uint64_t rl = la + lb - 1;
   const uint64_t mn = la < lb ? la : lb;
-  if (mn * 256 >= bb::P || rl >= (1ull << 32)) {
-    plk_set_error("poly_mul: %llu x %llu outside the exact range (min(la, lb) * 256 < %u, la + lb - 1 < 2^32)",
-                  (unsigned long long)la, (unsigned long long)lb, bb::P);
+  if (rl >= (1ull << 32)) {   // (the trimmed length is a 32-bit word)
+    plk_set_error("poly_mul: %llu x %llu: la + lb - 1 must be < 2^32", (unsigned long long)la,
+                  (unsigned long long)lb);
     return PLK_ERR_RANGE;
   }
+  if (blocked_shape(la, lb)) return blocked_launch(d_a, la, d_b, lb, d_out, d_nz, d_work, st);
   if (mn <= PLK_DIRECT_MAX) {
     const uint8_t* lg = la >= lb ? d_a : d_b;
     const uint8_t* sh = la >= lb ? d_b : d_a;

@@ -232,3 +232,62 @@ def test_batch_small_workspace_and_bad_groups(hip, oracle):
     assert len(outs[0]) == len(polys[0]) + len(polys[1]) - 1
     with pytest.raises(Exception, match="does not follow"):
         run([(2, 3, 0), (0, 1, 1)], 2 * one)              # shape differs from the preceding job
+
+
+# ---- blocked products: shapes beyond one transform's exact range --------------------------
+# (min(la, lb) * 256 >= the BabyBear prime, or more than 2^27 output coefficients): the
+# reference just runs its schoolbook loop; here they run as in-range piece products
+# accumulated mod 17 (ntt.hip blocked_launch).
+def _eval17(c):
+    """c(x) mod 17 at x = 0..16 (x^i mod 17 has period 16 for x != 0)"""
+    c = np.frombuffer(c, np.uint8) if isinstance(c, (bytes, bytearray)) else c
+    c = c.astype(np.int64)
+    s = np.concatenate([c, np.zeros((-len(c)) % 16, np.int64)]).reshape(-1, 16).sum(axis=0) % 17
+    return [int(c[0] % 17)] + [int((s * np.array([pow(x, r, 17) for r in range(16)])).sum() % 17)
+                               for x in range(1, 17)]
+
+
+@pytest.mark.parametrize("la,lb", [(20000, 15000), (12345, 999), (50000, 50001), (3001, 7000)])
+def test_blocked_forced_vs_oracle(hip, oracle, monkeypatch, la, lb):
+    """The blocked path with small pieces (PLK_POLY_BLOCK=L,S) against the oracle's NTT."""
+    monkeypatch.setenv("PLK_POLY_BLOCK", "3001,1000")
+    a, b = gen.poly_inputs(77 + la, la, lb)
+    assert hip.poly_mul(a, b) == oracle.poly_mul_ntt(a, b)
+
+
+def test_blocked_forced_device_api(hip, oracle, monkeypatch):
+    import torch
+    monkeypatch.setenv("PLK_POLY_BLOCK", "4096,513")
+    la, lb = 30000, 2100
+    a, b = gen.poly_inputs(5, la, lb)
+    dev = torch.device("cuda:0")
+    da, db = torch.from_numpy(np.frombuffer(a, np.uint8).copy()).to(dev), torch.from_numpy(np.frombuffer(b, np.uint8).copy()).to(dev)
+    out = torch.full((la + lb - 1,), 0xEE, dtype=torch.uint8, device=dev)
+    nz = torch.zeros(4, dtype=torch.int32, device=dev)
+    work = torch.zeros(max(16, hip.poly_mul_workspace(la, lb)), dtype=torch.uint8, device=dev)
+    hip.poly_mul_dev(da, la, db, lb, out, nz, work, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    n = int(nz[0].item()) or 1
+    assert bytes(out[:n].cpu().numpy()) == oracle.poly_mul_ntt(a, b)
+
+
+def test_blocked_beyond_babybear_range(hip, oracle):
+    """8,000,000 x 8,000,000 (min * 256 >= 15 2^27 + 1: no single transform is exact): the
+    product at all 17 points of GF(17) equals a(x) b(x), and the lowest / highest 3000
+    coefficients equal the oracle's products of the operands' first / last 3000 coefficients
+    (they depend on nothing else).  Parity unpinned by the reference at this size (its
+    schoolbook loop would take days); the checks are size-independent properties."""
+    la = lb = 8_000_000
+    a, b = gen.poly_inputs(8008, la, lb)
+    got = hip.poly_mul(a, b)
+    rl = la + lb - 1
+    full = np.zeros(rl, np.uint8)
+    full[:len(got)] = np.frombuffer(got, np.uint8)
+    ea, eb, ec = _eval17(a), _eval17(b), _eval17(full)
+    assert ec == [(x * y) % 17 for x, y in zip(ea, eb)]
+    t = 3000
+    lo = np.frombuffer(oracle.poly_mul_ntt(a[:t], b[:t]), np.uint8)
+    assert np.array_equal(full[:t], np.pad(lo, (0, max(0, t - len(lo))))[:t])
+    hi = np.frombuffer(oracle.poly_mul_ntt(a[-t:], b[-t:]), np.uint8)
+    hi = np.pad(hi, (0, 2 * t - 1 - len(hi)))
+    assert np.array_equal(full[rl - t:], hi[t - 1:])
