@@ -33,7 +33,8 @@
 #include <algorithm>
 
 #ifndef PLK_NTT_DIAG
-#define PLK_NTT_DIAG 0        // tuning builds only: bit 0 skips the butterflies, bit 1 the LDS exchanges
+#define PLK_NTT_DIAG 0        // tuning builds only: bit 0 skips the butterflies, bit 1 the LDS exchanges,
+                              // bit 2 makes them lane-linear (conflict-free, wrong data)
 #endif
 
 namespace {
@@ -49,6 +50,9 @@ namespace {
 #endif
 #ifndef PLK_NTT_BYTE_LUT
 #define PLK_NTT_BYTE_LUT 1     // byte values through a 256-entry LDS table (0: arithmetic in registers)
+#endif
+#ifndef PLK_NTT_SWZ
+#define PLK_NTT_SWZ 1          // XOR-swizzled (bank-conflict-free) exchange layout; 0: the 1-in-32 pad
 #endif
 #ifndef PLK_NTT_CW13
 #define PLK_NTT_CW13 8         // min waves per SIMD (launch bound): 8 = two 1024-thread blocks per CU
@@ -249,12 +253,134 @@ struct Eng {
     }
   }
 
+  // ---- exchange layout ------------------------------------------------------------------
+  // Tile element bit that thread-id bit i selects in round q's mapping (base() above).
+  static constexpr int lane_bit(int q, bool inv, int i) {
+    const int lb = lbq(q, inv);
+    if (!colsq(q, inv)) return i < lb ? i : i + R;
+    if (i < TB - M) return M + i;
+    return i - (TB - M) < lb ? i - (TB - M) : i - (TB - M) + R;
+  }
+  static constexpr bool indep5(const uint32_t* v, int n) {   // linear independence over GF(2)^5
+    uint32_t a[8] = {};
+    for (int i = 0; i < n; i++) a[i] = v[i];
+    int r = 0;
+    for (int bit = 0; bit < 5; bit++) {
+      int piv = -1;
+      for (int i = r; i < n && piv < 0; i++)
+        if ((a[i] >> bit) & 1) piv = i;
+      if (piv < 0) continue;
+      const uint32_t t = a[r];
+      a[r] = a[piv];
+      a[piv] = t;
+      for (int i = 0; i < n; i++)
+        if (i != r && ((a[i] >> bit) & 1)) a[i] ^= a[r];
+      r++;
+    }
+    return r == n;
+  }
+  // Exchange q stores element e at word e ^ h(e), h(e) = XOR of m[j] over the set bits j >= 5 of
+  // e (a bijection: only the low 5 bits move).  The bank of a ds_read/ds_write_b32 is (word mod
+  // 32) per half-wave, so the 32 lanes are conflict-free iff their 5 varying element bits map to
+  // 5 independent bank vectors: unit vectors for element bits < 5, m[j] for the others.  The
+  // masks are chosen greedily at compile time so that BOTH the writing round q and the reading
+  // round q+1 are conflict-free (checked for every instantiated pass).  With the 1-in-32 pad the
+  // column rounds of high passes -- consecutive lanes 2^M words apart -- were 8-way conflicted.
+  struct Swz {
+    uint32_t m[16];
+  };
+  static constexpr Swz swz(int q, bool inv) {
+    Swz s{};
+    int S[2][5] = {};
+    for (int i = 0; i < 5; i++) {
+      S[0][i] = lane_bit(q, inv, i);
+      S[1][i] = lane_bit(q + 1, inv, i);
+    }
+    for (int j = 5; j < 16; j++) {
+      bool in0 = false, in1 = false;
+      for (int i = 0; i < 5; i++) {
+        in0 = in0 || S[0][i] == j;
+        in1 = in1 || S[1][i] == j;
+      }
+      if (!in0 && !in1) continue;
+      for (uint32_t m = 1; m < 32; m++) {
+        bool ok = true;
+        for (int t = 0; t < 2 && ok; t++) {
+          if (!(t ? in1 : in0)) continue;
+          uint32_t v[6] = {};
+          int n = 0;
+          for (int i = 0; i < 5; i++) {
+            const int b = S[t][i];
+            if (b < 5) v[n++] = 1u << b;
+            else if (b < j) v[n++] = s.m[b];
+          }
+          v[n++] = m;
+          ok = indep5(v, n);
+        }
+        if (ok) {
+          s.m[j] = m;
+          break;
+        }
+      }
+    }
+    return s;
+  }
+  static constexpr bool swz_ok(int q, bool inv) {   // every lane-bit set got its basis
+    const Swz s = swz(q, inv);
+    for (int t = 0; t < 2; t++) {
+      uint32_t v[5] = {};
+      for (int i = 0; i < 5; i++) {
+        const int b = lane_bit(q + t, inv, i);
+        v[i] = b < 5 ? 1u << b : s.m[b];
+      }
+      if (!indep5(v, 5)) return false;
+    }
+    return true;
+  }
+  template <int Q, bool INV>
+  __device__ static __forceinline__ uint32_t swz_h(uint32_t e) {
+    constexpr Swz s = swz(Q, INV);
+    uint32_t h = 0;
+#pragma unroll
+    for (int j = 5; j < TB; j++)
+      if (s.m[j]) h ^= ((e >> j) & 1u) ? s.m[j] : 0u;
+    return h;
+  }
+
   // registers (mapping from) -> LDS -> registers (mapping to).  Double-buffered: one barrier
   // suffices (the buffer written next was last read before the previous barrier); single
   // buffer: a second barrier before the buffer is written again.
+  template <int Q, bool INV>
   __device__ static __forceinline__ void exchange(uint32_t (&v)[E], uint32_t* buf, uint32_t bf, int lbf, uint32_t bt,
                                                   int lbt) {
     if (PLK_NTT_DIAG & 2) return;
+    if (PLK_NTT_SWZ && HIGH && swz_ok(Q, INV)) {   // (M = TB passes: 1-2 way at most, and the center
+                                                      //  kernel has no VGPRs to spare for the bases)
+      // e = base | k << lb (disjoint bits) and h is linear: h(e) = h(base) ^ h(k << lb)
+      const uint32_t xw = bf ^ swz_h<Q, INV>(bf), xr = bt ^ swz_h<Q, INV>(bt);
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        const uint32_t ek = (uint32_t)k << lbf;
+        buf[xw ^ ek ^ swz_h<Q, INV>(ek)] = v[k];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        const uint32_t ek = (uint32_t)k << lbt;
+        v[k] = buf[xr ^ ek ^ swz_h<Q, INV>(ek)];
+      }
+      if (!DBUF) __syncthreads();
+      return;
+    }
+    if (PLK_NTT_DIAG & 4) {   // timing only: conflict-free lane-linear exchange (wrong data)
+#pragma unroll
+      for (int k = 0; k < E; k++) buf[k * NT + threadIdx.x] = v[k];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < E; k++) v[k] = buf[k * NT + (threadIdx.x ^ 1)];
+      if (!DBUF) __syncthreads();
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < E; k++) buf[wphys((int)(bf + ((uint32_t)k << lbf)))] = v[k];
     __syncthreads();
@@ -270,8 +396,8 @@ struct Eng {
                                               const uint32_t* Tsm) {
     round<Q, INV>(v, base_q<Q>(tid, INV), Tsm);
     if constexpr (Q + 1 < NR) {
-      exchange(v, bufs + (DBUF ? ((xc + Q) & 1) * BUF : 0), base_q<Q>(tid, INV), lbq(Q, INV),
-               base_q<Q + 1>(tid, INV), lbq(Q + 1, INV));
+      exchange<Q, INV>(v, bufs + (DBUF ? ((xc + Q) & 1) * BUF : 0), base_q<Q>(tid, INV), lbq(Q, INV),
+                       base_q<Q + 1>(tid, INV), lbq(Q + 1, INV));
       pass<INV, Q + 1>(v, tid, bufs, xc, Tsm);
     }
   }
