@@ -388,7 +388,10 @@ def prove_component(torch, hip, dev, log2n, reps=5):
             "deterministic": out == first, "matches_oracle": _prove_golden(n, out),
             "device_mib": round(pr.device_bytes() / 2**20, 1),
             "note": "rounds 1-5 of plonk_prove, synthetic interpolated polys (gen.prove_instance, seed 51), SRS len 2n+8, "
-                    "host wall time per synchronous call (proof bytes back on the host)"}
+                    "host wall time per synchronous call (proof bytes back on the host); matches_oracle: equal to the "
+                    "recorded answer of the CPU restatement oracle/prove_ref.py (tests/golden/prove_2_20.json), which is "
+                    "pinned to the reference's own proofs at n = 4 -- the reference cannot prove above 4 gates "
+                    "(no 2^20-point domain in GF(17)), so parity at 2^20 is pinned through that restatement"}
 
 
 def main():
