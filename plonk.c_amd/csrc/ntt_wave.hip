@@ -350,12 +350,11 @@ struct Eng {
   // registers (mapping from) -> LDS -> registers (mapping to).  Double-buffered: one barrier
   // suffices (the buffer written next was last read before the previous barrier); single
   // buffer: a second barrier before the buffer is written again.
-  template <int Q, bool INV>
+  template <int Q, bool INV, bool SWZ>
   __device__ static __forceinline__ void exchange(uint32_t (&v)[E], uint32_t* buf, uint32_t bf, int lbf, uint32_t bt,
                                                   int lbt) {
     if (PLK_NTT_DIAG & 2) return;
-    if (PLK_NTT_SWZ && HIGH && swz_ok(Q, INV)) {   // (M = TB passes: 1-2 way at most, and the center
-                                                      //  kernel has no VGPRs to spare for the bases)
+    if (PLK_NTT_SWZ && SWZ && swz_ok(Q, INV)) {
       // e = base | k << lb (disjoint bits) and h is linear: h(e) = h(base) ^ h(k << lb)
       const uint32_t xw = bf ^ swz_h<Q, INV>(bf), xr = bt ^ swz_h<Q, INV>(bt);
 #pragma unroll
@@ -391,14 +390,16 @@ struct Eng {
 
   // rounds Q .. NR-1 of a pass; registers hold the mapping of round Q on entry and of the
   // last round on exit.  xc selects the exchange buffer (it counts exchanges).
-  template <bool INV, int Q = 0>
+  // SWZ: the swizzled exchange layout where it is conflict-free (the center kernel passes false:
+  // it has no VGPRs to spare for the two extra base registers)
+  template <bool INV, bool SWZ = true, int Q = 0>
   __device__ static __forceinline__ void pass(uint32_t (&v)[E], uint32_t tid, uint32_t* bufs, int xc,
                                               const uint32_t* Tsm) {
     round<Q, INV>(v, base_q<Q>(tid, INV), Tsm);
     if constexpr (Q + 1 < NR) {
-      exchange<Q, INV>(v, bufs + (DBUF ? ((xc + Q) & 1) * BUF : 0), base_q<Q>(tid, INV), lbq(Q, INV),
-                       base_q<Q + 1>(tid, INV), lbq(Q + 1, INV));
-      pass<INV, Q + 1>(v, tid, bufs, xc, Tsm);
+      exchange<Q, INV, SWZ>(v, bufs + (DBUF ? ((xc + Q) & 1) * BUF : 0), base_q<Q>(tid, INV), lbq(Q, INV),
+                            base_q<Q + 1>(tid, INV), lbq(Q + 1, INV));
+      pass<INV, SWZ, Q + 1>(v, tid, bufs, xc, Tsm);
     }
   }
 
@@ -683,11 +684,11 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
       first = false;
     }
     __syncthreads();
-    G::template pass<false>(va, tid, bufs, 0, Tf);
-    G::template pass<false>(vb, tid, bufs, G::XCH, Tf);
+    G::template pass<false, false>(va, tid, bufs, 0, Tf);
+    G::template pass<false, false>(vb, tid, bufs, G::XCH, Tf);
 #pragma unroll
     for (int k = 0; k < G::E; k++) va[k] = F::pmul(va[k], vb[k]);
-    G::template pass<true>(va, tid, bufs, 2 * G::XCH, Tf);
+    G::template pass<true, false>(va, tid, bufs, 2 * G::XCH, Tf);
 #pragma unroll
     for (int k = 0; k < G::E; k++) dc[G::index(p, tile, bf + ((uint32_t)k << LF))] = va[k];
   }
