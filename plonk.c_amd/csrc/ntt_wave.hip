@@ -727,7 +727,7 @@ uint32_t center_blocks() {
     const char* e = getenv("PLK_NTT_CENTER_BLOCKS");
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    nb = e ? (uint32_t)atoi(e) : 2u * (uint32_t)cus;
+    nb = e ? (uint32_t)atoi(e) : (PLK_NTT_CW13 >= 8 ? 2u : 1u) * (uint32_t)cus;   // the resident blocks
     if (!nb) nb = 512;
   }
   return nb;
