@@ -39,6 +39,7 @@ struct Ctx {
   // pinned staging for host -> device copies
   uint8_t* h_stage = nullptr;
   size_t cap_stage = 0;
+  bool stage_busy = false;  // staged copies of a call may still be in flight (see Stage)
   // poly_mul staging
   uint8_t* d_a = nullptr;
   size_t cap_a = 0;
@@ -176,11 +177,16 @@ int grow_host(uint8_t** p, size_t* cap, size_t need, bool pinned) {
 
 // Host -> device through the pinned staging buffer in chunks (the caller's pageable memory is
 // copied into pinned memory while the previous chunk's DMA runs).  Synchronous on g.st.
+constexpr size_t STAGE_CHUNK = 4u << 20;
 int upload(uint8_t* dst, const uint8_t* src, size_t bytes) {
-  constexpr size_t CHUNK = 4u << 20;
+  constexpr size_t CHUNK = STAGE_CHUNK;
   if (!bytes) return PLK_OK;
   int rc = grow_host(&g.h_stage, &g.cap_stage, 2 * CHUNK, true);
   if (rc) return rc;
+  if (g.stage_busy) {
+    PLK_HIP(hipStreamSynchronize(g.st));
+    g.stage_busy = false;
+  }
   hipEvent_t done[2] = {nullptr, nullptr};
   PLK_HIP(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
   PLK_HIP(hipEventCreateWithFlags(&done[1], hipEventDisableTiming));
@@ -197,6 +203,61 @@ int upload(uint8_t* dst, const uint8_t* src, size_t bytes) {
   (void)hipEventDestroy(done[1]);
   return PLK_OK;
 }
+
+// The small copies of one host-buffer call without a synchronisation per copy (the drop-in makes
+// many calls of a few bytes each: a stream synchronize per upload cost ~20 us apiece): uploads are
+// copied into the pinned staging buffer and enqueued, downloads land in staging and are copied out
+// after the call's ONE stream synchronize (finish).  A copy that does not fit takes the chunked
+// upload() / a direct copy.  Staging is reused by the next call only after that synchronize
+// (stage_busy guards calls that returned early on an error).
+struct Stage {
+  struct Down {
+    uint8_t* dst;
+    size_t off, n;
+  };
+  size_t used = 0;
+  Down downs[8];
+  int nd = 0;
+  int begin() {
+    int rc = grow_host(&g.h_stage, &g.cap_stage, 2 * STAGE_CHUNK, true);
+    if (rc) return rc;
+    if (g.stage_busy) {
+      PLK_HIP(hipStreamSynchronize(g.st));
+      g.stage_busy = false;
+    }
+    return PLK_OK;
+  }
+  bool fits(size_t n) const { return used + ((n + 255) & ~(size_t)255) <= 2 * STAGE_CHUNK; }
+  int up(uint8_t* d, const uint8_t* h, size_t n) {
+    if (!n) return PLK_OK;
+    if (!fits(n)) return upload(d, h, n);   // (synchronises: earlier staged copies are done)
+    memcpy(g.h_stage + used, h, n);
+    PLK_HIP(hipMemcpyAsync(d, g.h_stage + used, n, hipMemcpyHostToDevice, g.st));
+    g.stage_busy = true;
+    used += (n + 255) & ~(size_t)255;
+    return PLK_OK;
+  }
+  int down(uint8_t* h, const uint8_t* d, size_t n) {
+    if (!n) return PLK_OK;
+    if (!fits(n) || nd == 8) {
+      PLK_HIP(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, g.st));
+      return PLK_OK;
+    }
+    PLK_HIP(hipMemcpyAsync(g.h_stage + used, d, n, hipMemcpyDeviceToHost, g.st));
+    g.stage_busy = true;
+    downs[nd++] = Down{h, used, n};
+    used += (n + 255) & ~(size_t)255;
+    return PLK_OK;
+  }
+  int finish() {
+    PLK_HIP(hipStreamSynchronize(g.st));
+    g.stage_busy = false;
+    for (int i = 0; i < nd; i++) memcpy(downs[i].dst, g.h_stage + downs[i].off, downs[i].n);
+    nd = 0;
+    used = 0;
+    return PLK_OK;
+  }
+};
 
 int init_locked(int device) {
   if (g.ready) {
@@ -373,16 +434,19 @@ int plk_msm_g1(const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t 
     }
     if ((rc = grow_host(&g.h_srs, &g.cap_h_srs, pb + 16, false))) return rc;
     g.srs_key = nullptr;   // invalid until the upload completed
-    if ((rc = upload(g.d_pts, points, pb))) return rc;
+  }
+  Stage S;
+  if ((rc = S.begin())) return rc;
+  if (!hit && n) {
+    if ((rc = S.up(g.d_pts, points, pb))) return rc;   // (ordered before the kernel on g.st)
     memcpy(g.h_srs, points, pb);
     g.srs_key = points;
     g.srs_cached = pb;
   }
-  if ((rc = upload(g.d_sc, scalars, n))) return rc;
+  if ((rc = S.up(g.d_sc, scalars, n))) return rc;
   if ((rc = plk_msm_launch(g.d_pts, g.d_sc, n, g.d_res, g.st))) return rc;
   PlkMsmResult h;
-  PLK_HIP(hipMemcpyAsync(&h, g.d_res, sizeof h, hipMemcpyDeviceToHost, g.st));
-  PLK_HIP(hipStreamSynchronize(g.st));
+  if ((rc = S.down((uint8_t*)&h, (const uint8_t*)g.d_res, 32)) || (rc = S.finish())) return rc;   // log, irregular, g1
   if (h.irregular) {
     if ((rc = plk_msm_serial_launch(g.d_pts, g.d_sc, n, g.d_res, g.st))) return rc;
     PLK_HIP(hipMemcpyAsync(&h, g.d_res, sizeof h, hipMemcpyDeviceToHost, g.st));
@@ -412,12 +476,13 @@ int plk_poly_mul(const uint8_t* a, size_t la, const uint8_t* b, size_t lb, uint8
       (rc = grow(&g.d_out, &g.cap_out, rl + 16)))
     return rc;
   if (ws && (rc = grow((uint8_t**)&g.d_work, &g.cap_work, ws))) return rc;
-  if ((rc = upload(g.d_a, a, la)) || (rc = upload(g.d_b, b, lb))) return rc;
+  Stage S;
+  if ((rc = S.begin()) || (rc = S.up(g.d_a, a, la)) || (rc = S.up(g.d_b, b, lb))) return rc;
   if ((rc = plk_poly_mul_launch(g.d_a, la, g.d_b, lb, g.d_out, g.d_nz, g.d_work, g.st))) return rc;
   uint32_t nz = 0;
-  PLK_HIP(hipMemcpyAsync(out, g.d_out, rl, hipMemcpyDeviceToHost, g.st));
-  PLK_HIP(hipMemcpyAsync(&nz, g.d_nz, 4, hipMemcpyDeviceToHost, g.st));
-  PLK_HIP(hipStreamSynchronize(g.st));
+  if ((rc = S.down(out, g.d_out, rl)) || (rc = S.down((uint8_t*)&nz, (const uint8_t*)g.d_nz, 4)) ||
+      (rc = S.finish()))
+    return rc;
   *out_len = nz ? nz : 1;
   return PLK_OK;
 }
@@ -557,12 +622,14 @@ int plk_poly_eval_batch(const uint8_t* const* polys, const size_t* lens, const u
   const size_t o_y = A.take(n), o_tick = A.take(plk_poly_eval_workspace(n));
   if ((rc = grow(&g.d_ops, &g.cap_ops, A.off))) return rc;
   std::vector<const uint8_t*> dp(n);
+  Stage S;
+  if ((rc = S.begin())) return rc;
   for (int i = 0; i < n; i++) {
     if (lens[i] && !polys[i]) {
       plk_set_error("plk_poly_eval_batch: NULL polynomial %d", i);
       return PLK_ERR_ARG;
     }
-    if (lens[i] && (rc = upload(g.d_ops + off[i], polys[i], lens[i]))) return rc;
+    if (lens[i] && (rc = S.up(g.d_ops + off[i], polys[i], lens[i]))) return rc;
     dp[i] = g.d_ops + off[i];
   }
   PLK_HIP(hipMemsetAsync(g.d_ops + o_tick, 0, plk_poly_eval_workspace(n), g.st));
@@ -574,8 +641,7 @@ int plk_poly_eval_batch(const uint8_t* const* polys, const size_t* lens, const u
                                          g.d_ops + o_tick + (size_t)128 * b, g.st)))
       return rc;
   }
-  PLK_HIP(hipMemcpyAsync(ys, g.d_ops + o_y, n, hipMemcpyDeviceToHost, g.st));
-  PLK_HIP(hipStreamSynchronize(g.st));
+  if ((rc = S.down(ys, g.d_ops + o_y, n)) || (rc = S.finish())) return rc;
   return PLK_OK;
 }
 
@@ -618,14 +684,14 @@ int plk_poly_divide(const uint8_t* num, size_t nl, const uint8_t* den, size_t dl
                o_w = A.take(plk_poly_divide_workspace_bytes(nl, dl));
   if ((rc = grow(&g.d_ops, &g.cap_ops, A.off))) return rc;
   uint8_t* d = g.d_ops;
-  if ((rc = upload(d + o_num, num, nl))) return rc;
+  Stage S;
+  if ((rc = S.begin()) || (rc = S.up(d + o_num, num, nl))) return rc;
   if ((rc = plk_poly_divide_launch(d + o_num, nl, den, dl, d + o_q, d + o_r, (uint32_t*)(d + o_len), d + o_w, g.st)))
     return rc;
   uint32_t lens[2] = {0, 0};
-  PLK_HIP(hipMemcpyAsync(quot, d + o_q, ql, hipMemcpyDeviceToHost, g.st));
-  if (rl) PLK_HIP(hipMemcpyAsync(rem, d + o_r, rl, hipMemcpyDeviceToHost, g.st));
-  PLK_HIP(hipMemcpyAsync(lens, d + o_len, 8, hipMemcpyDeviceToHost, g.st));
-  PLK_HIP(hipStreamSynchronize(g.st));
+  if ((rc = S.down(quot, d + o_q, ql)) || (rc = S.down(rem, d + o_r, rl)) ||
+      (rc = S.down((uint8_t*)lens, d + o_len, 8)) || (rc = S.finish()))
+    return rc;
   // poly_new's trim keeps one coefficient (src/poly.h:21-24); a zero-length remainder stays empty
   *quot_len = lens[0] ? lens[0] : 1;
   *rem_len = rl ? (lens[1] ? lens[1] : 1) : 0;
@@ -645,10 +711,10 @@ int plk_matrix_mul(const uint8_t* a, size_t m, size_t k, const uint8_t* b, size_
   const size_t o_a = A.take(m * k), o_b = A.take(k * n), o_o = A.take(m * n);
   if ((rc = grow(&g.d_ops, &g.cap_ops, A.off))) return rc;
   uint8_t* d = g.d_ops;
-  if ((rc = upload(d + o_a, a, m * k)) || (rc = upload(d + o_b, b, k * n))) return rc;
+  Stage S;
+  if ((rc = S.begin()) || (rc = S.up(d + o_a, a, m * k)) || (rc = S.up(d + o_b, b, k * n))) return rc;
   if ((rc = plk_matrix_mul_launch(d + o_a, m, k, d + o_b, n, d + o_o, g.st))) return rc;
-  PLK_HIP(hipMemcpyAsync(out, d + o_o, m * n, hipMemcpyDeviceToHost, g.st));
-  PLK_HIP(hipStreamSynchronize(g.st));
+  if ((rc = S.down(out, d + o_o, m * n)) || (rc = S.finish())) return rc;
   return PLK_OK;
 }
 
@@ -671,10 +737,10 @@ int plk_matrix_inv(const uint8_t* mat, size_t n, uint8_t* out) {
   const size_t o_m = A.take(n * n), o_aug = A.take(2 * n * n), o_o = A.take(n * n);
   if ((rc = grow(&g.d_ops, &g.cap_ops, A.off))) return rc;
   uint8_t* d = g.d_ops;
-  if ((rc = upload(d + o_m, mat, n * n))) return rc;
+  Stage S;
+  if ((rc = S.begin()) || (rc = S.up(d + o_m, mat, n * n))) return rc;
   if ((rc = plk_matrix_inv_launch(d + o_m, n, d + o_aug, d + o_o, g.st))) return rc;
-  PLK_HIP(hipMemcpyAsync(out, d + o_o, n * n, hipMemcpyDeviceToHost, g.st));
-  PLK_HIP(hipStreamSynchronize(g.st));
+  if ((rc = S.down(out, d + o_o, n * n)) || (rc = S.finish())) return rc;
   return PLK_OK;
 }
 
@@ -694,13 +760,12 @@ int plk_interpolate(const uint8_t* h_pows_inv, const uint8_t* values, size_t n, 
   const size_t o_m = A.take(n * n), o_v = A.take(n), o_o = A.take(n), o_len = A.take(16);
   if ((rc = grow(&g.d_ops, &g.cap_ops, A.off))) return rc;
   uint8_t* d = g.d_ops;
-  if ((rc = upload(d + o_m, h_pows_inv, n * n)) || (rc = upload(d + o_v, values, n))) return rc;
+  Stage S;
+  if ((rc = S.begin()) || (rc = S.up(d + o_m, h_pows_inv, n * n)) || (rc = S.up(d + o_v, values, n))) return rc;
   if ((rc = plk_matrix_mul_launch(d + o_m, n, n, d + o_v, 1, d + o_o, g.st))) return rc;
   if ((rc = plk_trim_launch(d + o_o, n, (uint32_t*)(d + o_len), g.st))) return rc;
   uint32_t nz = 0;
-  PLK_HIP(hipMemcpyAsync(out, d + o_o, n, hipMemcpyDeviceToHost, g.st));
-  PLK_HIP(hipMemcpyAsync(&nz, d + o_len, 4, hipMemcpyDeviceToHost, g.st));
-  PLK_HIP(hipStreamSynchronize(g.st));
+  if ((rc = S.down(out, d + o_o, n)) || (rc = S.down((uint8_t*)&nz, d + o_len, 4)) || (rc = S.finish())) return rc;
   *out_len = nz ? nz : 1;
   return PLK_OK;
 }
