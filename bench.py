@@ -346,7 +346,63 @@ def components(torch, hip, dev, st):
     out["poly_mul_2^19x2^19"] = {"ms": round(avg, 4), "Gcoeff_s_out": round((la + lb - 1) / (avg * 1e-3) / 1e9, 2),
                                  "roofline": roofline_obj(la + lb + (la + lb - 1), avg,
                                                           "SURVEY 8(d): la + lb + (la + lb - 1) bytes of HF")}
+    out.update(polyops_components(torch, hip, dev, st))
+    bfly = butterfly_roofline((1 << 19) * 20, out["ntt_2^20_forward"]["ms"], "bb_dif_Gbfly_s")
+    if bfly:
+        out["ntt_2^20_forward"]["roofline_butterfly"] = bfly
     out["prove_2^20_gates"] = prove_component(torch, hip, dev, 20)
+    return out
+
+
+def butterfly_roofline(bfly, ms, key):
+    """Compute roofline of an NTT component: radix-2 butterflies / time against the butterfly peak
+    measured by tools/bfly_peak.hip (the engine's own formulas in registers, no memory; committed
+    in profiles/r02_bfly_peak.json -- a peak, like the HBM spec peak, not a timing of this run)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r02_bfly_peak.json")) as f:
+            pk = json.loads([l for l in f if l.startswith("{")][0])
+    except (OSError, IndexError, ValueError):
+        return None
+    rate = bfly / (ms * 1e-3) / 1e9
+    return {"bound": "valu", "achieved": round(rate, 1), "peak": pk[key], "unit": "Gbutterfly/s",
+            "frac": round(rate / pk[key], 4), "butterflies": int(bfly),
+            "peak_source": "profiles/r02_bfly_peak.json (%s)" % key}
+
+
+def polyops_components(torch, hip, dev, st):
+    """SURVEY 8 (f) rows at the boundary, device-resident: poly_divide by Z_H = x^n - 1
+    (src/poly.h:124-177; the prover's t(x) division, n = 2^20, numerator 4n) and a batch of 8
+    poly_eval over 2^22-coefficient polynomials (src/poly.h:265-272); both read their inputs once,
+    so the HBM roofline applies (canonical random coefficients)."""
+    import numpy as np
+    out = {}
+    n = 1 << 20
+    nl = 4 * n
+    num = torch.randint(0, 17, (nl,), dtype=torch.int16, device=dev).to(torch.uint8)
+    den = np.zeros(n + 1, np.uint8)
+    den[0], den[n] = 16, 1
+    quot = torch.zeros(nl, dtype=torch.uint8, device=dev)
+    rem = torch.zeros(n, dtype=torch.uint8, device=dev)
+    lens = torch.zeros(4, dtype=torch.int32, device=dev)
+    work = torch.zeros(max(16, hip.poly_divide_workspace(nl, n + 1)), dtype=torch.uint8, device=dev)
+    call = lambda i, s: hip.poly_divide_dev(num, nl, den, quot, rem, lens, work, s)   # noqa: E731
+    gr = graph_avg_ms(torch, call, 20)
+    avg, _ = gr if gr else event_avg_ms(torch, st, lambda i: call(i, st), 20)
+    alg = nl + (nl - n) + n    # numerator read once, quotient and remainder written once
+    out["poly_divide_zh_2^22"] = {"ms": round(avg, 4), "roofline": roofline_obj(alg, avg,
+                                  "numerator read + quotient and remainder written once (bytes of HF)"),
+                                  "note": "plk_poly_divide_dev by x^(2^20) - 1, numerator 2^22 coefficients"}
+    m = 8
+    polys = [torch.randint(0, 17, (nl,), dtype=torch.int16, device=dev).to(torch.uint8) for _ in range(m)]
+    ys = torch.zeros(m, dtype=torch.uint8, device=dev)
+    tick = torch.zeros(max(16, hip.poly_eval_workspace(m)), dtype=torch.uint8, device=dev)
+    xs = np.arange(2, 2 + m, dtype=np.uint8)
+    call = lambda i, s: hip.poly_eval_batch_dev(polys, [nl] * m, xs, ys, tick, s)   # noqa: E731
+    gr = graph_avg_ms(torch, call, 20)
+    avg, _ = gr if gr else event_avg_ms(torch, st, lambda i: call(i, st), 20)
+    out["poly_eval_batch8_2^22"] = {"ms": round(avg, 4), "roofline": roofline_obj(m * nl, avg,
+                                    "every coefficient byte read once"),
+                                    "note": "plk_poly_eval_batch_dev: 8 polynomials of 2^22 coefficients per launch"}
     return out
 
 

@@ -126,18 +126,70 @@ __global__ __launch_bounds__(EVAL_NT) void eval_batch_kernel(EvalJobs J, uint8_t
 // q[i-dl+1] = c; rem[i-j] -= c den[dl-1-j] for j < dl) on raw bytes, one thread: the general
 // divisor and non-canonical inputs.
 // ---------------------------------------------------------------------------------------
-__global__ void div_serial_kernel(const uint8_t* __restrict__ num, uint64_t nl, const uint8_t* __restrict__ den,
-                                  uint64_t dl, uint8_t* __restrict__ q, uint64_t qcap, uint8_t* __restrict__ rem,
-                                  const uint32_t* __restrict__ gate) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  if (gate && *gate == 0) return;   // only when the parallel path flagged its inputs
+// The reference's loop (src/poly.h:124-177) on raw bytes, one thread.  den == nullptr: the
+// binomial divisor lead x^(dl-1) + d0 given by its two bytes (the gated re-run behind the chain
+// scans: no host-to-device copy of a mostly-zero divisor per call).
+// The running remainder lives in the workspace (nl bytes); the caller's rem receives its first
+// min(dl - 1, nl) bytes (the size plk_poly_divide_dev documents).
+__device__ void serial_divide(const uint8_t* __restrict__ num, uint64_t nl, const uint8_t* __restrict__ den, uint64_t dl,
+                              uint32_t d0, uint32_t lead, uint8_t* __restrict__ q, uint64_t qcap,
+                              uint8_t* __restrict__ rem, uint64_t rl, uint8_t* __restrict__ run) {
   for (uint64_t i = 0; i < qcap; i++) q[i] = 0;
-  for (uint64_t i = 0; i < nl; i++) rem[i] = num[i];
-  const uint32_t inv = c_hinv17[den[dl - 1]];   // lead < 17 (host-checked)
+  for (uint64_t i = 0; i < nl; i++) run[i] = num[i];
+  auto den_at = [&](uint64_t i) -> uint32_t { return den ? den[i] : (i == 0 ? d0 : (i == dl - 1 ? lead : 0u)); };
+  const uint32_t inv = c_hinv17[den_at(dl - 1)];   // lead < 17 (host-checked)
   for (uint64_t i = nl; i-- > dl - 1;) {
-    const uint32_t c = raw_mul(rem[i], inv);
+    const uint32_t c = raw_mul(run[i], inv);
     q[i - (dl - 1)] = (uint8_t)c;
-    for (uint64_t j = 0; j < dl; j++) rem[i - j] = (uint8_t)raw_sub(rem[i - j], raw_mul(c, den[dl - 1 - j]));
+    // every j, zero divisor bytes included: hf_sub of raw bytes normalises as the reference does
+    for (uint64_t j = 0; j < dl; j++) run[i - j] = (uint8_t)raw_sub(run[i - j], raw_mul(c, den_at(dl - 1 - j)));
+  }
+  for (uint64_t i = 0; i < rl; i++) rem[i] = run[i];
+}
+
+__device__ __forceinline__ uint32_t fin_block_max(uint32_t v, uint32_t* red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off, PLK_WAVE));
+  __syncthreads();
+  if ((threadIdx.x & (PLK_WAVE - 1)) == 0) red[threadIdx.x / PLK_WAVE] = v;
+  __syncthreads();
+  uint32_t m = 0;
+  for (int w = 0; w < (int)(blockDim.x / PLK_WAVE); w++) m = max(m, red[w]);
+  return m;
+}
+// index + 1 of the last non-zero byte of p[0, len) (0: all zero), scanning back 16 KiB at a time
+__device__ uint32_t fin_trim(const uint8_t* __restrict__ p, uint64_t len, uint32_t* red) {
+  constexpr int64_t CH = 16384;
+  for (int64_t end = (int64_t)len; end > 0; end -= CH) {
+    const int64_t start = end > CH ? end - CH : 0;
+    uint32_t last = 0;
+    for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x)
+      if (p[i]) last = max(last, (uint32_t)(i + 1));
+    last = fin_block_max(last, red);
+    if (last) return last;
+  }
+  return 0;
+}
+
+// ONE launch after the division kernels: the reference's loop when it is needed (mode 1: always,
+// the divisor copied to the device; mode 2: only when the chain scans flagged non-canonical
+// numerator bytes, binomial divisor by its two bytes), then the trimmed lengths of q and rem
+// (src/poly.h:158-170) -- three launches (serial re-run + two trims) folded into one.
+__global__ __launch_bounds__(1024) void div_finish_kernel(const uint8_t* __restrict__ num, uint64_t nl,
+                                                         const uint8_t* __restrict__ den, uint64_t dl, uint32_t d0,
+                                                         uint32_t lead, uint8_t* __restrict__ q, uint64_t ql,
+                                                         uint8_t* __restrict__ rem, uint64_t rl, int mode,
+                                                         const uint32_t* __restrict__ gate, uint8_t* __restrict__ scratch,
+                                                         uint32_t* __restrict__ lens) {
+  __shared__ uint32_t red[16];
+  const bool run = mode == 1 || (mode == 2 && *gate != 0);   // uniform
+  if (run && threadIdx.x == 0) serial_divide(num, nl, den, dl, d0, lead, q, ql, rem, rl, scratch);
+  __syncthreads();   // thread 0's global writes are visible to the block after the barrier
+  const uint32_t lq = fin_trim(q, ql, red);
+  const uint32_t lr = rl ? fin_trim(rem, rl, red) : 0u;
+  if (threadIdx.x == 0) {
+    lens[0] = lq;
+    lens[1] = lr;
   }
 }
 
@@ -398,7 +450,7 @@ size_t plk_poly_divide_workspace_bytes(uint64_t nl, uint64_t dl) {
   const uint64_t chains = m < lq ? m : lq;
   const uint64_t len = chains ? (lq + m - 1) / (m ? m : 1) : 0;
   const uint64_t nblk = (len + SCAN_B - 1) / SCAN_B;
-  return 256 + ((dl + 15) & ~15ull) + 4 * (chains * nblk + 16);
+  return 256 + ((dl + 15) & ~15ull) + 4 * (chains * nblk + 16) + ((nl + 15) & ~15ull);   // + the serial remainder
 }
 
 // Classifies the divisor on the host (den is a host array; the kernels get its bytes by value or
@@ -433,6 +485,7 @@ int plk_poly_divide_launch(const uint8_t* d_num, uint64_t nl, const uint8_t* den
   uint32_t* flag = (uint32_t*)w;           // [0] non-canonical flag
   uint8_t* d_den = w + 256;
   uint32_t* bsum = (uint32_t*)(w + 256 + ((dl + 15) & ~15ull));
+  uint8_t* scratch = w + plk_poly_divide_workspace_bytes(nl, dl) - ((nl + 15) & ~15ull);   // last nl bytes
   PLK_HIP(hipMemsetAsync(flag, 0, 16, st));
   bool canonical_den = true;
   bool binom = true;
@@ -480,17 +533,10 @@ int plk_poly_divide_launch(const uint8_t* d_num, uint64_t nl, const uint8_t* den
   // a divisor outside the parallel forms, or (binomial path) non-canonical numerator bytes: the
   // reference's loop.  (m = 0 and nl < dl are exact for any bytes: hf_mul reduces, copies copy.)
   const bool gated = !serial && nl >= dl && m > 0;
-  if (serial || gated) {
-    PLK_HIP(hipMemcpyAsync(d_den, den, dl, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(div_serial_kernel, dim3(1), dim3(64), 0, st, d_num, nl, d_den, dl, d_q, ql, d_rem,
-                       serial ? nullptr : flag);
-    PLK_HIP(hipGetLastError());
-  }
-  // trimmed lengths (src/poly.h:158-170): index + 1 of the last non-zero byte
-  int rc = plk_trim_launch(d_q, ql, d_lens, st);
-  if (rc) return rc;
-  if (rl) return plk_trim_launch(d_rem, rl, d_lens + 1, st);
-  PLK_HIP(hipMemsetAsync(d_lens + 1, 0, 4, st));
+  if (serial) PLK_HIP(hipMemcpyAsync(d_den, den, dl, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(div_finish_kernel, dim3(1), dim3(1024), 0, st, d_num, nl, serial ? d_den : nullptr, dl,
+                     (uint32_t)den[0], lead, d_q, ql, d_rem, rl, serial ? 1 : (gated ? 2 : 0), flag, scratch, d_lens);
+  PLK_HIP(hipGetLastError());
   return PLK_OK;
 }
 

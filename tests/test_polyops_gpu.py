@@ -134,3 +134,37 @@ def test_plonk_new_vandermonde_and_interpolate(hip):
     assert h_inv.hex() == setup["h_pows_inv"]
     for c in g["interpolate_at_h"]:
         assert hip.interpolate(h_inv, c["values"]).hex() == c["out"]
+
+
+@pytest.mark.parametrize("kind", ["raw_binomial", "general"])
+def test_divide_device_api_exact_buffers(hip, oracle, kind):
+    """The reference's loop on the device (non-canonical numerator bytes behind the binomial
+    chain scans, or a divisor with middle terms) writes ONLY the documented sizes: quot
+    nl - dl + 1 bytes, rem min(dl - 1, nl) bytes (the running remainder lives in the workspace);
+    guard bytes after both buffers stay intact."""
+    import torch
+    nl = 3000
+    num, _ = gen.poly_inputs(0x77 + len(kind), nl, 1)
+    num = num.copy()
+    if kind == "raw_binomial":
+        num[nl // 2] = 200                                # not a GF(17) value: the gated loop runs
+        den = np.zeros(65, np.uint8)
+        den[0], den[64] = 16, 1                           # x^64 - 1
+    else:
+        den = np.array([3, 0, 5, 0, 0, 1], np.uint8)      # middle terms: the loop always runs
+    dl = den.size
+    ql, rl = nl - dl + 1, min(dl - 1, nl)
+    G = 64
+    q = torch.full((ql + G,), 0xEE, dtype=torch.uint8, device="cuda")
+    r = torch.full((rl + G,), 0xEE, dtype=torch.uint8, device="cuda")
+    lens = torch.zeros(2, dtype=torch.int32, device="cuda")
+    work = torch.zeros(hip.poly_divide_workspace(nl, dl), dtype=torch.uint8, device="cuda")
+    hip.poly_divide_dev(torch.from_numpy(num).cuda(), nl, den, q, r, lens, work)
+    torch.cuda.synchronize()
+    qh, rh = q.cpu().numpy(), r.cpu().numpy()
+    assert (qh[ql:] == 0xEE).all() and (rh[rl:] == 0xEE).all()
+    wq, wr = hip.poly_divide(num, den)                    # host form (pinned to goldens above)
+    oq, orr = oracle.poly_divide(num, den)
+    assert wq == oq and wr.rstrip(b"\x00") == orr.rstrip(b"\x00")
+    lq, lr = lens.cpu().tolist()
+    assert bytes(qh[:max(lq, 1)]) == wq and bytes(rh[:max(lr, 1)]) == wr
