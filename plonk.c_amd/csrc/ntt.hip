@@ -223,18 +223,6 @@ __device__ void tile_stages(uint32_t* X, int M, int C, int RS, const uint32_t* T
 
 }  // namespace
 
-// max over the block (blockDim a multiple of 64, <= 1024); every thread gets the result
-__device__ __forceinline__ uint32_t block_max(uint32_t v) {
-  __shared__ uint32_t red[16];
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off, PLK_WAVE));
-  __syncthreads();
-  if ((threadIdx.x & (PLK_WAVE - 1)) == 0) red[threadIdx.x / PLK_WAVE] = v;
-  __syncthreads();
-  uint32_t m = 0;
-  for (int w = 0; w < (int)(blockDim.x / PLK_WAVE); w++) m = max(m, red[w]);
-  return m;
-}
 
 // Input/output modes of a pass
 enum : int { IN_U32 = 0, IN_U8 = 1 };
@@ -320,7 +308,7 @@ __global__ __launch_bounds__(1024) void polymul_small_kernel(const uint8_t* a8, 
       if (byte) last = max(last, (uint32_t)i + 1);
     }
   }
-  last = block_max(last);
+  last = plk_block_max(last);
   if (threadIdx.x == 0 && nz) *nz = last;
 }
 
@@ -335,7 +323,7 @@ __global__ __launch_bounds__(1024) void trim_kernel(const uint8_t* __restrict__ 
     uint32_t last = 0;
     for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x)
       if (out8[i]) last = max(last, (uint32_t)(i + 1));
-    last = block_max(last);
+    last = plk_block_max(last);
     if (last) {
       if (threadIdx.x == 0) *nz = last;
       return;
@@ -581,7 +569,9 @@ static size_t pass_lds(int M, int C, bool center) {
 
 // m products of one transform size 2^k through the wave engine (workspace 2^(k+3) bytes each);
 // es[i] > 0: a wrapped product (product_plan) with es[i] top coefficients.
-static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, void* d_work, hipStream_t st) {
+// d_nz (single products only): the trimmed length, computed by the last inverse pass
+static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, void* d_work, hipStream_t st,
+                     uint32_t* d_nz = nullptr) {
   // F29 (lazy reduction, fewer VALU per butterfly) whenever every convolution term fits it
   static int no29 = -1;
   if (no29 < 0) {
@@ -654,6 +644,7 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
                 W + ((size_t)slot[i][1] << k), W + ((size_t)cslot[i] << k)};
     w[i].ntop = (int)e;
   }
+  if (m == 1) w[0].nz = d_nz;
   // sum groups: a member (acc) adds its center output into its leader's first inverse pass
   for (int i = 0, L = 0; i < m; i++) {
     if (!g[i].acc) {
@@ -769,11 +760,8 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
     return PLK_ERR_ARG;
   }
   const PlkPolyMulJob job{d_a, la, d_b, lb, d_out};
-  int rc = ntt_group(&job, 1, k, e ? &e : nullptr, d_work, st);
-  if (rc) return rc;
-  if (d_nz) hipLaunchKernelGGL(trim_kernel, dim3(1), dim3(1024), 0, st, d_out, rl, d_nz);
-  PLK_HIP(hipGetLastError());
-  return PLK_OK;
+  // (the trimmed length comes out of the last inverse pass: no trim_kernel launch)
+  return ntt_group(&job, 1, k, e ? &e : nullptr, d_work, st, d_nz);
 }
 
 // Several independent products: direct / one-workgroup ones one by one, the NTT ones grouped

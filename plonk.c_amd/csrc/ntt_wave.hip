@@ -542,9 +542,11 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
 // at j < ntop.  c[N + j] (sum group: of the group's sum) has only the terms a[i] b[N + j - i]
 // with i >= la - ntop + j (ntop - j <= 16 of them): computed from the bytes by the few threads
 // that hold such j, after the pass's stores (a rare path outside the unrolled store loop).
+// Returns 1 + the largest index it left a non-zero byte at (0: none).
 template <class G>
-__device__ __forceinline__ void wrap_fix(const WJob& jb, uint32_t wrapped, const WPass& p, uint32_t tile, uint32_t bf,
-                                      int LF, uint64_t N) {
+__device__ __forceinline__ uint32_t wrap_fix(const WJob& jb, uint32_t wrapped, const WPass& p, uint32_t tile,
+                                          uint32_t bf, int LF, uint64_t N) {
+  uint32_t last = 0;
   for (int k = 0; k < G::E; k++) {
     if (!(wrapped >> k & 1)) continue;
     const uint64_t idx = G::index(p, tile, bf + ((uint32_t)k << LF));
@@ -556,9 +558,13 @@ __device__ __forceinline__ void wrap_fix(const WJob& jb, uint32_t wrapped, const
       for (uint64_t i = jb.la - (uint64_t)jb.ntop + j; i < jb.la; i++) s += (a[i] % 17u) * (b[N + j - i] % 17u);
     }
     s %= 17u;
-    jb.out8[j] = (uint8_t)((jb.out8[j] + 17u - s) % 17u);
+    const uint32_t lo = (jb.out8[j] + 17u - s) % 17u;
+    jb.out8[j] = (uint8_t)lo;
     jb.out8[N + j] = (uint8_t)s;
+    if (lo) last = max(last, (uint32_t)j + 1u);
+    if (s) last = max(last, (uint32_t)(N + j) + 1u);
   }
+  return last;
 }
 
 // Inverse (DIT) pass, u32 in place (the job's C); the final pass (TO_U8) scales by N^-1 (normal form,
@@ -620,6 +626,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, true);
   const uint32_t of = G::toff(p, bf);
   uint32_t wrapped = 0;   // elements of this thread that hold c[j] + c[N + j] (j < ntop)
+  uint32_t last = 0;      // 1 + the largest index this thread left a non-zero byte at
   const uint32_t N = 1u << p.k;   // (k <= 27: every index fits 32 bits)
   const uint32_t lim = out_len < N ? (uint32_t)out_len : N;
 #pragma unroll
@@ -635,10 +642,24 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
         const uint32_t r = F::out17(v[k], ninv);
         out8[j] = (uint8_t)r;
         if (j < (uint32_t)jb.ntop) wrapped |= 1u << k;
+        else if (r) last = max(last, j + 1u);
       }
     }
   }
-  if (TO_U8 && wrapped) wrap_fix<G>(jb, wrapped, p, tile, bf, LF, 1ull << p.k);
+  if (TO_U8 && wrapped) last = max(last, wrap_fix<G>(jb, wrapped, p, tile, bf, LF, 1ull << p.k));
+  // Trimmed length (src/poly.h:20-38).  The top coefficient of a single product is
+  // a[la-1] b[lb-1] mod 17 (one term, wrapped or not); when it is non-zero -- operands with
+  // non-zero leading bytes, the usual case -- the length is la + lb - 1 and one store says so.
+  // Otherwise every tile takes its block's maximum into the word (zeroed by the center kernel).
+  if (TO_U8 && jb.nz) {
+    const bool top = jb.ngroup == 0 && (jb.a8[jb.la - 1] % 17u) * (jb.b8[jb.lb - 1] % 17u) % 17u != 0u;
+    if (top) {
+      if (blockIdx.x == 0 && tid == 0) *jb.nz = (uint32_t)(out_len + (uint64_t)jb.ntop);
+    } else {
+      last = plk_block_max(last);
+      if (tid == 0 && last) atomicMax(jb.nz, last);
+    }
+  }
 }
 
 // Center of poly_mul: last forward pass (lo = 0) of a and b, pointwise product, first
@@ -666,6 +687,8 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
   // persistent: the grid (<= 2 blocks per CU) walks the batch's (job, tile) items, so the
   // 2^TB-word twiddle table is loaded once per block instead of once per tile
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB), items = tiles * nitems_jobs;
+  // trimmed-length words of the jobs that want one: zeroed here, before the last inverse pass
+  if (blockIdx.x == 0 && tid < nitems_jobs && jobs.j[tid].nz) *jobs.j[tid].nz = 0u;
   bool first = true;
   for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
     const uint32_t job = it / tiles, tile = it - job * tiles;

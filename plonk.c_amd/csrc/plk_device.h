@@ -22,6 +22,20 @@ __device__ __forceinline__ uint32_t plk_wave_sum(uint32_t v) {
          (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
+// max over the block (blockDim a multiple of 64, <= 1024); every thread gets the result.
+// Called by every thread of the block (two barriers inside).
+__device__ __forceinline__ uint32_t plk_block_max(uint32_t v) {
+  __shared__ uint32_t red[16];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off, PLK_WAVE));
+  __syncthreads();
+  if ((threadIdx.x & (PLK_WAVE - 1)) == 0) red[threadIdx.x / PLK_WAVE] = v;
+  __syncthreads();
+  uint32_t m = 0;
+  for (int w = 0; w < (int)(blockDim.x / PLK_WAVE); w++) m = max(m, red[w]);
+  return m;
+}
+
 // ----------------------------------------------------------------------------------------
 // BabyBear Montgomery arithmetic, R = 2^32.  Values are kept fully reduced in [0, p).
 // ----------------------------------------------------------------------------------------

@@ -93,6 +93,9 @@ struct WJob {
   int ngroup = 0;
   const uint8_t* ga8[2] = {nullptr, nullptr};
   const uint8_t* gb8[2] = {nullptr, nullptr};
+  // trimmed length word (poly_new_internal's len, 0 = all zero) written by the last inverse
+  // pass; the center kernel zeroes it first (nullptr: not wanted)
+  uint32_t* nz = nullptr;
 };
 constexpr int PLK_WAVE_MAX_JOBS = 12;   // jobs per launch of the wave engine (larger batches run in chunks)
 bool plk_wave_ntt_supported(int k);

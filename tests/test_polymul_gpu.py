@@ -82,6 +82,35 @@ def test_trailing_cancellation_and_zero(hip, oracle):
     assert hip.poly_mul(a, b) == oracle.poly_mul(a, b)
 
 
+@pytest.mark.parametrize("la,lb", [(8193, 8196), (8200, 8202), ((1 << 13) - 32 + 7, 33), (70000, 90000)])
+def test_trimmed_length_from_the_last_pass(hip, oracle, la, lb):
+    """The transform path takes the trimmed length (src/poly.h:20-38) out of its last inverse
+    pass: one store when the top coefficient a[la-1] b[lb-1] mod 17 is non-zero, else a block
+    maximum per tile.  Leading bytes that are 0 mod 17 (17, 34, 0) force the second form, on
+    wrapped shapes too (their top coefficients come from the direct fix-up)."""
+    import torch
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream()
+    work = torch.zeros(max(hip.poly_mul_workspace(la, lb), 4), dtype=torch.uint8, device=dev)
+    out = torch.zeros(la + lb - 1, dtype=torch.uint8, device=dev)
+    nz = torch.full((4,), 0x7FFFFFFF, dtype=torch.int32, device=dev)   # stale value: must be replaced
+    for ta, tb in [(None, None), (17, None), (None, 34), (0, 0), (17, 34)]:
+        a, b = gen.poly_inputs(la + 7 * lb, la, lb)
+        a, b = a.copy(), b.copy()
+        if ta is not None:
+            a[-1] = ta
+            a[-3:-1] = [0, 17]          # the next coefficients vanish too
+        if tb is not None:
+            b[-1] = tb
+        want = oracle.poly_mul(a, b) if la * lb <= (1 << 24) else oracle.poly_mul_ntt(a, b)
+        assert hip.poly_mul(a, b) == want, (ta, tb)
+        hip.poly_mul_dev(torch.from_numpy(a).to(dev), la, torch.from_numpy(b).to(dev), lb, out, nz, work, st)
+        torch.cuda.synchronize()
+        n = int(nz[0].item())
+        assert (n or 1) == len(want), (ta, tb, n, len(want))
+        assert bytes(out[:n or 1].cpu().numpy()) == want
+
+
 def test_empty_operand_mirrors_reference(hip):
     assert hip.poly_mul(b"", b"\x03\x04") == bytes([0])
 
