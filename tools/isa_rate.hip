@@ -25,6 +25,10 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
       if (OP == 5) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a[i]) : "s"(m));
       if (OP == 6) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(w[i]) : "v"(w[i]));
       if (OP == 7) asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(w[i]) : "v"(a[i]));
+      // gfx950 cross-lane swaps (the lane-swap center kernel): register pairs (i, i ^ 1), so
+      // 8 instructions per iteration as for the others
+      if (OP == 8) asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a[i]), "+v"(a[i ^ 1]));
+      if (OP == 9) asm volatile("v_permlane16_swap_b32 %0, %1" : "+v"(a[i]), "+v"(a[i ^ 1]));
     }
   }
   uint32_t s = 0;
@@ -63,5 +67,7 @@ int main() {
   printf("v_mul_f32      %.2f\n", run<5>(d));
   printf("v_mul_f64      %.2f\n", run<6>(d));
   printf("v_cvt_f64_u32  %.2f\n", run<7>(d));
+  printf("v_permlane32_swap_b32  %.2f\n", run<8>(d));
+  printf("v_permlane16_swap_b32  %.2f\n", run<9>(d));
   return 0;
 }
