@@ -390,49 +390,67 @@ __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, u
 namespace {
 struct RawPt { uint32_t x, y, inf; };
 
-__device__ __forceinline__ uint32_t r_add(uint32_t a, uint32_t b) { uint32_t s = a + b; return (s >= 101 ? s - 101 : s) & 0xFF; }
-__device__ __forceinline__ uint32_t r_sub(uint32_t a, uint32_t b) { int d = (int)a - (int)b; if (d < 0) d += 101; return (uint32_t)d & 0xFF; }
-__device__ __forceinline__ uint32_t r_mul(uint32_t a, uint32_t b) { return (a * b) % 101; }
-__device__ __forceinline__ uint32_t r_inv(uint32_t a) { return c_inv101[a % 101]; }
-__device__ __forceinline__ uint32_t r_red(uint32_t v) { return v % 101; }  // f101(uint64 of a byte)
+// inv: a^-1 mod 101 (0 -> 0), staged in LDS by the fold kernel (the serial lane's inverses are
+// then LDS reads, not constant-memory misses)
+struct RawOps {
+  const uint32_t* inv;
+  __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) const { uint32_t s = a + b; return (s >= 101 ? s - 101 : s) & 0xFF; }
+  __device__ __forceinline__ uint32_t sub(uint32_t a, uint32_t b) const { int d = (int)a - (int)b; if (d < 0) d += 101; return (uint32_t)d & 0xFF; }
+  __device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b) const { return (a * b) % 101; }
+  __device__ __forceinline__ uint32_t rinv(uint32_t a) const { return inv[a % 101]; }
+  __device__ __forceinline__ uint32_t red(uint32_t v) const { return v % 101; }  // f101(uint64 of a byte)
 
-__device__ RawPt r_double(RawPt a) {
-  if (a.inf || a.y == 0) return RawPt{0, 0, 1};
-  const uint32_t m = r_mul(r_mul(3, r_mul(a.x, a.x)), r_inv(r_mul(2, a.y)));
-  const uint32_t m2 = r_mul(m, m);
-  const uint32_t xr = r_sub(m2, r_mul(2, a.x));
-  const uint32_t yr = r_sub(r_mul(m, r_sub(r_mul(3, a.x), m2)), a.y);
-  return RawPt{r_red(xr), r_red(yr), 0};
-}
-
-__device__ RawPt r_addp(RawPt a, RawPt b) {
-  if (a.inf) return b;
-  if (b.inf) return a;
-  if (a.x == b.x) {
-    if (r_add(a.y, b.y) == 0) return RawPt{0, 0, 1};
-    return r_double(a);
+  __device__ RawPt dbl(RawPt a) const {
+    if (a.inf || a.y == 0) return RawPt{0, 0, 1};
+    const uint32_t m = mul(mul(3, mul(a.x, a.x)), rinv(mul(2, a.y)));
+    const uint32_t m2 = mul(m, m);
+    const uint32_t xr = sub(m2, mul(2, a.x));
+    const uint32_t yr = sub(mul(m, sub(mul(3, a.x), m2)), a.y);
+    return RawPt{red(xr), red(yr), 0};
   }
-  const uint32_t m = r_mul(r_sub(b.y, a.y), r_inv(r_sub(b.x, a.x)));
-  const uint32_t xr = r_sub(r_sub(r_mul(m, m), a.x), b.x);
-  const uint32_t yr = r_sub(r_mul(m, r_sub(a.x, xr)), a.y);
-  return RawPt{r_red(xr), r_red(yr), 0};
-}
+  __device__ RawPt addp(RawPt a, RawPt b) const {
+    if (a.inf) return b;
+    if (b.inf) return a;
+    if (a.x == b.x) {
+      if (add(a.y, b.y) == 0) return RawPt{0, 0, 1};
+      return dbl(a);
+    }
+    const uint32_t m = mul(sub(b.y, a.y), rinv(sub(b.x, a.x)));
+    const uint32_t xr = sub(sub(mul(m, m), a.x), b.x);
+    const uint32_t yr = sub(mul(m, sub(a.x, xr)), a.y);
+    return RawPt{red(xr), red(yr), 0};
+  }
+  // g1_mul (src/g1.h:91-103): LSB-first double-and-add over the scalar byte
+  __device__ RawPt mulp(RawPt run, uint32_t k) const {
+    RawPt term{0, 0, 1};
+    for (; k; k >>= 1) {
+      if (k & 1) term = addp(term, run);
+      run = dbl(run);
+    }
+    return term;
+  }
+};
 }  // namespace
 
 // The reference's fold for inputs with irregular encodings, exactly.  For canonical points the
 // raw formulas ARE the group law, so the fold's prefix up to the first irregular
 // point equals EXP[sum c_i LOG(P_i)]: one block sums that prefix in parallel (discrete logs
 // through the LDS table, 16 points per thread per chunk, stopping at the chunk that holds the
-// first irregular point), then one thread continues the raw fold from that point to the end.
-constexpr int FOLD_T = 1024, FOLD_E = 16;
+// first irregular point).  From that point on the fold is order-dependent: only the additions
+// acc = acc + term_i are serial.  The terms g1_mul(P_i, c_i) are independent, so waves 1-15
+// compute the next chunk of them into LDS while lane 0 of wave 0 folds the current chunk.
+constexpr int FOLD_T = 1024, FOLD_E = 16, FOLD_CH = 4096;
 __global__ __launch_bounds__(FOLD_T) void msm_serial_fold_kernel(const uint8_t* __restrict__ pts,
                                                                  const uint8_t* __restrict__ sc, uint64_t n,
                                                                  PlkMsmResult* res) {
   __shared__ uint32_t tab[TAB_ENTRIES];
   __shared__ uint32_t wsum[FOLD_T / PLK_WAVE];
+  __shared__ uint32_t invl[PLK_GF_P];
+  __shared__ uint32_t terms[2][FOLD_CH];   // packed x | y << 8 | inf << 16 (raw bytes)
   __shared__ unsigned long long s_first;
   if (blockIdx.x != 0) return;
   for (int i = threadIdx.x; i < TAB_ENTRIES; i += FOLD_T) tab[i] = c_ytab[i];
+  for (int i = threadIdx.x; i < PLK_GF_P; i += FOLD_T) invl[i] = c_inv101[i];
   if (threadIdx.x == 0) s_first = ~0ull;
   __syncthreads();
   uint32_t acc = 0;
@@ -465,20 +483,41 @@ __global__ __launch_bounds__(FOLD_T) void msm_serial_fold_kernel(const uint8_t* 
   const uint32_t ws = plk_wave_sum(acc);
   if ((threadIdx.x & (PLK_WAVE - 1)) == 0) wsum[threadIdx.x / PLK_WAVE] = ws;
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  uint32_t tot = 0;
-  for (int w = 0; w < FOLD_T / PLK_WAVE; w++) tot += wsum[w];
-  const uint32_t lg0 = tot % PLK_GROUP_ORDER;
-  RawPt a{c_exp[4 * lg0], c_exp[4 * lg0 + 1], c_exp[4 * lg0 + 2]};   // the fold over [0, first)
-  for (uint64_t i = first; i < n; i++) {
-    RawPt run{pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
-    RawPt term{0, 0, 1};
-    for (uint32_t k = sc[i]; k; k >>= 1) {
-      if (k & 1) term = r_addp(term, run);
-      run = r_double(run);
-    }
-    a = r_addp(a, term);
+  RawPt a{0, 0, 1};
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int w = 0; w < FOLD_T / PLK_WAVE; w++) tot += wsum[w];
+    const uint32_t lg0 = tot % PLK_GROUP_ORDER;
+    a = RawPt{c_exp[4 * lg0], c_exp[4 * lg0 + 1], c_exp[4 * lg0 + 2]};   // the fold over [0, first)
   }
+  const RawOps ops{invl};
+  if (first < n) {                      // uniform
+    auto fill = [&](uint32_t* buf, uint64_t base, uint32_t t0, uint32_t nt) {
+      for (uint32_t j = t0; j < (uint32_t)FOLD_CH && base + j < n; j += nt) {
+        const uint64_t i = base + j;
+        const RawPt t = ops.mulp(RawPt{pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]}, sc[i]);
+        buf[j] = t.x | t.y << 8 | t.inf << 16;
+      }
+    };
+    fill(terms[0], first, threadIdx.x, FOLD_T);
+    __syncthreads();
+    for (uint64_t c = 0;; c++) {
+      const uint64_t base = first + c * FOLD_CH, next = base + FOLD_CH;
+      if (threadIdx.x >= PLK_WAVE) {
+        if (next < n) fill(terms[(c + 1) & 1], next, threadIdx.x - PLK_WAVE, FOLD_T - PLK_WAVE);
+      } else if (threadIdx.x == 0) {
+        const uint32_t m = (uint32_t)(n - base < (uint64_t)FOLD_CH ? n - base : (uint64_t)FOLD_CH);
+        const uint32_t* tb = terms[c & 1];
+        for (uint32_t j = 0; j < m; j++) {
+          const uint32_t t = tb[j];
+          a = ops.addp(a, RawPt{t & 0xFFu, (t >> 8) & 0xFFu, t >> 16});
+        }
+      }
+      __syncthreads();
+      if (next >= n) break;
+    }
+  }
+  if (threadIdx.x != 0) return;
   res->g1[0] = (uint8_t)a.x;
   res->g1[1] = (uint8_t)a.y;
   res->g1[2] = (uint8_t)a.inf;

@@ -96,6 +96,34 @@ def test_irregular_in_2_22_points(hip, oracle, where):
     assert hip.msm_g1(pts, sc) == oracle.msm(pts, sc)
 
 
+def test_irregular_first_of_2_22_is_bounded(hip, oracle):
+    """The worst case of the raw fold: the first of 2^22 points irregular, so every addition is
+    order-dependent.  The g1_mul terms are computed in parallel (15 waves) while one lane folds
+    (src/srs.h:59-66); the device fold must stay within a few times the reference's own CPU
+    time for this input (~0.63 s, gcc -O2) -- one lane doing whole g1_mul chains took seconds."""
+    import time
+    import torch
+    c = load_golden("msm.json")["large"][7]
+    pts, sc = gen.msm_inputs(c["seed"], c["n"], c["kind"])
+    pts = pts.copy()
+    pts[0] = (7, 7, 1)                                  # identity flag with coordinates
+    dev = torch.device("cuda:0")
+    dp = torch.from_numpy(pts.reshape(-1).copy()).to(dev)
+    ds = torch.from_numpy(sc.copy()).to(dev)
+    res = torch.zeros(hip.MSM_RESULT_BYTES, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream()
+    hip.msm_g1_serial_dev(dp, ds, c["n"], res, st)     # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    hip.msm_g1_serial_dev(dp, ds, c["n"], res, st)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print("serial fold, 2^22 points, irregular first: %.3f s" % dt)
+    g = hip.MSM_G1_OFFSET
+    assert bytes(res[g:g + 3].cpu().numpy()) == oracle.msm(pts, sc)
+    assert dt < 2.5, dt
+
+
 def test_srs_eval_degree_check(hip):
     pts = np.tile(np.array([1, 2, 0], np.uint8), 4)
     with pytest.raises(ValueError):
