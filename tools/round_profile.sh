@@ -10,11 +10,14 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 500 python -m pytest tests -m gpu -q > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -30 $O/gpu_tests.log; exit 1; }
 tail -1 $O/gpu_tests.log
+# the PMC pass first: bench.py reads roofline.traffic from profiles/msm_pmc_latest.json only when
+# it was measured for the current kernel source, so the bench lines below carry it
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/pmc -o run -- python3 bench.py --profile-only > $O/pmc.out 2>&1 || exit 1
+python3 tools/pmc_summary.py $O/pmc/run_results.db msm_dlog_kernel --latest 22 40 $O/msm_pmc_latest.json > $O/msm_pmc.json || exit 1
+cp $O/msm_pmc_latest.json profiles/msm_pmc_latest.json
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail $O/bench.err; exit 1; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3 bench.py > $O/bench_traced.json 2> $O/bench_traced.err || exit 1
 python3 tools/kstats.py $O/trace/run_results.db --json $O/bench_kernel_stats.json > $O/bench_kernel_stats.txt || exit 1
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/pmc -o run -- python3 bench.py --profile-only > $O/pmc.out 2>&1 || exit 1
-python3 tools/pmc_summary.py $O/pmc/run_results.db msm_dlog_kernel --latest 22 40 $O/msm_pmc_latest.json > $O/msm_pmc.json || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prove -o run -- python3 tools/prove_bench.py 20 > $O/prove.json 2>&1 || exit 1
 python3 tools/prove_breakdown.py $O/prove/run_results.db > $O/prove_2^20_breakdown.txt || exit 1
 timeout -k 10 60 ./tools/bfly_peak > $O/bfly_peak.json || exit 1
