@@ -38,6 +38,7 @@
 __constant__ uint32_t c_ytab[512];             // E[idx], see above
 __constant__ __attribute__((aligned(16))) uint8_t c_exp[PLK_GROUP_ORDER * 4];  // EXP[k] = {x, y, inf, 0}
 __constant__ uint8_t c_inv101[PLK_GF_P];       // a^-1 mod 101 (0 -> 0), for the raw fold
+__constant__ uint32_t c_inv101w[PLK_GF_P];     // the same as words (scalar loads in the uniform fold)
 
 namespace {
 
@@ -390,14 +391,14 @@ __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, u
 namespace {
 struct RawPt { uint32_t x, y, inf; };
 
-// inv: a^-1 mod 101 (0 -> 0), staged in LDS by the fold kernel (the serial lane's inverses are
-// then LDS reads, not constant-memory misses)
+// inv: a^-1 mod 101 (0 -> 0), staged in LDS by the fold kernel for the per-lane term
+// computation; nullptr: the __constant__ table (wave-uniform folding: scalar-cache loads)
 struct RawOps {
   const uint32_t* inv;
   __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) const { uint32_t s = a + b; return (s >= 101 ? s - 101 : s) & 0xFF; }
   __device__ __forceinline__ uint32_t sub(uint32_t a, uint32_t b) const { int d = (int)a - (int)b; if (d < 0) d += 101; return (uint32_t)d & 0xFF; }
   __device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b) const { return (a * b) % 101; }
-  __device__ __forceinline__ uint32_t rinv(uint32_t a) const { return inv[a % 101]; }
+  __device__ __forceinline__ uint32_t rinv(uint32_t a) const { return inv ? inv[a % 101] : c_inv101w[a % 101]; }
   __device__ __forceinline__ uint32_t red(uint32_t v) const { return v % 101; }  // f101(uint64 of a byte)
 
   __device__ RawPt dbl(RawPt a) const {
@@ -483,12 +484,13 @@ __global__ __launch_bounds__(FOLD_T) void msm_serial_fold_kernel(const uint8_t* 
   const uint32_t ws = plk_wave_sum(acc);
   if ((threadIdx.x & (PLK_WAVE - 1)) == 0) wsum[threadIdx.x / PLK_WAVE] = ws;
   __syncthreads();
+  // the fold over [0, first): every lane of wave 0 holds it (wave-uniform, scalar registers)
   RawPt a{0, 0, 1};
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < PLK_WAVE) {
     uint32_t tot = 0;
     for (int w = 0; w < FOLD_T / PLK_WAVE; w++) tot += wsum[w];
-    const uint32_t lg0 = tot % PLK_GROUP_ORDER;
-    a = RawPt{c_exp[4 * lg0], c_exp[4 * lg0 + 1], c_exp[4 * lg0 + 2]};   // the fold over [0, first)
+    const uint32_t lg0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tot % PLK_GROUP_ORDER));
+    a = RawPt{c_exp[4 * lg0], c_exp[4 * lg0 + 1], c_exp[4 * lg0 + 2]};
   }
   const RawOps ops{invl};
   if (first < n) {                      // uniform
@@ -505,12 +507,25 @@ __global__ __launch_bounds__(FOLD_T) void msm_serial_fold_kernel(const uint8_t* 
       const uint64_t base = first + c * FOLD_CH, next = base + FOLD_CH;
       if (threadIdx.x >= PLK_WAVE) {
         if (next < n) fill(terms[(c + 1) & 1], next, threadIdx.x - PLK_WAVE, FOLD_T - PLK_WAVE);
-      } else if (threadIdx.x == 0) {
+      } else {
+        // wave 0 folds: 64 terms per LDS read (lane j holds term j), then term by term as
+        // wave-uniform values -- the addition runs on the scalar unit, its inverses come from
+        // the scalar cache (c_inv101)
         const uint32_t m = (uint32_t)(n - base < (uint64_t)FOLD_CH ? n - base : (uint64_t)FOLD_CH);
         const uint32_t* tb = terms[c & 1];
-        for (uint32_t j = 0; j < m; j++) {
-          const uint32_t t = tb[j];
-          a = ops.addp(a, RawPt{t & 0xFFu, (t >> 8) & 0xFFu, t >> 16});
+        const RawOps uni{nullptr};
+        for (uint32_t j0 = 0; j0 < m; j0 += PLK_WAVE) {
+          const uint32_t tv = j0 + threadIdx.x < m ? tb[j0 + threadIdx.x] : 0u;
+          const uint32_t cnt = m - j0 < (uint32_t)PLK_WAVE ? m - j0 : (uint32_t)PLK_WAVE;
+          for (uint32_t jj = 0; jj < cnt; jj++) {
+            const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)tv, (int)jj);
+            // (a is the same in every lane: read as scalars, the addition's branches and
+            // arithmetic stay on the scalar unit)
+            const RawPt au{(uint32_t)__builtin_amdgcn_readfirstlane((int)a.x),
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)a.y),
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)a.inf)};
+            a = uni.addp(au, RawPt{t & 0xFFu, (t >> 8) & 0xFFu, t >> 16});
+          }
         }
       }
       __syncthreads();
@@ -553,6 +568,9 @@ int plk_msm_upload_tables(const uint32_t* ytab, const uint8_t* exp4, const uint8
   PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_ytab), ytab, sizeof(uint32_t) * 512));
   PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_exp), exp4, PLK_GROUP_ORDER * 4));
   PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_inv101), inv101, PLK_GF_P));
+  uint32_t w[PLK_GF_P];
+  for (int i = 0; i < PLK_GF_P; i++) w[i] = inv101[i];
+  PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_inv101w), w, sizeof w));
   return PLK_OK;
 }
 
