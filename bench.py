@@ -333,6 +333,24 @@ def components(torch, hip, dev, st):
     out["ntt_2^20_forward_batch8"] = {"ms_per_launch": round(avg, 4),
                                       "Gelem_s": round(nb * (1 << k) / (avg * 1e-3) / 1e9, 2),
                                       "roofline": roofline_obj(nb * alg, avg, "8 transforms per launch")}
+    # C3 in the field poly_mul and the prover transform in: F29 (plk_ntt29_dev, lazy reduction,
+    # fully reduced outputs), single and 8 per launch
+    P29 = 7 * (1 << 26) + 1
+    b29 = [torch.randint(0, P29, (1 << k,), dtype=torch.int64, device=dev).to(torch.int32) for _ in range(4)]
+    for b in b29:
+        hip.ntt29_dev(b, k, False, st)
+    gr = graph_avg_ms(torch, lambda i, s: hip.ntt29_dev(b29[i % 4], k, False, s), 50)
+    avg, med = gr if gr else event_avg_ms(torch, st, lambda i: hip.ntt29_dev(b29[i % 4], k, False, st), 50)
+    out["ntt29_2^20_forward"] = {"ms": round(avg, 4), "Gelem_s": round((1 << k) / (avg * 1e-3) / 1e9, 2),
+                                 "passes": 2,
+                                 "roofline": roofline_obj(alg, avg, "SURVEY 8(d): u32 read + write once per element")}
+    b29 = [torch.randint(0, P29, (nb, 1 << k), dtype=torch.int64, device=dev).to(torch.int32) for _ in range(2)]
+    gr = graph_avg_ms(torch, lambda i, s: hip.ntt29_batch_dev(b29[i % 2], k, nb, False, s), 20)
+    avg, med = gr if gr else event_avg_ms(torch, st, lambda i: hip.ntt29_batch_dev(b29[i % 2], k, nb, False, st), 20)
+    out["ntt29_2^20_forward_batch8"] = {"ms_per_launch": round(avg, 4),
+                                        "Gelem_s": round(nb * (1 << k) / (avg * 1e-3) / 1e9, 2),
+                                        "roofline": roofline_obj(nb * alg, avg, "8 transforms per launch")}
+    del b29
     # poly_mul 2^19 x 2^19 -> 2^20 - 1 coefficients (device-resident)
     la = lb = 1 << 19
     a = torch.randint(0, 17, (la,), dtype=torch.int16, device=dev).to(torch.uint8)
@@ -347,9 +365,13 @@ def components(torch, hip, dev, st):
                                  "roofline": roofline_obj(la + lb + (la + lb - 1), avg,
                                                           "SURVEY 8(d): la + lb + (la + lb - 1) bytes of HF")}
     out.update(polyops_components(torch, hip, dev, st))
-    bfly = butterfly_roofline((1 << 19) * 20, out["ntt_2^20_forward"]["ms"], "bb_dif_Gbfly_s")
-    if bfly:
-        out["ntt_2^20_forward"]["roofline_butterfly"] = bfly
+    for key, peak, nt in (("ntt_2^20_forward", "bb_dif_Gbfly_s", 1), ("ntt_2^20_forward_batch8", "bb_dif_Gbfly_s", 8),
+                          ("ntt29_2^20_forward", "f29_dif_Gbfly_s", 1),
+                          ("ntt29_2^20_forward_batch8", "f29_dif_Gbfly_s", 8)):
+        c = out[key]
+        bfly = butterfly_roofline(nt * (1 << 19) * 20, c.get("ms", c.get("ms_per_launch")), peak)
+        if bfly:
+            c["roofline_butterfly"] = bfly
     out["prove_2^20_gates"] = prove_component(torch, hip, dev, 20)
     return out
 

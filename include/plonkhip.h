@@ -138,6 +138,12 @@ int plk_ntt_dev(uint32_t *d_data, int log_n, int inverse, void *stream);
 /* batch independent transforms of 2^log_n points, array b at d_data + b 2^log_n; the arrays
  * share each pass's launch (the prover's products run the same way). */
 int plk_ntt_batch_dev(uint32_t *d_data, int log_n, int batch, int inverse, void *stream);
+/* The same over F29 p = 7*2^26+1 -- the field poly_mul and the device prover transform in
+ * (lazy reduction inside, ~7 integer VALU per butterfly against ~10 for BabyBear): Montgomery
+ * form (R = 2^32) u32 < p in, fully reduced out, root of order 2^log_n = 3^((p-1)/2^log_n);
+ * log_n 13..26. */
+int plk_ntt29_dev(uint32_t *d_data, int log_n, int inverse, void *stream);
+int plk_ntt29_batch_dev(uint32_t *d_data, int log_n, int batch, int inverse, void *stream);
 
 /* ---- the ops around the hot path ---------------------------------
  * Byte-exact restatements of the reference's host ops on the GPU, for every byte value

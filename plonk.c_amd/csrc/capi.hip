@@ -586,6 +586,22 @@ int plk_ntt_batch_dev(uint32_t* d_data, int log_n, int batch, int inverse, void*
   return plk_ntt_launch(d_data, log_n, batch, inverse, pick(stream));
 }
 
+int plk_ntt29_dev(uint32_t* d_data, int log_n, int inverse, void* stream) {
+  int rc = ensure_dev();
+  if (rc) return rc;
+  return plk_ntt29_launch(d_data, log_n, 1, inverse, pick(stream));
+}
+
+int plk_ntt29_batch_dev(uint32_t* d_data, int log_n, int batch, int inverse, void* stream) {
+  int rc = ensure_dev();
+  if (rc) return rc;
+  if (!d_data || batch < 1) {
+    plk_set_error("plk_ntt29_batch_dev: null data or batch %d", batch);
+    return PLK_ERR_ARG;
+  }
+  return plk_ntt29_launch(d_data, log_n, batch, inverse, pick(stream));
+}
+
 // ---- the ops around the hot path -----------------------------------------
 size_t plk_poly_eval_workspace(int n) { return (size_t)128 * (n > 0 ? n : 1); }
 

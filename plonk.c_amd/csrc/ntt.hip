@@ -846,12 +846,22 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
 // Standalone forward NTT (DIF, natural -> bit-reversed), in place on Montgomery-form u32,
 // or inverse (DIT, bit-reversed -> natural, NOT scaled by N^-1).  Same passes as poly_mul.
 // batch independent arrays at d + b 2^k share each pass's launch (up to 12 per launch).
+// F29 (p = 7 2^26 + 1, the field poly_mul and the prover transform in): the wave engine only,
+// 2^13 .. 2^26 points, results fully reduced
+int plk_ntt29_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st) {
+  if (k < 13 || k > f29::TWO_ADICITY || batch < 1) {
+    plk_set_error("ntt29: log_n %d (13..%d), batch %d", k, f29::TWO_ADICITY, batch);
+    return PLK_ERR_RANGE;
+  }
+  return plk_wave_ntt_launch(d, k, batch, inverse, 1, st);
+}
+
 int plk_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st) {
   if (k < 1 || k > bb::TWO_ADICITY || batch < 1) {
     plk_set_error("ntt: log_n %d (1..%d), batch %d", k, bb::TWO_ADICITY, batch);
     return PLK_ERR_RANGE;
   }
-  if (plk_wave_ntt_supported(k)) return plk_wave_ntt_launch(d, k, batch, inverse, st);
+  if (plk_wave_ntt_supported(k)) return plk_wave_ntt_launch(d, k, batch, inverse, 0, st);
   // k <= 12: one workgroup-tile pass (lo = 0, a single tile holds the whole array)
   const Tw tw = inverse ? tw_inv() : tw_fwd();
   const Pass p{k, 0, k, 1};

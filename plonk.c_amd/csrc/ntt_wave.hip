@@ -128,6 +128,7 @@ struct FBB {
   // pointwise product's R^-1 is folded into the final scale, see ntt_group)
   __device__ static __forceinline__ uint32_t byte_val(uint32_t b) { return b % 17u; }
   __device__ static __forceinline__ uint32_t out17(uint32_t v, uint32_t ninv) { return bb::mmul(v, ninv) % 17u; }
+  __device__ static __forceinline__ uint32_t canon(uint32_t v) { return v; }   // always reduced
 };
 // F29 bounds.  Montgomery REDC of t < p 2^32 lands in [0, 2p); so a product of ANY u32 with a
 // twiddle w < p is < 2p, and so is the DIF difference term t = a w + b (p - w) (= (a - b) w
@@ -165,6 +166,8 @@ struct F29 {
   // a, b < 4p: reduce one below 2p so that a b < p 2^32
   __device__ static __forceinline__ uint32_t pmul(uint32_t a, uint32_t b) { return f29::mmul(a, f29::red2(b)); }
   __device__ static __forceinline__ uint32_t colf(uint32_t cl, uint32_t ch) { return f29::red1(f29::mmul(cl, ch)); }
+  // [0, 8p) -> [0, p): the stored result of a standalone transform
+  __device__ static __forceinline__ uint32_t canon(uint32_t v) { return f29::red1(f29::red2(red4(v))); }
   // Centered residues: a coefficient v in [0, 17) enters as v - 17 when v > 8, so every
   // convolution term is at most 64 in absolute value and a product is exact while
   // 64 min(la, lb) <= (p - 1) / 2 (min(la, lb) * 128 < p: up to 3,670,016 coefficients, four
@@ -533,6 +536,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
     uint32_t x = v[k];
     if constexpr (G::HIGH && COLT) x = F::mul(x, cl[k]);
     else if constexpr (G::HIGH) x = F::mul(x, F::colf(cl[k], ch[k]));
+    else x = F::canon(x);   // the lo = 0 pass is the last one of a standalone transform
     dt[G::template toff_k<G::NR - 1, false>(p, of, bf, k)] = x;
   }
 }
@@ -633,7 +637,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   for (int k = 0; k < G::E; k++) {
     const uint32_t o = G::template toff_k<G::NR - 1, true>(p, of, bf, k);
     if (!TO_U8) {
-      dt[o] = v[k];
+      dt[o] = F::canon(v[k]);   // (the standalone inverse's last pass; poly_mul's 3-pass middle one)
     } else {
       // poly_mul runs its inverse with the FORWARD roots (no inverse table in LDS): that
       // yields N c[-idx mod N], so the coefficient lands at the negated position
@@ -912,9 +916,9 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
   return PLK_OK;
 }
 
-template <int TB>
+template <int TB, class F>
 int wave_ntt_t(const WJobs& jobs, const WArrs& arrs, int nj, int k, int inverse, hipStream_t st) {
-  const PlkTwTables t = plk_ntt_tables();
+  const PlkTwTables t = F::ADIC == f29::TWO_ADICITY ? plk_ntt_tables29() : plk_ntt_tables();
   int Ms[4];
   const int np = wave_plan(k, TB, Ms);
   int lo[4];
@@ -922,8 +926,8 @@ int wave_ntt_t(const WJobs& jobs, const WArrs& arrs, int nj, int k, int inverse,
   for (int s = 0; s < np; s++) {
     const int i = inverse ? np - 1 - s : s;
     const WPass p{k, lo[i]};
-    const int rc = inverse ? inv_m<TB, false, FBB>(Ms[i], p, jobs, nj, to_wtw(t, true), 0u, st)
-                           : fwd_m<TB, false, FBB>(Ms[i], p, arrs, nj, fwd_wtw<FBB>(k), st);
+    const int rc = inverse ? inv_m<TB, false, F>(Ms[i], p, jobs, nj, to_wtw(t, true), 0u, st)
+                           : fwd_m<TB, false, F>(Ms[i], p, arrs, nj, fwd_wtw<F>(k), st);
     if (rc) return rc;
   }
   return PLK_OK;
@@ -978,7 +982,7 @@ int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, int field, u
 }
 
 // batch independent in-place transforms of 2^k points: array i at d + i 2^k, <= 12 per launch
-int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st) {
+int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, int field, hipStream_t st) {
   for (int j0 = 0; j0 < batch; j0 += WT_MAX_JOBS) {
     const int m = batch - j0 < WT_MAX_JOBS ? batch - j0 : WT_MAX_JOBS;
     WJobs w{};
@@ -986,7 +990,9 @@ int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t 
     for (int i = 0; i < m; i++) {
       w.j[i].A = w.j[i].C = a.a[i].d = d + ((uint64_t)(j0 + i) << k);
     }
-    const int rc = tile_bits(k) == 13 ? wave_ntt_t<13>(w, a, m, k, inverse, st) : wave_ntt_t<12>(w, a, m, k, inverse, st);
+    const bool t13 = tile_bits(k) == 13;
+    const int rc = field == 1 ? (t13 ? wave_ntt_t<13, F29>(w, a, m, k, inverse, st) : wave_ntt_t<12, F29>(w, a, m, k, inverse, st))
+                              : (t13 ? wave_ntt_t<13, FBB>(w, a, m, k, inverse, st) : wave_ntt_t<12, FBB>(w, a, m, k, inverse, st));
     if (rc) return rc;
   }
   return PLK_OK;

@@ -55,6 +55,7 @@ size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb);
 int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
                         uint32_t* d_nz, void* d_work, hipStream_t st);
 int plk_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st);
+int plk_ntt29_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st);
 struct PlkPolyMulJob {
   const uint8_t* a;
   uint64_t la;
@@ -102,7 +103,7 @@ bool plk_wave_ntt_supported(int k);
 // field 0 = BabyBear, 1 = F29 (lazy; only when every job's min(la, lb) * 256 < f29::P);
 // ninv = 2^-k mod p in normal form for that field
 int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, int field, uint32_t ninv, hipStream_t st);
-int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st);
+int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, int field, hipStream_t st);   // field 0 BabyBear, 1 F29
 int plk_wave_init_coltabs(void);    // after plk_ntt_init_tables' root tables
 void plk_wave_free_coltabs(void);
 

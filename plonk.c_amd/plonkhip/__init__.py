@@ -51,6 +51,8 @@ SIGNATURES = {
     "plk_poly_mul_batch_dev": (C.c_int, [_vp, C.c_int, _vp, _sz, _vp]),
     "plk_ntt_dev": (C.c_int, [_vp, C.c_int, C.c_int, _vp]),
     "plk_ntt_batch_dev": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, _vp]),
+    "plk_ntt29_dev": (C.c_int, [_vp, C.c_int, C.c_int, _vp]),
+    "plk_ntt29_batch_dev": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, _vp]),
     "plk_poly_eval": (C.c_int, [_u8p, _sz, C.c_uint8, _u8p]),
     "plk_poly_eval_batch": (C.c_int, [C.POINTER(_u8p), C.POINTER(_sz), _u8p, C.c_int, _u8p]),
     "plk_poly_eval_workspace": (_sz, [C.c_int]),
@@ -351,6 +353,16 @@ def ntt_dev(data, log_n, inverse=False, stream=None):
 def ntt_batch_dev(data, log_n, batch, inverse=False, stream=None):
     _check("plk_ntt_batch_dev", lib().plk_ntt_batch_dev(_ptr(data), int(log_n), int(batch), 1 if inverse else 0,
                                                         _stream(stream)))
+
+
+def ntt29_dev(data, log_n, inverse=False, stream=None):
+    """plk_ntt29_dev: the same transform over F29 (p = 7 2^26 + 1), log_n 13..26."""
+    _check("plk_ntt29_dev", lib().plk_ntt29_dev(_ptr(data), int(log_n), 1 if inverse else 0, _stream(stream)))
+
+
+def ntt29_batch_dev(data, log_n, batch, inverse=False, stream=None):
+    _check("plk_ntt29_batch_dev", lib().plk_ntt29_batch_dev(_ptr(data), int(log_n), int(batch),
+                                                            1 if inverse else 0, _stream(stream)))
 
 
 def parse_result(res_bytes):

@@ -1,5 +1,6 @@
-"""The standalone BabyBear NTT (plk_ntt_dev): forward DIF natural -> bit-reversed against an
-O(n^2) DFT at small sizes, forward/inverse round trip and linearity at 2^20-2^23."""
+"""The standalone NTTs -- BabyBear (plk_ntt_dev) and F29 (plk_ntt29_dev, the field of poly_mul
+and the prover): forward DIF natural -> bit-reversed against an O(n^2) DFT at small sizes and an
+independent numpy transform, forward/inverse round trip and linearity up to the 2-adicity."""
 import numpy as np
 import pytest
 
@@ -61,13 +62,13 @@ def test_roundtrip_and_linearity(hip, k):
     assert torch.equal(got, (a * n) % P)
 
 
-def ntt_dif_reference(x, k):
-    """Independent numpy DIF NTT over BabyBear (natural order in, bit-reversed out), on the
-    raw stored u32 values -- the transform commutes with the Montgomery scaling, so this is
-    exactly what the GPU must produce from the same stored words."""
+def ntt_dif_reference(x, k, P=P, gen=31):
+    """Independent numpy DIF NTT over BabyBear (or F29: P29, generator 3), natural order in,
+    bit-reversed out, on the raw stored u32 values -- the transform commutes with the
+    Montgomery scaling, so this is exactly what the GPU must produce from the same stored words."""
     a = x.astype(np.uint64) % P
     n = 1 << k
-    w = pow(31, (P - 1) >> k, P)
+    w = pow(gen, (P - 1) >> k, P)
     for s in range(k - 1, -1, -1):
         h = 1 << s
         ws_ = pow(w, 1 << (k - s - 1), P)
@@ -120,3 +121,47 @@ def test_batch_matches_single(hip, k, batch):
         hip.ntt_batch_dev(many, k, batch, inv, st)
         torch.cuda.synchronize()
         assert torch.equal(one, many), (k, batch, inv)
+
+
+# ---- F29 (plk_ntt29_dev): the field poly_mul and the device prover transform in ----------------
+P29 = 7 * (1 << 26) + 1
+
+
+@pytest.mark.parametrize("k", [13, 14, 17, 20, 21, 22, 23, 24, 26])
+def test_f29_forward_vs_numpy_reference(hip, k):
+    """Every pass plan (2^12 tiles to 2^20, 2^13 tiles above, 3-pass plans from 2^24) against
+    the independent transform; outputs fully reduced; the unscaled inverse brings back n x."""
+    import torch
+    rng = np.random.default_rng(200 + k)
+    x = rng.integers(0, P29, 1 << k, dtype=np.int64)
+    d = torch.from_numpy(x.astype(np.int32)).cuda()
+    st = torch.cuda.current_stream()
+    hip.ntt29_dev(d, k, False, st)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy().view(np.uint32).astype(np.uint64)
+    if k <= 23:
+        assert np.array_equal(got, ntt_dif_reference(x, k, P29, 3)), k
+    assert int(got.max()) < P29
+    hip.ntt29_dev(d, k, True, st)
+    torch.cuda.synchronize()
+    back = d.cpu().numpy().view(np.uint32).astype(np.uint64)
+    assert np.array_equal(back, (x.astype(np.uint64) * np.uint64(pow(2, k, P29))) % np.uint64(P29))
+
+
+def test_f29_batch_and_range(hip):
+    import torch
+    st = torch.cuda.current_stream()
+    k, batch = 20, 9
+    g = torch.Generator(device="cpu").manual_seed(29)
+    x = torch.randint(0, P29, (batch, 1 << k), generator=g, dtype=torch.int64).to(torch.int32).cuda()
+    for inv in (False, True):
+        one = x.clone()
+        for b in range(batch):
+            hip.ntt29_dev(one[b], k, inv, st)
+        many = x.clone()
+        hip.ntt29_batch_dev(many, k, batch, inv, st)
+        torch.cuda.synchronize()
+        assert torch.equal(one, many), inv
+    for bad in (12, 27):
+        with pytest.raises(hip.PlonkHipError):
+            hip.ntt29_dev(x[0], bad, False, st)

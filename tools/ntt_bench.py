@@ -28,6 +28,18 @@ for k in ((20,) if quick else (20, 22)):
     avg, med = event_avg_ms(torch, st, lambda i: hip.ntt_batch_dev(bb_[i % 2], k, nb, False, st), 20)
     out["ntt_fwd_2^%d_batch8_us" % k] = round(avg * 1e3, 2)
     out["ntt_fwd_2^%d_batch8_Gelem_s" % k] = round(nb * (1 << k) / (avg * 1e-3) / 1e9, 1)
+P29 = 7 * (1 << 26) + 1
+for k in ((20, 22) if quick else (16, 20, 22, 23)):
+    bufs = [torch.randint(0, P29, (1 << k,), dtype=torch.int64, device=dev).to(torch.int32) for _ in range(4)]
+    avg, med = event_avg_ms(torch, st, lambda i: hip.ntt29_dev(bufs[i % 4], k, False, st), 40)
+    out["ntt29_fwd_2^%d_us" % k] = round(avg * 1e3, 2)
+    out["ntt29_fwd_2^%d_Gelem_s" % k] = round((1 << k) / (avg * 1e-3) / 1e9, 1)
+for k in ((20,) if quick else (20, 22)):
+    nb = 8
+    bb_ = [torch.randint(0, P29, (nb, 1 << k), dtype=torch.int64, device=dev).to(torch.int32) for _ in range(2)]
+    avg, med = event_avg_ms(torch, st, lambda i: hip.ntt29_batch_dev(bb_[i % 2], k, nb, False, st), 20)
+    out["ntt29_fwd_2^%d_batch8_us" % k] = round(avg * 1e3, 2)
+    out["ntt29_fwd_2^%d_batch8_Gelem_s" % k] = round(nb * (1 << k) / (avg * 1e-3) / 1e9, 1)
 for la, lb in (((1 << 19, 1 << 19),) if quick else
                ((1 << 12, 1 << 12), (1 << 16, 1 << 16), (1 << 19, 1 << 19), (3 * (1 << 20) + 4, (1 << 20) + 3))):
     a = torch.randint(0, 17, (la,), dtype=torch.int16, device=dev).to(torch.uint8)
