@@ -34,7 +34,8 @@
 
 #ifndef PLK_NTT_DIAG
 #define PLK_NTT_DIAG 0        // tuning builds only: bit 0 skips the butterflies, bit 1 the LDS exchanges,
-                              // bit 2 makes them lane-linear (conflict-free, wrong data)
+                              // bit 2 makes them lane-linear (conflict-free, wrong data), bit 3 loads
+                              // one input byte per thread instead of E, bit 4 skips the column-table loads
 #endif
 
 namespace {
@@ -498,6 +499,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
       const uint32_t o = G::template toff_k<0, false>(p, o0, b0, k);
+      if ((PLK_NTT_DIAG & 8) && k > 0) { v[k] = (v[0] + k) & 0xFFu; continue; }
       v[k] = o < lim ? st[o] : 0u;
       if (!PLK_NTT_BYTE_LUT) v[k] = F::byte_val(v[k]);
     }
@@ -514,7 +516,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
       if constexpr (COLT) {
-        cl[k] = colt[G::template toff_k<G::NR - 1, false>(p, of, bf, k)];
+        cl[k] = (PLK_NTT_DIAG & 16) ? 0x12345u + k : colt[G::template toff_k<G::NR - 1, false>(p, of, bf, k)];
       } else {
         const uint32_t ex = G::col_exp(p, tile, bf + ((uint32_t)k << LF));
         cl[k] = tw.lo[ex & 4095u];
