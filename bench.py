@@ -323,7 +323,18 @@ def components(torch, hip, dev, st):
     alg = NTT_BYTES_PER_ELEM * (1 << k)
     out["ntt_2^20_forward"] = {"ms": round(avg, 4), "eager_ms": round(eag, 4),
                                "Gelem_s": round((1 << k) / (avg * 1e-3) / 1e9, 2), "passes": 2,
-                               "roofline": roofline_obj(alg, avg, "SURVEY 8(d): u32 read + write once per element")}
+                               "roofline": roofline_obj(alg, avg, "SURVEY 8(d): u32 read + write once per element"),
+                               "inputs": "4 rotating 4 MiB arrays: Infinity-Cache resident, as when a transform follows "
+                                         "the kernel that wrote its input; ms_cold: 136 arrays (544 MiB, twice the cache) rotated"}
+    # the same with cold inputs (SURVEY 8(d) cache caveat): 136 arrays (544 MiB > 2 x the 256 MiB
+    # Infinity Cache) rotated, every launch of a replay on a different array
+    ncold = 136
+    cold = torch.empty((ncold, 1 << k), dtype=torch.int32, device=dev)
+    cold.random_(0, 2013265921)
+    gr = graph_avg_ms(torch, lambda i, s: hip.ntt_dev(cold[i % ncold], k, False, s), ncold)
+    if gr:
+        out["ntt_2^20_forward"]["ms_cold"] = round(gr[1], 4)
+    del cold
     # the same transform, 8 independent arrays sharing each pass's launch (plk_ntt_batch_dev)
     nb = 8
     bb_ = [torch.randint(0, 2013265921, (nb, 1 << k), dtype=torch.int64, device=dev).to(torch.int32)
