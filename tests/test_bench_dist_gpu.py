@@ -1,0 +1,32 @@
+"""The multi-rank bench path (what the driver's N = 2/4/8 runs execute, one process per GPU over
+RCCL) rehearsed on the one GPU of a test box: two ranks over gloo sharing cuda:0, strong scaling
+(each 2^22-point MSM split by point range, plonkhip.dist.finish_sharded).  The line must carry the
+strong-scaling config and both correctness checks -- the first MSM against a single-GPU recompute
+and the reference's own 2^22-point golden through the sharded path."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_two_rank_strong_scaling_line():
+    env = dict(os.environ, PLK_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--msm-batch", "8", "--rotate-mib", "160",
+           "--no-components", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]          # rank 0 prints exactly one line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["steps"] == 3
+    assert d["config"]["points_per_gpu"] * 2 == d["config"]["points_per_msm"] == 1 << 22
+    assert d["checks"] == {"first_msm_single_gpu_recompute": True, "golden_2^22_reference": True}
+    assert d["irregular_inputs"] == 0 and d["value"] > 0
