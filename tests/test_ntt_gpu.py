@@ -127,7 +127,7 @@ def test_batch_matches_single(hip, k, batch):
 P29 = 7 * (1 << 26) + 1
 
 
-@pytest.mark.parametrize("k", [13, 14, 17, 20, 21, 22, 23, 24, 26])
+@pytest.mark.parametrize("k", [13, 14, 17, 20, 21, 22, 23, 24, 25, 26])
 def test_f29_forward_vs_numpy_reference(hip, k):
     """Every pass plan (2^12 tiles to 2^20, 2^13 tiles above, 3-pass plans from 2^24) against
     the independent transform; outputs fully reduced; the unscaled inverse brings back n x."""
