@@ -554,6 +554,12 @@ static bool blocked_shape(uint64_t la, uint64_t lb) {
 }
 static size_t blocked_ws(uint64_t la, uint64_t lb);
 
+// direct convolution + trim_kernel: both only plain-store their outputs (no atomics), so their
+// operands and outputs may live in mapped host memory (the host ABI's toy-size calls)
+bool plk_poly_mul_is_direct(uint64_t la, uint64_t lb) {
+  return la && lb && (la < lb ? la : lb) <= PLK_DIRECT_MAX && !blocked_shape(la, lb);
+}
+
 size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb) {
   if (la == 0 || lb == 0) return 0;
   if (blocked_shape(la, lb)) return blocked_ws(la, lb);

@@ -52,6 +52,7 @@ PlkTwTables plk_ntt_tables29(void);    // F29 (roots of order 2^26; lo/hi: w_{2^
 int plk_ntt_init_tables(void);
 void plk_ntt_free_tables(void);
 size_t plk_poly_mul_workspace_bytes(uint64_t la, uint64_t lb);
+bool plk_poly_mul_is_direct(uint64_t la, uint64_t lb);
 int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uint64_t lb, uint8_t* d_out,
                         uint32_t* d_nz, void* d_work, hipStream_t st);
 int plk_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st);
