@@ -168,3 +168,67 @@ def test_divide_device_api_exact_buffers(hip, oracle, kind):
     assert wq == oq and wr.rstrip(b"\x00") == orr.rstrip(b"\x00")
     lq, lr = lens.cpu().tolist()
     assert bytes(qh[:max(lq, 1)]) == wq and bytes(rh[:max(lr, 1)]) == wr
+
+
+def _tiny_cases(seed):
+    """host-call shapes on both sides of the 16 KiB toy-size path (capi.hip tiny_ok): evaluations
+    in batches over 12 (several launches), empty and raw-byte (>= 240: the reference-loop re-run)
+    polynomials, short-operand products with raw bytes and trailing cancellation"""
+    rng = np.random.default_rng(seed)
+    evals = []
+    for t in range(6):
+        n = int(rng.integers(1, 30))
+        polys = []
+        for _ in range(n):
+            ln = int(rng.integers(0, 3000 if t < 4 else 9000))
+            p = rng.integers(0, 17 if t % 2 else 256, ln).astype(np.uint8)
+            polys.append(p)
+        evals.append((polys, rng.integers(0, 256, n).astype(np.uint8)))
+    muls = []
+    for t in range(40):
+        la = int(rng.integers(1, 33))
+        lb = int(rng.integers(1, 20000 if t % 3 == 0 else 3000))
+        a = rng.integers(0, 17 if t % 2 else 256, la).astype(np.uint8)
+        b = rng.integers(0, 17, lb).astype(np.uint8)
+        if t % 5 == 0:
+            b[-1] = 0   # trailing zero: the trimmed length comes from the trim pass
+        muls.append((a, b) if t % 4 else (b, a))
+    return evals, muls
+
+
+def test_toy_size_calls_vs_oracle(hip, oracle):
+    evals, muls = _tiny_cases(5)
+    for polys, xs in evals:
+        got = hip.poly_eval_batch(polys, xs)
+        assert list(got) == [oracle.poly_eval(p, x) for p, x in zip(polys, xs)]
+    for a, b in muls:
+        assert hip.poly_mul(a, b) == oracle.poly_mul(a, b), (len(a), len(b))
+
+
+def test_toy_size_path_matches_staged_path(hip):
+    """PLK_TINY=0 (every host call staged through device copies) in a child process gives the
+    same bytes as the mapped-memory path of this process"""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, json; sys.path[:0] = [%r, %r, %r]; import torch; import plonkhip as h; h.init(0); "
+            "import test_polyops_gpu as t; print(json.dumps(t._child_digest(h)))"
+            % (os.path.join(root, "plonk.c_amd"), os.path.join(root, "tests"), os.path.join(root, "tests", "golden")))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, PLK_TINY="0"), capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1]) == _child_digest(hip)
+
+
+def _child_digest(h):
+    import hashlib
+    evals, muls = _tiny_cases(9)
+    m = hashlib.sha256()
+    for polys, xs in evals:
+        m.update(bytes(h.poly_eval_batch(polys, xs)))
+    for a, b in muls:
+        m.update(h.poly_mul(a, b))
+    return m.hexdigest()
