@@ -226,6 +226,15 @@ int plk_prover_prove(plk_prover_t *p, const plk_circuit_t *circuit, const uint8_
  * Without PLK_PROVE_STRICT non-zero remainders are tolerated (synthetic inputs). */
 int plk_prover_rounds_dev(plk_prover_t *p, const uint8_t *const d_polys[13], const uint8_t chal[5],
                           const uint8_t rand9[9], int flags, uint8_t proof[34]);
+/* Preprocessed circuit (PLONK's preprocessed input; the reference re-derives it inside every
+ * plonk_prove, src/plonk.h:386-503): the forward transforms round 3 needs of the fixed circuit
+ * polynomials q_o q_m q_l q_r s_sigma_3 l_1_x (d_polys indices 3 4 5 6 10 12, device-resident,
+ * zero padded to n) are computed once here.  plk_prover_rounds_dev with PLK_PROVE_PREPROCESSED
+ * then uses them for the entries whose address equals the one given here; the bytes at those
+ * addresses must not change while they are in use (call again after a change; d_polys = NULL
+ * drops them).  Proof bytes are identical with and without. */
+#define PLK_PROVE_PREPROCESSED 2
+int plk_prover_preprocess(plk_prover_t *p, const uint8_t *const d_polys[13]);
 
 #ifdef __cplusplus
 }

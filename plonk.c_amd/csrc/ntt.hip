@@ -612,8 +612,14 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
   }
   uint32_t* W = (uint32_t*)d_work;
   int slot[64][2], refs[128] = {0};
+  bool fixb[64];   // b's forward transform supplied (PlkPolyMulJob::bt) for this k and field
+  for (int i = 0; i < m; i++) fixb[i] = g[i].bt && g[i].bt_k == k && g[i].bt_field == (use29 ? 1 : 0);
   for (int i = 0; i < m; i++)
     for (int s = 0; s < 2; s++) {
+      if (s && fixb[i]) {
+        slot[i][1] = -1;
+        continue;
+      }
       const uint8_t* ptr = s ? g[i].b : g[i].a;
       const uint64_t len = s ? g[i].lb : g[i].la;
       slot[i][s] = 2 * i + s;
@@ -649,6 +655,10 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
     w[i] = WJob{j.a, j.b, j.la, j.lb, j.out, j.la + j.lb - 1 - e, W + ((size_t)slot[i][0] << k),
                 W + ((size_t)slot[i][1] << k), W + ((size_t)cslot[i] << k)};
     w[i].ntop = (int)e;
+    if (fixb[i]) {
+      w[i].B = const_cast<uint32_t*>(j.bt);   // (read only)
+      w[i].bfix = 1;
+    }
   }
   if (m == 1) w[0].nz = d_nz;
   // sum groups: a member (acc) adds its center output into its leader's first inverse pass
@@ -768,6 +778,25 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
   const PlkPolyMulJob job{d_a, la, d_b, lb, d_out};
   // (the trimmed length comes out of the last inverse pass: no trim_kernel launch)
   return ntt_group(&job, 1, k, e ? &e : nullptr, d_work, st, d_nz);
+}
+
+int plk_poly_mul_transform_plan(uint64_t la, uint64_t lb, int* field) {
+  if (!la || !lb || blocked_shape(la, lb)) return -1;
+  const uint64_t mn = la < lb ? la : lb;
+  const int k = product_plan(la, lb, nullptr);
+  if (mn <= PLK_DIRECT_MAX || k <= PLK_SMALL_LOG || !plk_wave_ntt_supported(k)) return -1;
+  const char* e = getenv("PLK_NTT_NO_F29");
+  const bool use29 = !(e && atoi(e) != 0) && k <= f29::TWO_ADICITY && mn * 128 < f29::P;
+  if (field) *field = use29 ? 1 : 0;
+  return k;
+}
+
+int plk_poly_mul_pretransform(const uint8_t* d_b, uint64_t lb, int k, int field, uint32_t* d_out, hipStream_t st) {
+  if (field == 1 && k > f29::TWO_ADICITY) {
+    plk_set_error("pretransform: 2^%d is beyond F29's roots", k);
+    return PLK_ERR_RANGE;
+  }
+  return plk_wave_pretransform(d_b, lb, k, field, d_out, st);
 }
 
 // Several independent products: direct / one-workgroup ones one by one, the NTT ones grouped

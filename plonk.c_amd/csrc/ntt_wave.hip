@@ -714,13 +714,37 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
     }
     __syncthreads();
     G::template pass<false, false>(va, tid, bufs, 0, Tf);
-    G::template pass<false, false>(vb, tid, bufs, G::XCH, Tf);
+    // (bfix: b's transform is finished -- plk_wave_pretransform stored this pass's output
+    // registers where their inputs were read -- so its lo = 0 pass is skipped)
+    if (!jobs.j[job].bfix) G::template pass<false, false>(vb, tid, bufs, G::XCH, Tf);
 #pragma unroll
     for (int k = 0; k < G::E; k++) va[k] = F::pmul(va[k], vb[k]);
     G::template pass<true, false>(va, tid, bufs, 2 * G::XCH, Tf);
 #pragma unroll
     for (int k = 0; k < G::E; k++) dc[G::index(p, tile, bf + ((uint32_t)k << LF))] = va[k];
   }
+}
+
+// The lo = 0 forward pass of a fixed operand, exactly as wt_center_kernel runs it on b, each
+// thread storing its output registers where it read its inputs (so a later center launch loads
+// them unchanged: WJob::bfix).  In place: every position is read and written by one thread.
+template <int TB, int R, class F>
+__global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_fixfwd_kernel(WPass p, uint32_t* d,
+                                                                                                    WTw twf) {
+  using G = Eng<TB, R, TB, F>;
+  __shared__ uint32_t Tlds[1 << TB];
+  __shared__ uint32_t bufs[(G::DBUF ? 2 : 1) * G::BUF];
+  const uint32_t tid = threadIdx.x, tile = blockIdx.x;
+  const uint32_t b0 = G::template base_q<0>(tid, false);
+  constexpr int L0 = G::lbq(0, false);
+  uint32_t v[G::E];
+#pragma unroll
+  for (int k = 0; k < G::E; k++) v[k] = d[G::index(p, tile, b0 + ((uint32_t)k << L0))];
+  load_pass_tw<TB, G::NT>(Tlds, twf.small);
+  __syncthreads();
+  G::template pass<false, false>(v, tid, bufs, G::XCH, Tlds);
+#pragma unroll
+  for (int k = 0; k < G::E; k++) d[G::index(p, tile, b0 + ((uint32_t)k << L0))] = v[k];
 }
 
 // Column-factor table of a 2-pass plan (lo = TB, M = k - TB): entry i = the high pass's factor
@@ -889,7 +913,7 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
   WArrs arrs{};
   int na = 0;
   for (int j = 0; j < nj; j++)
-    for (int s = 0; s < 2; s++) {
+    for (int s = 0; s < (jobs.j[j].bfix ? 1 : 2); s++) {   // (a finished b has no forward passes)
       const WArr a = s ? WArr{jobs.j[j].B, jobs.j[j].b8, jobs.j[j].lb} : WArr{jobs.j[j].A, jobs.j[j].a8, jobs.j[j].la};
       bool seen = false;
       for (int q = 0; q < na; q++) seen |= arrs.a[q].d == a.d;
@@ -915,6 +939,28 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
                 : inv_m<TB, false, F>(Ms[i], p, jj, nj, twf, 0u, st);
     if (rc) return rc;
   }
+  return PLK_OK;
+}
+
+// b's forward transform for WJob::bfix: the forward passes of a product (bytes in), then the
+// center's lo = 0 pass stored in its register order
+template <int TB, class F>
+int wave_pretransform_t(const uint8_t* b8, uint64_t lb, int k, uint32_t* d, hipStream_t st) {
+  const WTw twf = fwd_wtw<F>(k);
+  int Ms[4];
+  const int np = wave_plan(k, TB, Ms);
+  int lo[4];
+  for (int i = 0, top = k; i < np; i++) { lo[i] = top - Ms[i]; top = lo[i]; }
+  WArrs arrs{};
+  arrs.a[0] = WArr{d, b8, lb};
+  for (int i = 0; i < np - 1; i++) {
+    const WPass p{k, lo[i]};
+    const int rc = i == 0 ? fwd_m<TB, true, F>(Ms[i], p, arrs, 1, twf, st) : fwd_m<TB, false, F>(Ms[i], p, arrs, 1, twf, st);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL((wt_fixfwd_kernel<TB, wt_rc(TB), F>), dim3((unsigned)((1ull << k) >> TB)), dim3(wt_ntc(TB)), 0, st,
+                     WPass{k, 0}, d, twf);
+  PLK_HIP(hipGetLastError());
   return PLK_OK;
 }
 
@@ -981,6 +1027,16 @@ int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, int field, u
     if (rc) return rc;
   }
   return PLK_OK;
+}
+
+int plk_wave_pretransform(const uint8_t* b8, uint64_t lb, int k, int field, uint32_t* d_out, hipStream_t st) {
+  if (!plk_wave_ntt_supported(k) || lb == 0 || lb > (1ull << k)) {
+    plk_set_error("pretransform: %llu coefficients at 2^%d", (unsigned long long)lb, k);
+    return PLK_ERR_ARG;
+  }
+  const bool t13 = tile_bits(k) == 13;
+  return field == 1 ? (t13 ? wave_pretransform_t<13, F29>(b8, lb, k, d_out, st) : wave_pretransform_t<12, F29>(b8, lb, k, d_out, st))
+                    : (t13 ? wave_pretransform_t<13, FBB>(b8, lb, k, d_out, st) : wave_pretransform_t<12, FBB>(b8, lb, k, d_out, st));
 }
 
 // batch independent in-place transforms of 2^k points: array i at d + i 2^k, <= 12 per launch

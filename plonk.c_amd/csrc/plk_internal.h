@@ -67,9 +67,20 @@ struct PlkPolyMulJob {
   // members of the same shape, all of one transform size; the members' out is not written).
   // The sum is exact while it fits the field (the caller's bound).
   int acc = 0;
+  // optional: b's forward transform computed beforehand (plk_poly_mul_pretransform with the
+  // same bytes, bt_k and bt_field): used when this product runs at 2^bt_k in field bt_field,
+  // which skips b's forward passes; ignored otherwise (the product is the same either way)
+  const uint32_t* bt = nullptr;
+  int bt_k = 0, bt_field = -1;
 };
 int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, size_t work_bytes, hipStream_t st);
 bool plk_poly_mul_summable(uint64_t la, uint64_t lb);
+// transform size (log2) and field (1 F29, 0 BabyBear) a wave-engine product of this shape runs
+// at on its own (sum groups may force BabyBear); -1 when it does not use the wave engine
+int plk_poly_mul_transform_plan(uint64_t la, uint64_t lb, int* field);
+// the forward transform of b (2^k words into d_out, in the center kernel's load positions) for
+// PlkPolyMulJob::bt
+int plk_poly_mul_pretransform(const uint8_t* d_b, uint64_t lb, int k, int field, uint32_t* d_out, hipStream_t st);
 
 // ntt_wave.hip (transforms of 2^13 .. 2^27 points).  One product job: u32 work arrays A, B
 // (2^k each; a batch's jobs may share one when their operands are the same bytes), byte
@@ -81,7 +92,7 @@ struct WJob {
   uint8_t* out8;
   uint64_t out_len;                // outputs of the cyclic transform: min(la + lb - 1, 2^k)
   uint32_t* A;
-  uint32_t* B;
+  uint32_t* B;                     // (bfix: b's finished forward transform, plk_wave_pretransform)
   uint32_t* C = nullptr;           // center output and inverse work array (read by no other job)
   // sum groups: the leader's inverse passes add the members' center outputs (linear), the
   // members run no inverse pass of their own
@@ -98,6 +109,7 @@ struct WJob {
   // trimmed length word (poly_new_internal's len, 0 = all zero) written by the last inverse
   // pass; the center kernel zeroes it first (nullptr: not wanted)
   uint32_t* nz = nullptr;
+  int bfix = 0;                    // B holds a plk_poly_mul_pretransform result
 };
 constexpr int PLK_WAVE_MAX_JOBS = 12;   // jobs per launch of the wave engine (larger batches run in chunks)
 bool plk_wave_ntt_supported(int k);
@@ -105,6 +117,7 @@ bool plk_wave_ntt_supported(int k);
 // ninv = 2^-k mod p in normal form for that field
 int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, int field, uint32_t ninv, hipStream_t st);
 int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, int field, hipStream_t st);   // field 0 BabyBear, 1 F29
+int plk_wave_pretransform(const uint8_t* b8, uint64_t lb, int k, int field, uint32_t* d_out, hipStream_t st);
 int plk_wave_init_coltabs(void);    // after plk_ntt_init_tables' root tables
 void plk_wave_free_coltabs(void);
 

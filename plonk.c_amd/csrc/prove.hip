@@ -1120,6 +1120,14 @@ struct plk_prover {
   // mapped pinned host memory: 64 proof bytes + NSTAT status words (trim_pack_kernel)
   uint8_t* h_res = nullptr;
   uint8_t* d_res_host = nullptr;   // its device address
+  // preprocessed circuit (plk_prover_preprocess): the round-3 forward transforms of the fixed
+  // polynomials q_o q_m q_l q_r s_sigma_3 l_1_x (PlkPolyMulJob::bt), for the addresses given
+  struct Fixed {
+    const uint8_t* src = nullptr;   // the d_polys entry it was computed from
+    uint32_t* t = nullptr;          // 2^k words
+    int k = 0, field = -1;
+  } fix[13];
+  uint32_t* fix_mem = nullptr;
 };
 
 namespace {
@@ -1483,6 +1491,7 @@ void plk_prover_destroy(plk_prover_t* P) {
   if (P->st) (void)hipStreamSynchronize(P->st);
   (void)hipFree(P->mem);
   if (P->h_res) (void)hipHostFree(P->h_res);
+  (void)hipFree(P->fix_mem);
   if (P->st) (void)hipStreamDestroy(P->st);
   delete P;
   plk_ctx_release();
@@ -1496,7 +1505,7 @@ namespace {
 
 // rounds 1-5 (src/plonk.h:277-655) on polys[13] = f_a f_b f_c q_o q_m q_l q_r q_c s1 s2 s3 acc_x l_1_x
 // (each of length <= n, zero padded to n).  Enqueued on P->st; status words in P->d_stat.
-int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const uint8_t rnd[9]) {
+int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const uint8_t rnd[9], bool pre = false) {
   const uint64_t n = P->n;
   const Lens L = lens_for(n, P->zh_len);
   const uint8_t *FA = pl[0], *FB = pl[1], *FC = pl[2], *QO = pl[3], *QM = pl[4], *QL = pl[5], *QR = pl[6],
@@ -1575,7 +1584,7 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     // F29's centered range: 3 * 64 n <= (p - 1) / 2 (n <= 1,223,338)
     const int lin = plk_poly_mul_summable(L.la, n) && (uint64_t)3 * L.la * 128 < f29::P ? 1 : 0;
     P->lin_sum = lin;
-    const PlkPolyMulJob g1[] = {{cA, L.la, cB, L.la, P->AB},      {cA, L.la, QL, n, P->AQL},
+    PlkPolyMulJob g1[] = {{cA, L.la, cB, L.la, P->AB},      {cA, L.la, QL, n, P->AQL},
                                 {cB, L.la, QR, n, P->BQR, lin},   {cC, L.la, QO, n, P->CQO, lin},
                                 {P->A2, L.la, P->B2, L.la, P->T2a}, {P->A3, L.la, P->B3, L.la, P->T3a},
                                 {P->Z1, L.lz1, L1, n, P->T4},
@@ -1589,10 +1598,22 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
                                 // come in one batch (associativity over GF(17); the centered F29
                                 // residues hold the 2n x 2n products exactly)
                                 {P->C2, L.la, cZ, L.lzx, P->T2b}, {P->C3, L.la, P->ZW, L.lzw, P->T3b}};
+    PlkPolyMulJob g2[] = {{P->AB, L.lab, QM, n, P->ABQM},
+                          {P->T2a, L.l2a, P->T2b, L.la + L.lzx - 1, P->T2},
+                          {P->T3a, L.l2a, P->T3b, L.la + L.lzw - 1, P->T3}};
+    if (pre) {   // preprocessed circuit: the fixed b operands' transforms (plk_prover_preprocess)
+      PlkPolyMulJob* const js[] = {&g1[1], &g1[2], &g1[3], &g1[6], &g1[7], &g2[0]};
+      const int which[] = {5, 6, 3, 12, 10, 4};   // q_l q_r q_o l_1_x s_sigma_3 q_m
+      for (int i = 0; i < 6; i++) {
+        const plk_prover::Fixed& f = P->fix[which[i]];
+        if (f.t && f.src == pl[which[i]] && js[i]->b == pl[which[i]]) {
+          js[i]->bt = f.t;
+          js[i]->bt_k = f.k;
+          js[i]->bt_field = f.field;
+        }
+      }
+    }
     RC(plk_poly_mul_batch_launch(g1, 10, P->work, P->work_bytes, P->st));
-    const PlkPolyMulJob g2[] = {{P->AB, L.lab, QM, n, P->ABQM},
-                                {P->T2a, L.l2a, P->T2b, L.la + L.lzx - 1, P->T2},
-                                {P->T3a, L.l2a, P->T3b, L.la + L.lzw - 1, P->T3}};
     RC(plk_poly_mul_batch_launch(g2, 3, P->work, P->work_bytes, P->st));
   }
   // t(x) = numerator / Z_H; t_lo / t_mid / t_hi = poly_slice(t_x, ...) with part n + 2
@@ -1741,9 +1762,50 @@ int plk_prover_rounds_dev(plk_prover_t* P, const uint8_t* const d_polys[13], con
   if (!P || !d_polys || !chal || !rand9) { plk_set_error("plk_prover_rounds_dev: NULL argument"); return PLK_ERR_ARG; }
   for (int i = 0; i < 13; i++)
     if (!d_polys[i]) { plk_set_error("plk_prover_rounds_dev: polynomial %d is NULL", i); return PLK_ERR_ARG; }
-  int rc = rounds(P, d_polys, chal, rand9);
+  int rc = rounds(P, d_polys, chal, rand9, (flags & PLK_PROVE_PREPROCESSED) != 0);
   if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
   return finish(P, (flags & PLK_PROVE_STRICT) != 0, 0, proof);
+}
+
+int plk_prover_preprocess(plk_prover_t* P, const uint8_t* const d_polys[13]) {
+  if (!P) { plk_set_error("plk_prover_preprocess: NULL prover"); return PLK_ERR_ARG; }
+  PLK_HIP(hipStreamSynchronize(P->st));   // (no round may still read the old transforms)
+  for (auto& f : P->fix) f = plk_prover::Fixed{};
+  (void)hipFree(P->fix_mem);
+  P->fix_mem = nullptr;
+  if (!d_polys) return PLK_OK;   // dropped
+  const uint64_t n = P->n;
+  const Lens L = lens_for(n, P->zh_len);
+  // the round-3 products with a fixed b (rounds(): g1[1..3], g1[6], g1[7], g2[0]) and their a
+  // operands' upper-bound lengths
+  const int which[] = {5, 6, 3, 12, 10, 4};   // q_l q_r q_o l_1_x s_sigma_3 q_m
+  const uint64_t la[] = {L.la, L.la, L.la, L.lz1, L.lzx, L.lab};
+  size_t words = 0;
+  int ks[6], fs[6];
+  for (int i = 0; i < 6; i++) {
+    if (!d_polys[which[i]]) { plk_set_error("plk_prover_preprocess: polynomial %d is NULL", which[i]); return PLK_ERR_ARG; }
+    ks[i] = plk_poly_mul_transform_plan(la[i], n, &fs[i]);
+    if (ks[i] > 0) words += (size_t)1 << ks[i];
+  }
+  if (!words) return PLK_OK;   // (small circuits: no product runs through the transform engine)
+  if (hipMalloc((void**)&P->fix_mem, 4 * words) != hipSuccess) {
+    P->fix_mem = nullptr;
+    plk_set_error("plk_prover_preprocess: hipMalloc(%zu) failed", 4 * words);
+    return PLK_ERR_NOMEM;
+  }
+  uint32_t* t = P->fix_mem;
+  for (int i = 0; i < 6; i++) {
+    if (ks[i] <= 0) continue;
+    const int rc = plk_poly_mul_pretransform(d_polys[which[i]], n, ks[i], fs[i], t, P->st);
+    if (rc) {
+      plk_prover_preprocess(P, nullptr);
+      return rc;
+    }
+    P->fix[which[i]] = plk_prover::Fixed{d_polys[which[i]], t, ks[i], fs[i]};
+    t += (size_t)1 << ks[i];
+  }
+  PLK_HIP(hipStreamSynchronize(P->st));
+  return PLK_OK;
 }
 
 int plk_prover_prove(plk_prover_t* P, const plk_circuit_t* c, const uint8_t chal[5], const uint8_t rand9[9],

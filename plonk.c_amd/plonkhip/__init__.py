@@ -68,9 +68,11 @@ SIGNATURES = {
     "plk_prover_device_bytes": (_sz, [_vp]),
     "plk_prover_prove": (C.c_int, [_vp, _vp, _u8p, _u8p, _u8p]),
     "plk_prover_rounds_dev": (C.c_int, [_vp, C.POINTER(_vp), _u8p, _u8p, C.c_int, _u8p]),
+    "plk_prover_preprocess": (C.c_int, [_vp, C.POINTER(_vp)]),
 }
 
 PLK_PROVE_STRICT = 1
+PLK_PROVE_PREPROCESSED = 2
 
 
 class PlonkDesc(C.Structure):
@@ -410,11 +412,19 @@ class Prover:
         _check("plk_prover_prove", lib().plk_prover_prove(self._h, C.byref(cir), _p(ch), _p(rd), _p(out)))
         return bytes(out)
 
-    def rounds_dev(self, polys, chal, rand, strict=False):
-        """polys: 13 device tensors / pointers (n bytes each)."""
+    def rounds_dev(self, polys, chal, rand, strict=False, preprocessed=False):
+        """polys: 13 device tensors / pointers (n bytes each).  preprocessed: use the fixed
+        polynomials' transforms from `preprocess` (same addresses, unchanged bytes)."""
         arr = (_vp * 13)(*[_ptr(p) for p in polys])
         ch, rd = _u8(chal), _u8(rand)
         out = np.zeros(34, np.uint8)
+        flags = (PLK_PROVE_STRICT if strict else 0) | (PLK_PROVE_PREPROCESSED if preprocessed else 0)
         _check("plk_prover_rounds_dev", lib().plk_prover_rounds_dev(
-            self._h, arr, _p(ch), _p(rd), PLK_PROVE_STRICT if strict else 0, _p(out)))
+            self._h, arr, _p(ch), _p(rd), flags, _p(out)))
         return bytes(out)
+
+    def preprocess(self, polys):
+        """plk_prover_preprocess: the round-3 transforms of q_o q_m q_l q_r s_sigma_3 l_1_x
+        (entries 3 4 5 6 10 12 of the 13 device polys); None drops them."""
+        arr = None if polys is None else (_vp * 13)(*[_ptr(p) for p in polys])
+        _check("plk_prover_preprocess", lib().plk_prover_preprocess(self._h, arr))

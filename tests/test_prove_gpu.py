@@ -195,3 +195,36 @@ def test_rounds_2_16_tiles13_vs_oracle(hip, oracle, tmp_path):
                        env=env, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().splitlines()[-1] == c["want"].hex()
+
+
+def test_rounds_preprocessed_vs_golden(hip):
+    """Config C5 with a preprocessed circuit (plk_prover_preprocess: the six fixed polynomials'
+    round-3 transforms computed once): the same proof bytes as the golden, repeatedly, and the
+    plain path unchanged beside it; a fixed polynomial moved to another address is transformed
+    in the call again (its stale transform is not used)."""
+    g = load_golden("prove_2_20.json")
+    n = g["n"]
+    polys, chal, rnd, zh, pts = _synthetic(n, g["seed"], g["srs_len"])
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    pr.preprocess(dev)
+    for _ in range(2):
+        assert pr.rounds_dev(dev, chal, rnd, preprocessed=True).hex() == g["proof"]
+    assert pr.rounds_dev(dev, chal, rnd).hex() == g["proof"]
+    moved = list(dev)
+    moved[5] = dev[5].clone()                       # q_l at a new address
+    assert pr.rounds_dev(moved, chal, rnd, preprocessed=True).hex() == g["proof"]
+    pr.preprocess(None)
+    assert pr.rounds_dev(dev, chal, rnd, preprocessed=True).hex() == g["proof"]
+
+
+@pytest.mark.parametrize("n,seed", [(1 << 16, 41), (1 << 12, 7), (64, 3)])
+def test_rounds_preprocessed_vs_plain(hip, n, seed):
+    """Preprocessed and plain provers agree at sizes whose round-3 products run at 2^13..2^19
+    transforms (12- and 13-bit tiles) and at a size with no transform-engine product at all."""
+    polys, chal, rnd, zh, pts = _synthetic(n, seed, 2 * n + 8)
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    want = pr.rounds_dev(dev, chal, rnd)
+    pr.preprocess(dev)
+    assert pr.rounds_dev(dev, chal, rnd, preprocessed=True).hex() == want.hex()

@@ -12,6 +12,7 @@ cp $P/bench_kernel_stats.json profiles/${R}_bench_kernel_stats.json
 cp $P/msm_pmc.json profiles/${R}_msm_pmc.json
 cp $P/msm_pmc_latest.json profiles/msm_pmc_latest.json
 cp "$P/prove_2^20_breakdown.txt" "profiles/${R}_prove_2^20_breakdown.txt"
+[ -f "$P/prove_2^20_preprocessed_breakdown.txt" ] && cp "$P/prove_2^20_preprocessed_breakdown.txt" "profiles/${R}_prove_2^20_preprocessed_breakdown.txt"
 cp $P/ntt_bench.json profiles/${R}_ntt_bench.json
 for f in bfly_peak.json prove_ntt_roofline.json prove_ntt_roofline.txt ntt_roofline.json ntt_roofline.txt; do
   [ -f $P/$f ] && cp $P/$f profiles/${R}_$f

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Prove-shaped pipeline timing at n = 2^k gates (tuning aid; run under rocprofv3 for the
-per-kernel split).  Usage: python tools/prove_bench.py [k ...]"""
+per-kernel split).  Usage: python tools/prove_bench.py [--pre] [k ...]"""
 import json
 import os
 import sys
@@ -15,5 +15,6 @@ from bench import prove_component  # noqa: E402
 
 hip.init(0)
 dev = torch.device("cuda", 0)
-ks = [int(x) for x in sys.argv[1:]] or [16, 18, 20]
-print(json.dumps({"prove_2^%d" % k: prove_component(torch, hip, dev, k) for k in ks}))
+pre = "--pre" in sys.argv   # the preprocessed-circuit path (plk_prover_preprocess) instead
+ks = [int(x) for x in sys.argv[1:] if x != "--pre"] or [16, 18, 20]
+print(json.dumps({"prove_2^%d" % k: prove_component(torch, hip, dev, k, preprocessed=pre) for k in ks}))
