@@ -642,7 +642,7 @@ def main():
         "warmup": W,
         "ms_per_step": round(elapsed / K * 1e3, 5),
         "higher_is_better": True,
-        "scaling": "strong" if strong else "weak",
+        "scaling": "weak" if args.weak else "strong",   # (N = 1: the mode the N > 1 runs use)
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: SRS points kG (k uniform 1..16), HF scalars uniform 0..16, %d distinct "
