@@ -935,7 +935,7 @@ __global__ void scalars_init_kernel(SlotFile f, uint8_t* __restrict__ S, uint32_
 constexpr int PACK_T = 1024;
 __global__ __launch_bounds__(PACK_T) void trim_pack_kernel(TrimArgs a, int nt, const PlkMsmResult* __restrict__ res,
                                                            const uint8_t* __restrict__ S, uint32_t* __restrict__ stat,
-                                                           uint8_t* __restrict__ host) {
+                                                           uint8_t* __restrict__ host, uint32_t seq) {
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
   const int ntrim = nt > 0 && (a.dst[nt - 1] & TRIM_ANY) ? nt - 1 : nt;   // the vote buffer comes last
   __shared__ uint32_t got[11];
@@ -981,6 +981,12 @@ __global__ __launch_bounds__(PACK_T) void trim_pack_kernel(TrimArgs a, int nt, c
   const int ev[7] = {S_AZ, S_BZ, S_CZ, S_S1Z, S_S2Z, S_RZ, S_ZWZ};
   if (t >= 27 && t < 34) host[t] = S[ev[t - 27]];
   if (t < NSTAT) ((uint32_t*)(host + 64))[t] = stat[t];
+  // the call's completion word (host bytes 60..63) last: every writer's bytes are visible to the
+  // host before it (system-scope fence, then the barrier), so the host can poll it instead of
+  // waiting for the stream (finish())
+  __threadfence_system();
+  __syncthreads();
+  if (t == 0) __hip_atomic_store((uint32_t*)(host + 60), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------------------ stage A (circuit)
@@ -1120,6 +1126,7 @@ struct plk_prover {
   // mapped pinned host memory: 64 proof bytes + NSTAT status words (trim_pack_kernel)
   uint8_t* h_res = nullptr;
   uint8_t* d_res_host = nullptr;   // its device address
+  uint32_t seq = 0;                // calls so far: trim_pack_kernel's completion word
   // preprocessed circuit (plk_prover_preprocess): the round-3 forward transforms of the fixed
   // polynomials q_o q_m q_l q_r s_sigma_3 l_1_x (PlkPolyMulJob::bt), for the addresses given
   struct Fixed {
@@ -1440,6 +1447,7 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
     plk_prover_destroy(P);
     return PLK_ERR_NOMEM;
   }
+  memset(P->h_res, 0, 64 + 4 * NSTAT);   // (completion word 0: no call yet)
   uint8_t* m = P->mem;
   P->d_srs = m + o_srs; P->d_zh = m + o_zh; P->d_h3 = m + o_h3; P->d_hinv = m + o_hinv; P->d_S = m + o_S;
   P->d_stat = (uint32_t*)(m + o_stat); P->d_tick = (uint32_t*)(m + o_tick); P->d_rem = m + o_rem; P->d_bsum = (uint32_t*)(m + o_bsum);
@@ -1717,7 +1725,7 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   }
   // (each record's finishing block already wrote its point: no finalize launch)
   hipLaunchKernelGGL(trim_pack_kernel, dim3(1), dim3(PACK_T), 0, P->st, trims, ntrims, P->d_res, P->d_S, P->d_stat,
-                     P->d_res_host);
+                     P->d_res_host, ++P->seq);
   PLK_HIP(hipGetLastError());
 #undef RC
   return PLK_OK;
@@ -1744,7 +1752,29 @@ int check_status(const plk_prover* P, const uint32_t* st, int strict, int circui
 }
 
 int finish(plk_prover* P, int strict, int circuit, uint8_t proof[34]) {
-  PLK_HIP(hipStreamSynchronize(P->st));   // trim_pack_kernel wrote P->h_res (mapped pinned)
+  // trim_pack_kernel wrote P->h_res (mapped pinned) and then this call's completion word: poll it
+  // (the stream's own completion is noticed later than the word; PLK_PROVE_SYNC=1 waits for the
+  // stream instead).  A failed launch never writes it: the stream is queried now and then.
+  static int sync_only = -1;
+  if (sync_only < 0) {
+    const char* e = getenv("PLK_PROVE_SYNC");
+    sync_only = e && atoi(e) != 0;
+  }
+  bool seen = false;
+  if (!sync_only) {
+    const uint32_t* w = (const uint32_t*)(P->h_res + 60);
+    for (uint64_t it = 1;; it++) {
+      if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == P->seq) { seen = true; break; }
+      if (!(it & 4095) && hipStreamQuery(P->st) != hipErrorNotReady) break;   // done (word re-read below) or failed
+    }
+  }
+  if (!seen) {
+    PLK_HIP(hipStreamSynchronize(P->st));
+    if (__atomic_load_n((const uint32_t*)(P->h_res + 60), __ATOMIC_ACQUIRE) != P->seq) {
+      plk_set_error("prover: the packing kernel did not complete");
+      return PLK_ERR_HIP;
+    }
+  }
   uint32_t hs[NSTAT];
   memcpy(hs, P->h_res + 64, sizeof hs);
   const int rc = check_status(P, hs, strict, circuit);
