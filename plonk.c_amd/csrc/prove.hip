@@ -193,6 +193,9 @@ __global__ __launch_bounds__(256) void lincomb16_kernel(LcArgs a, const uint8_t*
 //   gamma, c + beta k2 x + gamma, alpha (a + beta s1 + gamma), b + beta s2 + gamma, c + beta s3 +
 //   gamma, z(omega x), alpha^2 (z - 1) (:409-489).  Same bytes as the 4 blinding poly_muls and 3
 //   lincomb launches it replaces (the first kernels of a proof are host-launch bound).
+struct SlotFile {
+  uint8_t b[NSLOT];
+};
 struct PrepArgs {
   const uint8_t *zh, *fa, *fb, *fc, *acc, *s1, *s2, *s3;
   uint64_t lz, n, la, lzx;
@@ -217,7 +220,15 @@ __device__ __forceinline__ void store4(uint8_t* out, uint64_t len, uint64_t i, u
       if (i + k < len) out[i + k] = (uint8_t)(w >> (8 * k));
   }
 }
-__global__ __launch_bounds__(256) void prep_kernel(PrepArgs a, const uint8_t* __restrict__ S) {
+// The scalar file comes in as an argument: block 0 also stores it to the device copy the later
+// kernels read and clears status words [0, st1) (scalars_init_kernel's work: one launch fewer).
+__global__ __launch_bounds__(256) void prep_kernel(PrepArgs a, const SlotFile f, uint8_t* __restrict__ Sd,
+                                                   uint32_t* __restrict__ stat, int st1) {
+  const uint8_t* S = f.b;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < NSLOT) Sd[threadIdx.x] = f.b[threadIdx.x];
+    if ((int)threadIdx.x < st1) stat[threadIdx.x] = 0;
+  }
   const uint32_t al = S[S_ALPHA], be = S[S_BETA], ga = S[S_GAMMA], bk1 = S[S_BK1], bk2 = S[S_BK2];
   const uint32_t al2 = S[S_ALPHA2], om = S[S_OMEGA];
   const uint32_t ba0 = S[P_BLA], ba1 = S[P_BLA + 1], bb0 = S[P_BLB], bb1 = S[P_BLB + 1], bc0 = S[P_BLC],
@@ -912,10 +923,7 @@ __device__ void scalars_r5(uint8_t* S) {
 
 // The scalar file (challenges, constants, blinding scalars) travels as a kernel argument, and
 // the same launch clears status words [st0, st1): no pageable host->device copy (each of those
-// stalls the host ~20 us) before the first compute kernel.
-struct SlotFile {
-  uint8_t b[NSLOT];
-};
+// stalls the host ~20 us) before the first compute kernel.  (prep_kernel does both itself.)
 __global__ void scalars_init_kernel(SlotFile f, uint8_t* __restrict__ S, uint32_t* __restrict__ stat, int st0,
                                     int st1) {
   const int t = threadIdx.x;
@@ -1537,8 +1545,15 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   S[P_BLC] = rnd[5] % HFP; S[P_BLC + 1] = rnd[4] % HFP;
   S[P_BLZ] = rnd[8] % HFP; S[P_BLZ + 1] = rnd[7] % HFP; S[P_BLZ + 2] = rnd[6] % HFP;
   // status: stage-A words (gate/copy/acc) are owned by the circuit path; reset the rest
-  hipLaunchKernelGGL(scalars_init_kernel, dim3(1), dim3(NSLOT), 0, P->st, sf, P->d_S, P->d_stat, 0, (int)ST_GATE);
-  PLK_HIP(hipGetLastError());
+  // (the aligned path's prep_kernel stores the scalar file and clears the status words itself)
+  const uint8_t* ins[8] = {P->d_zh, pl[0], pl[1], pl[2], pl[11], pl[8], pl[9], pl[10]};
+  bool aligned = true;
+  for (const uint8_t* q : ins) aligned = aligned && ((uintptr_t)q % 16) == 0;
+  const bool prep = aligned && L.la <= L.lzx && L.lzx <= L.la + 1;
+  if (!prep) {
+    hipLaunchKernelGGL(scalars_init_kernel, dim3(1), dim3(NSLOT), 0, P->st, sf, P->d_S, P->d_stat, 0, (int)ST_GATE);
+    PLK_HIP(hipGetLastError());
+  }
   // (the commitment arena needs no clearing: it is zeroed at plk_prover_create and every proof
   // writes the same upper-bound ranges of its 9 slots, so the bytes past them stay zero)
   uint8_t* const cA = P->arena;
@@ -1554,14 +1569,12 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   int rc;
 #define RC(x) do { if ((rc = (x))) return rc; } while (0)
   // ---- rounds 1-2 (a_x b_x c_x z_x) and round 3's linear factors, src/plonk.h:280-489
-  const uint8_t* ins[8] = {P->d_zh, FA, FB, FC, ACC, S1, S2, S3};
-  bool aligned = true;
-  for (const uint8_t* q : ins) aligned = aligned && ((uintptr_t)q % 16) == 0;
-  if (aligned && L.la <= L.lzx && L.lzx <= L.la + 1) {
+  if (prep) {
     const PrepArgs pa{P->d_zh, FA, FB, FC, ACC, S1, S2, S3, L.lz, n, L.la, L.lzx,
                       cA, cB, cC, cZ, P->A2, P->B2, P->C2, P->A3, P->B3, P->C3, P->ZW, P->Z1};
     const uint64_t blocks = std::min<uint64_t>((L.lzx + 1023) / 1024, 4096);
-    hipLaunchKernelGGL(prep_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, pa, dS);
+    hipLaunchKernelGGL(prep_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, pa, sf,
+                       P->d_S, P->d_stat, (int)ST_GATE);
     PLK_HIP(hipGetLastError());
   } else {
     // ---- round 1: a_x = (b2 + b1 x) Z_H + f_a, ...  (3 poly_mul)
