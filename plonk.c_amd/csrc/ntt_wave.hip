@@ -713,8 +713,8 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
       first = false;
     }
     __syncthreads();
-    G::template pass<false, false>(va, tid, bufs, 0, Tf);
-    // (bfix: b's transform is finished -- plk_wave_pretransform stored this pass's output
+    if (!jobs.j[job].afix) G::template pass<false, false>(va, tid, bufs, 0, Tf);
+    // (afix / bfix: b's transform is finished -- plk_wave_pretransform stored this pass's output
     // registers where their inputs were read -- so its lo = 0 pass is skipped)
     if (!jobs.j[job].bfix) G::template pass<false, false>(vb, tid, bufs, G::XCH, Tf);
 #pragma unroll
@@ -727,11 +727,13 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
 
 // The lo = 0 forward pass of a fixed operand, exactly as wt_center_kernel runs it on b, each
 // thread storing its output registers where it read its inputs (so a later center launch loads
-// them unchanged: WJob::bfix).  In place: every position is read and written by one thread.
+// them unchanged: WJob::bfix / afix).  In place: every position is read and written by one
+// thread.  blockIdx.y = which array.
 template <int TB, int R, class F>
-__global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_fixfwd_kernel(WPass p, uint32_t* d,
+__global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_fixfwd_kernel(WPass p, WArrs arrs,
                                                                                                     WTw twf) {
   using G = Eng<TB, R, TB, F>;
+  uint32_t* d = arrs.a[blockIdx.y].d;
   __shared__ uint32_t Tlds[1 << TB];
   __shared__ uint32_t bufs[(G::DBUF ? 2 : 1) * G::BUF];
   const uint32_t tid = threadIdx.x, tile = blockIdx.x;
@@ -926,8 +928,42 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
     if (rc) return rc;
   }
   const uint32_t tiles = (uint32_t)((1ull << k) >> TB);
+  // operands shared by several products of the batch: their lo = 0 forward pass runs once, in
+  // its own launch, instead of once per product inside the center items (PLK_NTT_SHARED_FIX=0:
+  // off, 2: also next to pretransformed operands).  The extra launch moves a tile's loads and
+  // stores besides its pass (768 tiles: 18.6 us against 20 us less center time in the prover's
+  // 2^21 batch): within the ~10 us run-to-run spread of a proof's kernel span either way
+  // (tools/prove_ab_prof.sh, medians over 4-5 calls), so batches holding a pretransformed
+  // operand keep the per-item passes.
+  static int shfix = -1;
+  if (shfix < 0) {
+    const char* e = getenv("PLK_NTT_SHARED_FIX");
+    shfix = e ? atoi(e) : 1;
+  }
+  bool anyfix = false;
+  for (int j = 0; j < nj; j++) anyfix |= jobs.j[j].bfix != 0;
+  WJobs cj = jobs;
+  if (shfix > 1 || (shfix == 1 && !anyfix)) {
+    WArrs sh{};
+    int ns = 0;
+    for (int q = 0; q < na; q++) {
+      int uses = 0;
+      for (int j = 0; j < nj; j++) uses += (jobs.j[j].A == arrs.a[q].d) + (!jobs.j[j].bfix && jobs.j[j].B == arrs.a[q].d);
+      if (uses < 2) continue;
+      sh.a[ns++] = arrs.a[q];
+      for (int j = 0; j < nj; j++) {
+        if (cj.j[j].A == arrs.a[q].d) cj.j[j].afix = 1;
+        if (!jobs.j[j].bfix && cj.j[j].B == arrs.a[q].d) cj.j[j].bfix = 1;
+      }
+    }
+    if (ns) {
+      hipLaunchKernelGGL((wt_fixfwd_kernel<TB, wt_rc(TB), F>), dim3(tiles, ns), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, sh,
+                         twf);
+      PLK_HIP(hipGetLastError());
+    }
+  }
   const uint32_t grid = std::min<uint32_t>(tiles * nj, center_blocks());
-  hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F>), dim3(grid), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, jobs, twf,
+  hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F>), dim3(grid), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, cj, twf,
                      (uint32_t)nj);
   PLK_HIP(hipGetLastError());
   WJobs later = jobs;   // sum groups add their members in the FIRST inverse pass only
@@ -959,7 +995,7 @@ int wave_pretransform_t(const uint8_t* b8, uint64_t lb, int k, uint32_t* d, hipS
     if (rc) return rc;
   }
   hipLaunchKernelGGL((wt_fixfwd_kernel<TB, wt_rc(TB), F>), dim3((unsigned)((1ull << k) >> TB)), dim3(wt_ntc(TB)), 0, st,
-                     WPass{k, 0}, d, twf);
+                     WPass{k, 0}, arrs, twf);
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }

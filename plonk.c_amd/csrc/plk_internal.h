@@ -110,6 +110,7 @@ struct WJob {
   // pass; the center kernel zeroes it first (nullptr: not wanted)
   uint32_t* nz = nullptr;
   int bfix = 0;                    // B holds a plk_poly_mul_pretransform result
+  int afix = 0;                    // (wave engine only: A finished in the batch, see wt_fixfwd_kernel)
 };
 constexpr int PLK_WAVE_MAX_JOBS = 12;   // jobs per launch of the wave engine (larger batches run in chunks)
 bool plk_wave_ntt_supported(int k);

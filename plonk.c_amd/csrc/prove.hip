@@ -1605,25 +1605,28 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     // F29's centered range: 3 * 64 n <= (p - 1) / 2 (n <= 1,223,338)
     const int lin = plk_poly_mul_summable(L.la, n) && (uint64_t)3 * L.la * 128 < f29::P ? 1 : 0;
     P->lin_sum = lin;
-    PlkPolyMulJob g1[] = {{cA, L.la, cB, L.la, P->AB},      {cA, L.la, QL, n, P->AQL},
-                                {cB, L.la, QR, n, P->BQR, lin},   {cC, L.la, QO, n, P->CQO, lin},
-                                {P->A2, L.la, P->B2, L.la, P->T2a}, {P->A3, L.la, P->B3, L.la, P->T3a},
-                                {P->Z1, L.lz1, L1, n, P->T4},
-                                // the 17th poly_mul, z_x s_sigma_3 (src/plonk.h:560), as z_x * s3:
-                                // its scalar beta z_omega_z (a round-4 value) moves into r(x)'s
-                                // lincomb (S_R3B), so the product joins this batch
-                                {cZ, L.lzx, S3, n, P->P3},
-                                // t_2 = ((A2 B2) C2) z and t_3 = ((A3 B3) C3) z(omega x)
-                                // (src/plonk.h:432-434, 471-473) re-associated as (A2 B2)(C2 z):
-                                // C2 z and C3 z(omega x) join this batch and the 4n products
-                                // come in one batch (associativity over GF(17); the centered F29
-                                // residues hold the 2n x 2n products exactly)
-                                {P->C2, L.la, cZ, L.lzx, P->T2b}, {P->C3, L.la, P->ZW, L.lzw, P->T3b}};
+    // (order: the center launch's blocks 0-255 take the even jobs and 256-511 the odd ones; with
+    // a_x, b_x, z_x transformed once for their two products each, both halves carry 12 of the
+    // batch's 24 tile passes; with the preprocessed circuit 13 / 12 of 25)
+    PlkPolyMulJob g1[] = {{cA, L.la, QL, n, P->AQL},          {cB, L.la, QR, n, P->BQR, lin},
+                          {cC, L.la, QO, n, P->CQO, lin},      {P->Z1, L.lz1, L1, n, P->T4},
+                          {cA, L.la, cB, L.la, P->AB},
+                          // the 17th poly_mul, z_x s_sigma_3 (src/plonk.h:560), as z_x * s3:
+                          // its scalar beta z_omega_z (a round-4 value) moves into r(x)'s
+                          // lincomb (S_R3B), so the product joins this batch
+                          {cZ, L.lzx, S3, n, P->P3},
+                          // t_2 = ((A2 B2) C2) z and t_3 = ((A3 B3) C3) z(omega x)
+                          // (src/plonk.h:432-434, 471-473) re-associated as (A2 B2)(C2 z):
+                          // C2 z and C3 z(omega x) join this batch and the 4n products
+                          // come in one batch (associativity over GF(17); the centered F29
+                          // residues hold the 2n x 2n products exactly)
+                          {P->A2, L.la, P->B2, L.la, P->T2a}, {P->C2, L.la, cZ, L.lzx, P->T2b},
+                          {P->A3, L.la, P->B3, L.la, P->T3a}, {P->C3, L.la, P->ZW, L.lzw, P->T3b}};
     PlkPolyMulJob g2[] = {{P->AB, L.lab, QM, n, P->ABQM},
                           {P->T2a, L.l2a, P->T2b, L.la + L.lzx - 1, P->T2},
                           {P->T3a, L.l2a, P->T3b, L.la + L.lzw - 1, P->T3}};
     if (pre) {   // preprocessed circuit: the fixed b operands' transforms (plk_prover_preprocess)
-      PlkPolyMulJob* const js[] = {&g1[1], &g1[2], &g1[3], &g1[6], &g1[7], &g2[0]};
+      PlkPolyMulJob* const js[] = {&g1[0], &g1[1], &g1[2], &g1[3], &g1[5], &g2[0]};
       const int which[] = {5, 6, 3, 12, 10, 4};   // q_l q_r q_o l_1_x s_sigma_3 q_m
       for (int i = 0; i < 6; i++) {
         const plk_prover::Fixed& f = P->fix[which[i]];
@@ -1819,7 +1822,7 @@ int plk_prover_preprocess(plk_prover_t* P, const uint8_t* const d_polys[13]) {
   if (!d_polys) return PLK_OK;   // dropped
   const uint64_t n = P->n;
   const Lens L = lens_for(n, P->zh_len);
-  // the round-3 products with a fixed b (rounds(): g1[1..3], g1[6], g1[7], g2[0]) and their a
+  // the round-3 products with a fixed b (rounds(): g1[0..3], g1[5], g2[0]) and their a
   // operands' upper-bound lengths
   const int which[] = {5, 6, 3, 12, 10, 4};   // q_l q_r q_o l_1_x s_sigma_3 q_m
   const uint64_t la[] = {L.la, L.la, L.la, L.lz1, L.lzx, L.lab};
