@@ -941,11 +941,19 @@ __global__ void scalars_init_kernel(SlotFile f, uint8_t* __restrict__ S, uint32_
 // buffer w's last non-zero byte from the top, 1 KB per step (16 bytes per lane, the highest
 // non-zero lane by ballot); the remaining waves OR the remainder-vote bytes (TRIM_ANY).
 constexpr int PACK_T = 1024;
+static_assert(NSTAT <= 64 && 34 <= 64, "trim_pack_kernel: wave 0 writes the status words, the last wave the proof");
 __global__ __launch_bounds__(PACK_T) void trim_pack_kernel(TrimArgs a, int nt, const PlkMsmResult* __restrict__ res,
                                                            const uint8_t* __restrict__ S, uint32_t* __restrict__ stat,
                                                            uint8_t* __restrict__ host, uint32_t seq) {
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
   const int ntrim = nt > 0 && (a.dst[nt - 1] & TRIM_ANY) ? nt - 1 : nt;   // the vote buffer comes last
+  // the proof bytes do not depend on the trimmed lengths: the last waves load and send them to
+  // the host first, so their round trips overlap the scans below
+  if (wv == PACK_T / 64 - 1) {
+    const int ev[7] = {S_AZ, S_BZ, S_CZ, S_S1Z, S_S2Z, S_RZ, S_ZWZ};
+    if (lane < 27) host[lane] = res[lane / 3].g1[lane % 3];
+    else if (lane < 34) host[lane] = S[ev[lane - 27]];
+  }
   __shared__ uint32_t got[11];
   if (t < 11) got[t] = 0;
   __syncthreads();
@@ -985,14 +993,11 @@ __global__ __launch_bounds__(PACK_T) void trim_pack_kernel(TrimArgs a, int nt, c
     }
   }
   __syncthreads();   // the stat words written above, visible to the block
-  if (t < 27) host[t] = res[t / 3].g1[t % 3];
-  const int ev[7] = {S_AZ, S_BZ, S_CZ, S_S1Z, S_S2Z, S_RZ, S_ZWZ};
-  if (t >= 27 && t < 34) host[t] = S[ev[t - 27]];
   if (t < NSTAT) ((uint32_t*)(host + 64))[t] = stat[t];
   // the call's completion word (host bytes 60..63) last: every writer's bytes are visible to the
-  // host before it (system-scope fence, then the barrier), so the host can poll it instead of
-  // waiting for the stream (finish())
-  __threadfence_system();
+  // host before it (a system-scope fence in the two waves that wrote host bytes, then the
+  // barrier), so the host can poll it instead of waiting for the stream (finish())
+  if (wv == 0 || wv == PACK_T / 64 - 1) __threadfence_system();
   __syncthreads();
   if (t == 0) __hip_atomic_store((uint32_t*)(host + 60), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
