@@ -320,3 +320,52 @@ def test_blocked_beyond_babybear_range(hip, oracle):
     hi = np.frombuffer(oracle.poly_mul_ntt(a[-t:], b[-t:]), np.uint8)
     hi = np.pad(hi, (0, 2 * t - 1 - len(hi)))
     assert np.array_equal(full[rl - t:], hi[t - 1:])
+
+
+_SHFIX_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [sys.argv[1], sys.argv[2], sys.argv[2] + "/golden"]
+import plonkhip as hip
+import test_polymul_gpu as t
+hip.init(0)
+d = np.load(sys.argv[3])
+polys = [d["p%d" % i] for i in range(int(d["np"]))]
+spec = [tuple(int(v) for v in r) for r in d["spec"]]
+for out in t._run_batch(hip, polys, spec):
+    print(t._trim(out).hex())
+"""
+
+
+@pytest.mark.parametrize("mode", ["0", "2"])
+def test_batch_shared_operands_fix_modes(hip, oracle, tmp_path, mode):
+    """The batch of test_batch_shared_operands with the shared operands' separate lo = 0 pass off
+    (PLK_NTT_SHARED_FIX=0: every center item transforms its operands) and forced (2), each read
+    once per process: a child process per mode."""
+    import os
+    import subprocess
+    import sys
+    polys = [np.frombuffer(gen.poly_inputs(40 + i, n, 1)[0], np.uint8) for i, n in enumerate(_POOL)]
+    spec = [(0, 1, 0), (0, 2, 0), (1, 2, 0), (0, 0, 0), (3, 4, 0), (4, 5, 0), (2, 5, 0), (0, 1, 0),
+            (6, 7, 1), (0, 7, 1), (5, 5, 0), (1, 4, 0), (1, 1, 0), (3, 3, 0), (2, 4, 0)]
+    f = tmp_path / "case.npz"
+    np.savez(f, np=len(polys), spec=np.array(spec), **{"p%d" % i: p for i, p in enumerate(polys)})
+    here = os.path.dirname(os.path.abspath(__file__))
+    pkg = os.path.join(os.path.dirname(here), "plonk.c_amd")
+    env = dict(os.environ, PLK_NTT_SHARED_FIX=mode)
+    r = subprocess.run([sys.executable, "-c", _SHFIX_SCRIPT, pkg, here, str(f)], capture_output=True, text=True,
+                       env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = r.stdout.strip().splitlines()[-len(spec):]
+    full = len(polys[6]) + len(polys[7]) - 1
+
+    def prod(i, j):
+        p = np.frombuffer(oracle.poly_mul(polys[i].tobytes(), polys[j].tobytes()), np.uint8).astype(np.int64)
+        return np.pad(p, (0, full - len(p)))
+    for k, (i, j, acc) in enumerate(spec):
+        if k == 7:   # sum group leader: a_0 a_1 + a_6 a_7 + a_0 a_7
+            want = _trim(((prod(0, 1) + prod(6, 7) + prod(0, 7)) % 17).astype(np.uint8).tobytes())
+        elif acc:
+            continue
+        else:
+            want = oracle.poly_mul(polys[i].tobytes(), polys[j].tobytes())
+        assert bytes.fromhex(got[k]) == want, (mode, k)
