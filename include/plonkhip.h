@@ -194,7 +194,9 @@ int plk_interpolate(const uint8_t *h_pows_inv, const uint8_t *values, size_t n, 
  * src/plonk.h:53-139, 223-656, 120-139) ---------------------------------------------------
  * plk_prover_create uploads the SRS and Z_H once (the PLONK struct of plonk_new); the
  * circuit tables h, k1_h, k2_h, h_pows_inv are optional (needed only by plk_prover_prove).
- * h_pows_inv is the inverse Vandermonde matrix row-major, [r * n + c] = matrix_get(r, c). */
+ * h_pows_inv is the inverse Vandermonde matrix row-major, [r * n + c] = matrix_get(r, c).
+ * A prover owns its stream and work buffers: one call at a time per plk_prover_t (distinct
+ * provers may run from different threads). */
 typedef struct plk_prover plk_prover_t;
 typedef struct {
   size_t n;                                  /* gates = |H| */
