@@ -55,7 +55,11 @@ def parse():
     ap.add_argument("--rotate-mib", type=int, default=640)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-components", action="store_true")
+    ap.add_argument("--no-components", action="store_true", help="same as --components none")
+    ap.add_argument("--components", default="all",
+                    help="all | none | comma list of: msm, ntt, polymul, polyops, prove, cpu -- what rank 0 "
+                         "reports beside the headline; at N > 1 'prove' (in 'all') runs C5's replica leg "
+                         "(one concurrent proof per GPU)")
     ap.add_argument("--profile-only", action="store_true",
                     help="just launch the timed MSM loop (for rocprofv3 runs)")
     ap.add_argument("--weak", action="store_true",
@@ -270,7 +274,44 @@ def cpu_other_baselines(hip):
     return out
 
 
-def components(torch, hip, dev, st):
+COMPONENT_GROUPS = ("msm", "ntt", "polymul", "polyops", "prove", "cpu")
+
+
+def wanted_components(args):
+    """the set of component groups this run reports"""
+    if args.no_components or args.components == "none":
+        return set()
+    if args.components == "all":
+        return set(COMPONENT_GROUPS)
+    want = {c.strip() for c in args.components.split(",") if c.strip()}
+    bad = want - set(COMPONENT_GROUPS)
+    if bad:
+        raise SystemExit("unknown --components %s (choose from %s)" % (sorted(bad), ", ".join(COMPONENT_GROUPS)))
+    return want
+
+
+def pts_label(m):
+    """component key fragment naming the points one MSM actually reads: 2^k, or the count"""
+    return "2^%d" % (m.bit_length() - 1) if m & (m - 1) == 0 else "%dpts" % m
+
+
+def components(torch, hip, dev, st, want):
+    out = {}
+    if "msm" in want:
+        out.update(msm_components(torch, hip, dev, st))
+    if "ntt" in want:
+        out.update(ntt_components(torch, hip, dev, st))
+    if "polymul" in want:
+        out.update(polymul_components(torch, hip, dev, st))
+    if "polyops" in want:
+        out.update(polyops_components(torch, hip, dev, st))
+    if "prove" in want:
+        out["prove_2^20_gates"] = prove_component(torch, hip, dev, 20)
+        out["prove_2^20_gates_preprocessed"] = prove_component(torch, hip, dev, 20, preprocessed=True)
+    return out
+
+
+def msm_components(torch, hip, dev, st):
     out = {}
     # C2: 2^16-point MSM -- device-resident kernel time and host-buffer call (PCIe incl.)
     n = 1 << 16
@@ -311,6 +352,12 @@ def components(torch, hip, dev, st):
                                  "note": "plk_msm_g1 (what the drop-in srs_eval_at_s calls), host buffers, PCIe "
                                          "included; cached = same SRS pointer and bytes (reference: 9 commitments "
                                          "per proof over one SRS, src/plonk.h:299-301,379,522-524,620-621)"}
+    return out
+
+
+def ntt_components(torch, hip, dev, st):
+    out = {}
+    nb = 8
     # C3: forward NTT 2^20 over BabyBear (Montgomery u32, in place, 2 passes)
     k = 20
     bufs = [torch.randint(0, 2013265921, (1 << k,), dtype=torch.int64, device=dev).to(torch.int32)
@@ -336,7 +383,6 @@ def components(torch, hip, dev, st):
         out["ntt_2^20_forward"]["ms_cold"] = round(gr[1], 4)
     del cold
     # the same transform, 8 independent arrays sharing each pass's launch (plk_ntt_batch_dev)
-    nb = 8
     bb_ = [torch.randint(0, 2013265921, (nb, 1 << k), dtype=torch.int64, device=dev).to(torch.int32)
            for _ in range(2)]
     gr = graph_avg_ms(torch, lambda i, s: hip.ntt_batch_dev(bb_[i % 2], k, nb, False, s), 20)
@@ -362,6 +408,18 @@ def components(torch, hip, dev, st):
                                         "Gelem_s": round(nb * (1 << k) / (avg * 1e-3) / 1e9, 2),
                                         "roofline": roofline_obj(nb * alg, avg, "8 transforms per launch")}
     del b29
+    for key, peak, nt in (("ntt_2^20_forward", "bb_dif_Gbfly_s", 1), ("ntt_2^20_forward_batch8", "bb_dif_Gbfly_s", 8),
+                          ("ntt29_2^20_forward", "f29_dif_Gbfly_s", 1),
+                          ("ntt29_2^20_forward_batch8", "f29_dif_Gbfly_s", 8)):
+        c = out[key]
+        bfly = butterfly_roofline(nt * (1 << 19) * 20, c.get("ms", c.get("ms_per_launch")), peak)
+        if bfly:
+            c["roofline_butterfly"] = bfly
+    return out
+
+
+def polymul_components(torch, hip, dev, st):
+    out = {}
     # poly_mul 2^19 x 2^19 -> 2^20 - 1 coefficients (device-resident)
     la = lb = 1 << 19
     a = torch.randint(0, 17, (la,), dtype=torch.int16, device=dev).to(torch.uint8)
@@ -375,16 +433,11 @@ def components(torch, hip, dev, st):
     out["poly_mul_2^19x2^19"] = {"ms": round(avg, 4), "Gcoeff_s_out": round((la + lb - 1) / (avg * 1e-3) / 1e9, 2),
                                  "roofline": roofline_obj(la + lb + (la + lb - 1), avg,
                                                           "SURVEY 8(d): la + lb + (la + lb - 1) bytes of HF")}
-    out.update(polyops_components(torch, hip, dev, st))
-    for key, peak, nt in (("ntt_2^20_forward", "bb_dif_Gbfly_s", 1), ("ntt_2^20_forward_batch8", "bb_dif_Gbfly_s", 8),
-                          ("ntt29_2^20_forward", "f29_dif_Gbfly_s", 1),
-                          ("ntt29_2^20_forward_batch8", "f29_dif_Gbfly_s", 8)):
-        c = out[key]
-        bfly = butterfly_roofline(nt * (1 << 19) * 20, c.get("ms", c.get("ms_per_launch")), peak)
-        if bfly:
-            c["roofline_butterfly"] = bfly
-    out["prove_2^20_gates"] = prove_component(torch, hip, dev, 20)
-    out["prove_2^20_gates_preprocessed"] = prove_component(torch, hip, dev, 20, preprocessed=True)
+    # three 2^20-point transforms over F29 (a and b forward, the product inverse): 3 x 2^19 x 20
+    # butterflies
+    bfly = butterfly_roofline(3 * (1 << 19) * 20, avg, "f29_dif_Gbfly_s")
+    if bfly:
+        out["poly_mul_2^19x2^19"]["roofline_butterfly"] = bfly
     return out
 
 
@@ -450,7 +503,7 @@ def _prove_golden(n, out):
     return out.hex() == g["proof"] if g["n"] == n and g["seed"] == 51 else None
 
 
-def prove_component(torch, hip, dev, log2n, reps=5, preprocessed=False):
+def prove_component(torch, hip, dev, log2n, reps=5, preprocessed=False, barrier=None):
     """C5: plonk_prove rounds 1-5 (src/plonk.h:277-655) at n = 2^log2n gates on the device
     prover: 17 poly_mul (largest (3n+4) x (n+3) -> NTT 2^(log2n+3)), 9 commitments, 3
     divisions, evaluations.  Synthetic interpolated polynomials (GF(17) has no subgroup of
@@ -458,7 +511,9 @@ def prove_component(torch, hip, dev, log2n, reps=5, preprocessed=False):
     for every commitment; non-strict (remainders not asserted).  Wall time per call, the
     call synchronous and returning the 34 proof bytes to the host.  preprocessed: the six fixed
     circuit polynomials' round-3 transforms computed once beforehand (plk_prover_preprocess,
-    outside the timed calls -- PLONK's preprocessed input), every timed call the same proof."""
+    outside the timed calls -- PLONK's preprocessed input), every timed call the same proof.
+    barrier: called right before the timed calls (the N-GPU replica leg starts every rank's
+    proofs together)."""
     n = 1 << log2n
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import gen
@@ -476,6 +531,8 @@ def prove_component(torch, hip, dev, log2n, reps=5, preprocessed=False):
         pre_ms = round((time.perf_counter() - t0) * 1e3, 3)
         first = pr.rounds_dev(polys, chal, rnd, preprocessed=True)
     torch.cuda.synchronize()
+    if barrier is not None:
+        barrier()
     t = []
     for _ in range(reps):
         t0 = time.perf_counter()
@@ -519,6 +576,7 @@ def main():
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
     dev = torch.device("cuda", gpu)
+    tuned = hip.tune_from_env()              # PLK_TUNE (A/B runs only; empty by default)
     hip.init(gpu)
     st = torch.cuda.current_stream()
 
@@ -595,8 +653,9 @@ def main():
                 full_logs.append(one_msm_log(torch, hip, fp, fs, n, dev, st))
         want = g1_bytes(ops.exp(torch.tensor([sum(full_logs) % 102], dtype=torch.int32, device=dev)))[0]
         check["first_msm_single_gpu_recompute"] = want == g1s[0]
-    if strong and args.log2n == 22:
-        # the reference's own answer for a 2^22-point input, through the same sharded path
+    if (strong or world == 1) and args.log2n == 22:
+        # the reference's own answer for a 2^22-point input through the timed kernel and the same
+        # finish (sharded at N > 1: every rank its point range)
         sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
         import gen
         with open(os.path.join(ROOT, "tests", "golden", "msm.json")) as f:
@@ -668,6 +727,7 @@ def main():
                      "timing": "hipEvent pair around %d back-to-back launches on the kernel's "
                                "stream, opened after one primer launch is queued" % L},
         "checks": check,
+        **({"tuning": tuned} if tuned else {}),
         "irregular_inputs": irregular,
         "serial_fold_fallbacks": folded,
     }
@@ -675,31 +735,47 @@ def main():
         torch.cuda.synchronize()
         line["cpu_baseline"] = cpu_baseline(pts[first_set].cpu().numpy(), sc[first_set].cpu().numpy(),
                                             args.cpu_seconds, g1s[0])
-    if rank == 0 and not args.no_components:
-        comp = components(torch, hip, dev, st)
-        comp["msm_2^%d_one_per_launch" % args.log2n] = single_msm_component(torch, hip, pts, sc, m, sets, dev)
-        B8 = 8
-        r8 = torch.zeros((B8, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
-        avg8, med8 = event_avg_ms(torch, st, lambda i: hip.msm_g1_batch_dev(
-            pts[(i * B8) % sets], 3 * m, sc[(i * B8) % sets], m, m, B8, r8[0], st), 16)
-        comp["msm_2^%d_8_per_launch" % args.log2n] = {
-            "device_us_per_launch": round(avg8 * 1e3, 2),
-            "GB_s": round(MSM_BYTES_PER_POINT * m * B8 / (avg8 * 1e-3) / 1e9, 1),
-            "note": "8 MSMs per launch (the prover's commitments are 9 per launch)"}
-        if world == 1 and not args.no_cpu_baseline:
-            comp["cpu_reference_other"] = cpu_other_baselines(hip)
-        line["components"] = comp
-    if world > 1 and not args.no_components:
-        # C5 at N GPUs: replicas only (the prover's NTT work stays on one GPU) --
-        # every rank proves its own 2^20-gate instance at the same time; slowest rank reported
-        pc = prove_component(torch, hip, dev, 20, reps=3)
-        t = torch.tensor([pc["ms"]], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    comps = wanted_components(args)
+    comp = {}
+    if world > 1 and "prove" in comps:
+        # C5 at N GPUs: replicas only (a proof's NTT work stays on one GPU).  Every rank
+        # builds its prover first, then ALL ranks start their timed proofs after one barrier, so
+        # the N proofs run at the same time (rank 0's other components run after this leg); each
+        # rank's proof bytes are checked against the recorded answer and the check is reduced
+        pc = prove_component(torch, hip, dev, 20, reps=3, barrier=dist.barrier)
+        t = torch.tensor([pc["ms"], pc["median_ms"], 1.0 if pc["matches_oracle"] else 0.0,
+                          1.0 if pc["deterministic"] else 0.0], dtype=torch.float64, device=dev)
+        tmax, tmin = t.clone(), t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tmin, op=dist.ReduceOp.MIN)
         if rank == 0:
-            line.setdefault("components", {})["prove_2^20_gates_replicas"] = {
-                "gpus": world, "ms_slowest_rank": round(float(t.item()), 3),
-                "proofs_per_s": round(world / (float(t.item()) * 1e-3), 1),
-                "note": "one independent proof per GPU concurrently, no exchange"}
+            ms = float(tmax[0].item())
+            comp["prove_2^20_gates_replicas"] = {
+                "gpus": world, "ms_slowest_rank": round(ms, 3), "median_ms_slowest_rank": round(float(tmax[1].item()), 3),
+                "proofs_per_s": round(world / (ms * 1e-3), 1),
+                "matches_oracle_all_ranks": bool(tmin[2].item() == 1.0),
+                "deterministic_all_ranks": bool(tmin[3].item() == 1.0),
+                "note": "one independent 2^20-gate proof per GPU, all ranks released by one barrier and timing "
+                        "concurrently, no exchange; ms = the slowest rank's best call; matches_oracle: every rank's "
+                        "34 bytes equal the recorded answer of the CPU restatement (tests/golden/prove_2_20.json)"}
+    if rank == 0 and comps:
+        comp.update(components(torch, hip, dev, st, comps - ({"prove"} if world > 1 else set())))
+        if "msm" in comps:
+            lab = pts_label(m)
+            comp["msm_%s_one_per_launch" % lab] = single_msm_component(torch, hip, pts, sc, m, sets, dev)
+            B8 = 8
+            r8 = torch.zeros((B8, hip.MSM_RESULT_BYTES), dtype=torch.uint8, device=dev)
+            avg8, med8 = event_avg_ms(torch, st, lambda i: hip.msm_g1_batch_dev(
+                pts[(i * B8) % sets], 3 * m, sc[(i * B8) % sets], m, m, B8, r8[0], st), 16)
+            comp["msm_%s_8_per_launch" % lab] = {
+                "device_us_per_launch": round(avg8 * 1e3, 2),
+                "GB_s": round(MSM_BYTES_PER_POINT * m * B8 / (avg8 * 1e-3) / 1e9, 1),
+                "points_per_msm": m,
+                "note": "8 MSMs per launch (the prover's commitments are 9 per launch)"}
+        if world == 1 and "cpu" in comps and not args.no_cpu_baseline:
+            comp["cpu_reference_other"] = cpu_other_baselines(hip)
+    if rank == 0 and comp:
+        line["components"] = comp
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -46,6 +46,33 @@ const char *plk_last_error(void);
 int plk_device_count(void);
 const char *plk_version(void);
 
+/* ---- options --------------------------------------------------------------------------
+ * Every default is the production setting; the others exist for A/B measurement and for tests
+ * that force a rarely taken path.  None changes a result: every setting gives the same bytes.
+ * The library reads no environment variable except PLK_DEVICE (device selection).  Options
+ * marked [init] shape tables built by plk_init and may only be set before it (PLK_ERR_ARG
+ * after). */
+enum {
+  PLK_OPT_TINY_CALLS = 1,        /* 1: toy-size host calls through mapped pinned memory; 0: staged copies */
+  PLK_OPT_PROVE_SYNC = 2,        /* 0: a proof's end is seen by polling its completion word; 1: stream sync */
+  PLK_OPT_POLY_BLOCK_L = 3,      /* blocked poly_mul piece lengths; 0 = the exact-range maxima       */
+  PLK_OPT_POLY_BLOCK_S = 4,      /*   (both set: forces the blocked path with those pieces, >= 33)   */
+  PLK_OPT_NTT_F29 = 5,           /* 1: poly_mul over F29 where exact; 0: BabyBear only                */
+  PLK_OPT_NTT_SHARE = 6,         /* 1: an operand given twice in one batch is transformed once        */
+  PLK_OPT_NTT_SHARED_FIX = 7,    /* 1: shared operands' lo = 0 pass in its own launch (auto), 0 off, 2 forced */
+  PLK_OPT_NTT_T13_MIN_K = 8,     /* [init] 21: 2^13-element tiles from 2^k points up (13..27)        */
+  PLK_OPT_NTT_CENTER_BLOCKS = 9, /* 0: resident blocks of the center kernel from the CU count        */
+  PLK_OPT_MSM_THREADS = 10,      /* MSM launch geometry overrides (0 = the built-in choice):          */
+  PLK_OPT_MSM_MAX_BLOCKS = 11,   /*   threads 256/512/1024, resident blocks, groups in flight 1/2/4, */
+  PLK_OPT_MSM_GROUPS = 12,       /*   table copies 1/8, half groups for single MSMs (1 = on)          */
+  PLK_OPT_MSM_COPIES = 13,
+  PLK_OPT_MSM_HALF = 14,
+  PLK_OPT_MSM_SHARD_MIN = 15,    /* multi-device plk_msm_g1: split from this many points (2^16)      */
+  PLK_OPT_COUNT = 16
+};
+int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
+int64_t plk_get_option(int opt);              /* -1 for an unknown option */
+
 /* ---- host-buffer entry points (what the drop-in headers call) ------------------------ */
 
 /* Replaces the body of srs_eval_at_s (src/srs.h:53-68):

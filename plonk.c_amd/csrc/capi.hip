@@ -5,6 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -61,6 +62,11 @@ struct Ctx {
   uint8_t* d_ops = nullptr;
   size_t cap_ops = 0;
 } g;
+
+// the initialised device, published after init_locked (-1: not initialised), so that device
+// entry points take no lock once the library is up: a host-buffer call holding g.mu for its
+// uploads or a serial fold does not stall another thread's kernel launches
+std::atomic<int> g_live_dev{-1};
 
 // ---- E(F101) tables, built from the group law on canonical points ----------------------
 struct HP { int x, y, inf; };
@@ -268,15 +274,10 @@ struct Stage {
 
 // Toy-size calls: TINY_BYTES of mapped coherent pinned memory (h_tiny / d_tiny).  Only for
 // kernels that read their inputs and plain-store their outputs there (no atomics on host memory);
-// PLK_TINY=0 sends every call through the staged device copies instead.
+// PLK_OPT_TINY_CALLS = 0 sends every call through the staged device copies instead.
 constexpr size_t TINY_BYTES = 16u << 10;
 bool tiny_ok(size_t bytes) {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("PLK_TINY");
-    on = e ? atoi(e) != 0 : 1;
-  }
-  if (!on || bytes > TINY_BYTES) return false;
+  if (!plk_opt(PLK_OPT_TINY_CALLS) || bytes > TINY_BYTES) return false;
   if (!g.h_tiny) {
     if (hipHostMalloc((void**)&g.h_tiny, TINY_BYTES, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
       g.h_tiny = nullptr;
@@ -338,6 +339,7 @@ int init_locked(int device) {
   PLK_HIP(hipMalloc((void**)&g.d_nz, 16));
   g.device = device;
   g.ready = true;
+  g_live_dev.store(device, std::memory_order_release);
   return PLK_OK;
 }
 
@@ -352,8 +354,8 @@ int ensure_locked(void) {
 }
 
 int ensure_dev(void) {
-  int dev = -1;
-  {
+  int dev = g_live_dev.load(std::memory_order_acquire);
+  if (dev < 0) {
     std::lock_guard<std::mutex> lk(g.mu);
     int rc = init_locked(-1);
     if (rc) return rc;
@@ -367,6 +369,37 @@ int ensure_dev(void) {
   }
   return PLK_OK;
 }
+
+// ---- options (include/plonkhip.h PLK_OPT_*): the library's only switches besides the
+// device selection; atomics so that a launch reads a consistent value without the lock
+struct OptDef {
+  int64_t def, lo, hi;
+  bool init_only;
+};
+const OptDef kOpt[PLK_OPT_COUNT] = {
+    {0, 0, 0, false},                          // (0: unused)
+    {1, 0, 1, false},                          // TINY_CALLS
+    {0, 0, 1, false},                          // PROVE_SYNC
+    {0, 0, (1ll << 26) - 3670016 + 1, false},  // POLY_BLOCK_L
+    {0, 0, 3670016, false},                    // POLY_BLOCK_S
+    {1, 0, 1, false},                          // NTT_F29
+    {1, 0, 1, false},                          // NTT_SHARE
+    {1, 0, 2, false},                          // NTT_SHARED_FIX
+    {21, 13, 28, true},                        // NTT_T13_MIN_K (the column tables depend on it)
+    {0, 0, 1 << 20, false},                    // NTT_CENTER_BLOCKS
+    {0, 0, 1024, false},                       // MSM_THREADS
+    {0, 0, 8 * 65535, false},                  // MSM_MAX_BLOCKS
+    {0, 0, 4, false},                          // MSM_GROUPS
+    {0, 0, 8, false},                          // MSM_COPIES
+    {1, 0, 1, false},                          // MSM_HALF
+    {1 << 16, 1, 1ll << 40, false},            // MSM_SHARD_MIN
+};
+struct Opts {
+  std::atomic<int64_t> v[PLK_OPT_COUNT];
+  Opts() {
+    for (int i = 0; i < PLK_OPT_COUNT; i++) v[i].store(kOpt[i].def);
+  }
+} g_opt;
 
 // Bump-carves the small-op device arena (poly_eval / poly_divide / matrix host calls).
 struct Arena {
@@ -391,6 +424,10 @@ void plk_set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+int64_t plk_opt(int opt) {
+  return opt > 0 && opt < PLK_OPT_COUNT ? g_opt.v[opt].load(std::memory_order_relaxed) : -1;
+}
+
 // device provers (prove.hip) hold the context: plk_shutdown keeps the tables while any is alive
 int plk_ctx_retain(void) {
   int rc = ensure_dev();
@@ -408,6 +445,28 @@ void plk_ctx_release(void) {
 extern "C" {
 
 const char* plk_last_error(void) { return g_err; }
+
+int plk_set_option(int opt, int64_t value) {
+  if (opt <= 0 || opt >= PLK_OPT_COUNT) {
+    plk_set_error("plk_set_option: unknown option %d", opt);
+    return PLK_ERR_ARG;
+  }
+  const OptDef& d = kOpt[opt];
+  if (value < d.lo || value > d.hi) {
+    plk_set_error("plk_set_option(%d): %lld outside [%lld, %lld]", opt, (long long)value, (long long)d.lo,
+                  (long long)d.hi);
+    return PLK_ERR_ARG;
+  }
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (d.init_only && g.ready && g_opt.v[opt].load() != value) {
+    plk_set_error("plk_set_option(%d) shapes the tables plk_init builds: set it before plk_init", opt);
+    return PLK_ERR_ARG;
+  }
+  g_opt.v[opt].store(value);
+  return PLK_OK;
+}
+
+int64_t plk_get_option(int opt) { return plk_opt(opt); }
 const char* plk_version(void) { return "libplonkhip 0.1 gfx950"; }
 
 int plk_device_count(void) {
@@ -428,6 +487,7 @@ void plk_shutdown(void) {
     plk_set_error("plk_shutdown: %d prover(s) still alive; nothing released", g.live_provers);
     return;
   }
+  g_live_dev.store(-1, std::memory_order_release);
   (void)hipSetDevice(g.device);
   (void)hipStreamSynchronize(g.st);
   (void)hipFree(g.d_pts); (void)hipFree(g.d_sc); (void)hipFree(g.d_res);

@@ -587,24 +587,11 @@ int plk_msm_upload_tables(const uint32_t* ytab, const uint8_t* exp4, const uint8
 // at 8 x 2^22: 25.3 -> 24.9 us; one MSM: unchanged (tools/msm_layout_lab.hip).
 // G (groups in flight per thread and iteration) is 1: with <= 2 groups per thread two
 // iterations of one group measured faster than one of two.
-// Overridable for tuning with PLK_MSM_THREADS / PLK_MSM_MAX_BLOCKS / PLK_MSM_G.
-namespace {
-int env_int(const char* name) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : 0;
-}
-}  // namespace
-
+// Overridable for tuning with PLK_OPT_MSM_THREADS / _MAX_BLOCKS / _GROUPS / _COPIES / _HALF.
 void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* gpt, int* copies, int* half) {
-  static int env_threads = -1, env_blocks = -1, env_g = -1, env_c = -1, env_half = -1;
-  if (env_threads < 0) {
-    env_threads = env_int("PLK_MSM_THREADS");
-    env_blocks = env_int("PLK_MSM_MAX_BLOCKS");
-    env_g = env_int("PLK_MSM_G");
-    env_c = env_int("PLK_MSM_COPIES");
-    const char* e = getenv("PLK_MSM_HALF");
-    env_half = e ? atoi(e) : 1;
-  }
+  const int env_threads = (int)plk_opt(PLK_OPT_MSM_THREADS), env_blocks = (int)plk_opt(PLK_OPT_MSM_MAX_BLOCKS),
+            env_g = (int)plk_opt(PLK_OPT_MSM_GROUPS), env_c = (int)plk_opt(PLK_OPT_MSM_COPIES),
+            env_half = (int)plk_opt(PLK_OPT_MSM_HALF);
   const uint64_t groups = n >> 4;
   int th = groups >= 64ull * 1024 ? 512 : 256;
   if (env_threads == 256 || env_threads == 512 || env_threads == 1024) th = env_threads;
@@ -619,12 +606,12 @@ void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* gpt
   const uint64_t per_thread = groups / (b * (uint64_t)th);
   int g = 1;
   // two groups in flight per thread where a thread has them (with the 16 KB table four blocks
-  // share a CU; +1.5-2 % on the headline over one group; PLK_MSM_G overrides)
+  // share a CU; +1.5-2 % on the headline over one group; PLK_OPT_MSM_GROUPS overrides)
   const int gmax = (env_g == 1 || env_g == 2 || env_g == 4) ? env_g : 2;
   while (g < gmax && (uint64_t)(2 * g) <= per_thread) g *= 2;
   // table copies: eight keep the gathers nearly conflict-free (a single 2^22-point MSM: lookups
   // 0.2 us shorter than with one copy, tools/msm_single_lab.hip) and the fill is off the
-  // critical path (its words are loaded before the points); PLK_MSM_COPIES=1 for tuning
+  // critical path (its words are loaded before the points); PLK_OPT_MSM_COPIES = 1 for tuning
   int c = 8;
   if (env_c == 1 || env_c == 8) c = env_c;
   // a single MSM whose threads have at most one group each (one resident round): half groups

@@ -534,22 +534,21 @@ bool plk_poly_mul_summable(uint64_t la, uint64_t lb) {
 // schoolbook loop -- run BLOCKED: the longer operand in pieces of PLK_BLK_L, the shorter in
 // pieces of PLK_BLK_S coefficients, every piece product an in-range F29 product of a 2^26-point
 // transform, accumulated mod 17 into the zeroed output at the pieces' offset sum.
-// PLK_POLY_BLOCK=L,S (host env) forces the blocked path with smaller pieces (tests).
-static uint64_t PLK_BLK_S = 3670016;                    // F29's exact range: 128 S < p
-static uint64_t PLK_BLK_L = (1ull << 26) - 3670016 + 1;  // L + S - 1 = 2^26 (no wrap)
-static bool g_blk_forced = false;
-static void blk_env() {   // read on every call (tests switch it within one process)
-  const char* e = getenv("PLK_POLY_BLOCK");
-  unsigned long long l = 0, s = 0;
-  g_blk_forced = e && sscanf(e, "%llu,%llu", &l, &s) == 2 && l >= 33 && s >= 33 && s <= 3670016 &&
-                 l <= (1ull << 26) - 3670016 + 1;
-  PLK_BLK_L = g_blk_forced ? l : (1ull << 26) - 3670016 + 1;
-  PLK_BLK_S = g_blk_forced ? s : 3670016;
+// PLK_OPT_POLY_BLOCK_L / _S force the blocked path with smaller pieces (tests).
+struct BlkSizes {
+  uint64_t L, S;   // piece lengths of the longer / shorter operand
+  bool forced;
+};
+static BlkSizes blk_sizes() {
+  const int64_t l = plk_opt(PLK_OPT_POLY_BLOCK_L), s = plk_opt(PLK_OPT_POLY_BLOCK_S);
+  const bool forced = l >= 33 && s >= 33;
+  return forced ? BlkSizes{(uint64_t)l, (uint64_t)s, true}
+                : BlkSizes{(1ull << 26) - 3670016 + 1, 3670016, false};   // F29's range: 128 S < p; L + S - 1 = 2^26
 }
 static bool blocked_shape(uint64_t la, uint64_t lb) {
-  blk_env();
+  const BlkSizes bs = blk_sizes();
   const uint64_t mn = la < lb ? la : lb, mx = la < lb ? lb : la;
-  if (g_blk_forced) return mn > PLK_BLK_S || mx > PLK_BLK_L;
+  if (bs.forced) return mn > bs.S || mx > bs.L;
   return mn * 256 >= bb::P || product_plan(la, lb, nullptr) > bb::TWO_ADICITY;
 }
 static size_t blocked_ws(uint64_t la, uint64_t lb);
@@ -579,12 +578,7 @@ static size_t pass_lds(int M, int C, bool center) {
 static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, void* d_work, hipStream_t st,
                      uint32_t* d_nz = nullptr) {
   // F29 (lazy reduction, fewer VALU per butterfly) whenever every convolution term fits it
-  static int no29 = -1;
-  if (no29 < 0) {
-    const char* e = getenv("PLK_NTT_NO_F29");
-    no29 = e && atoi(e) != 0;
-  }
-  bool use29 = !no29 && k <= f29::TWO_ADICITY;
+  bool use29 = plk_opt(PLK_OPT_NTT_F29) && k <= f29::TWO_ADICITY;
   for (int i = 0; i < m; i++) {
     // a sum group of gs products must fit as a whole: gs * 64 min <= (p - 1) / 2
     int gs = 1;
@@ -605,11 +599,7 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
   // operands: job i owns slots 2i (a) and 2i+1 (b) of d_work; an operand equal (same bytes,
   // same length) to an earlier one of the same launch chunk (PLK_WAVE_MAX_JOBS jobs: a chunk's
   // forward passes transform its distinct arrays) reuses that slot's transform
-  static int noshare = -1;
-  if (noshare < 0) {
-    const char* e = getenv("PLK_NTT_NO_SHARE");
-    noshare = e && atoi(e) != 0;
-  }
+  const bool noshare = !plk_opt(PLK_OPT_NTT_SHARE);
   uint32_t* W = (uint32_t*)d_work;
   int slot[64][2], refs[128] = {0};
   bool fixb[64];   // b's forward transform supplied (PlkPolyMulJob::bt) for this k and field
@@ -652,13 +642,12 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
   for (int i = 0; i < m; i++) {
     const PlkPolyMulJob& j = g[i];
     const uint64_t e = es ? es[i] : 0;
-    w[i] = WJob{j.a, j.b, j.la, j.lb, j.out, j.la + j.lb - 1 - e, W + ((size_t)slot[i][0] << k),
-                W + ((size_t)slot[i][1] << k), W + ((size_t)cslot[i] << k)};
+    // (a supplied b transform has no slot: B is the caller's words, read only)
+    uint32_t* B = fixb[i] ? const_cast<uint32_t*>(j.bt) : W + ((size_t)slot[i][1] << k);
+    w[i] = WJob{j.a, j.b, j.la, j.lb, j.out, j.la + j.lb - 1 - e, W + ((size_t)slot[i][0] << k), B,
+                W + ((size_t)cslot[i] << k)};
     w[i].ntop = (int)e;
-    if (fixb[i]) {
-      w[i].B = const_cast<uint32_t*>(j.bt);   // (read only)
-      w[i].bfix = 1;
-    }
+    w[i].bfix = fixb[i] ? 1 : 0;
   }
   if (m == 1) w[0].nz = d_nz;
   // sum groups: a member (acc) adds its center output into its leader's first inverse pass
@@ -690,8 +679,9 @@ __global__ __launch_bounds__(256) void acc17_kernel(uint8_t* __restrict__ out, c
 static uint64_t align256(uint64_t v) { return (v + 255) & ~255ull; }
 // workspace of the blocked path: one piece product's bytes + the largest piece's own workspace
 static size_t blocked_ws(uint64_t la, uint64_t lb) {
+  const BlkSizes bs = blk_sizes();
   const uint64_t mn = la < lb ? la : lb, mx = la < lb ? lb : la;
-  const uint64_t pl = mx < PLK_BLK_L ? mx : PLK_BLK_L, ps = mn < PLK_BLK_S ? mn : PLK_BLK_S;
+  const uint64_t pl = mx < bs.L ? mx : bs.L, ps = mn < bs.S ? mn : bs.S;
   return (size_t)align256(pl + ps - 1) + plk_poly_mul_workspace_bytes(pl, ps);
 }
 
@@ -708,13 +698,14 @@ static int blocked_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, u
   const uint8_t* L = aL ? d_a : d_b;
   const uint8_t* S = aL ? d_b : d_a;
   const uint64_t lL = aL ? la : lb, lS = aL ? lb : la, rl = la + lb - 1;
-  const uint64_t pl = lL < PLK_BLK_L ? lL : PLK_BLK_L, ps = lS < PLK_BLK_S ? lS : PLK_BLK_S;
+  const BlkSizes bs = blk_sizes();
+  const uint64_t pl = lL < bs.L ? lL : bs.L, ps = lS < bs.S ? lS : bs.S;
   uint8_t* part = (uint8_t*)d_work;
   void* pwork = part + align256(pl + ps - 1);
   PLK_HIP(hipMemsetAsync(d_out, 0, rl, st));
-  for (uint64_t i = 0; i < lL; i += PLK_BLK_L)
-    for (uint64_t j = 0; j < lS; j += PLK_BLK_S) {
-      const uint64_t li = lL - i < PLK_BLK_L ? lL - i : PLK_BLK_L, lj = lS - j < PLK_BLK_S ? lS - j : PLK_BLK_S;
+  for (uint64_t i = 0; i < lL; i += bs.L)
+    for (uint64_t j = 0; j < lS; j += bs.S) {
+      const uint64_t li = lL - i < bs.L ? lL - i : bs.L, lj = lS - j < bs.S ? lS - j : bs.S;
       int rc = plk_poly_mul_launch(L + i, li, S + j, lj, part, nullptr, pwork, st);
       if (rc) return rc;
       const uint64_t len = li + lj - 1, blocks = (len + 255) / 256;
@@ -785,8 +776,7 @@ int plk_poly_mul_transform_plan(uint64_t la, uint64_t lb, int* field) {
   const uint64_t mn = la < lb ? la : lb;
   const int k = product_plan(la, lb, nullptr);
   if (mn <= PLK_DIRECT_MAX || k <= PLK_SMALL_LOG || !plk_wave_ntt_supported(k)) return -1;
-  const char* e = getenv("PLK_NTT_NO_F29");
-  const bool use29 = !(e && atoi(e) != 0) && k <= f29::TWO_ADICITY && mn * 128 < f29::P;
+  const bool use29 = plk_opt(PLK_OPT_NTT_F29) && k <= f29::TWO_ADICITY && mn * 128 < f29::P;
   if (field) *field = use29 ? 1 : 0;
   return k;
 }

@@ -31,6 +31,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 
 #ifndef PLK_NTT_DIAG
 #define PLK_NTT_DIAG 0        // tuning builds only: bit 0 skips the butterflies, bit 1 the LDS exchanges,
@@ -765,25 +766,19 @@ __global__ __launch_bounds__(256) void coltab_kernel(uint32_t* __restrict__ out,
 // ------------------------------------------------------------------------------ host side
 namespace {
 
-// tile bits for a 2^k transform: 2^13 tiles from PLK_NTT_T13_MIN_K (default 21) up
-int tile_bits(int k) {
-  static int min_k = -1;
-  if (min_k < 0) {
-    const char* e = getenv("PLK_NTT_T13_MIN_K");
-    min_k = e ? atoi(e) : 21;
-  }
-  return k >= min_k ? 13 : 12;
-}
+// tile bits for a 2^k transform: 2^13 tiles from PLK_OPT_NTT_T13_MIN_K (default 21) up
+int tile_bits(int k) { return k >= plk_opt(PLK_OPT_NTT_T13_MIN_K) ? 13 : 12; }
 
-// resident blocks of the persistent center kernel: 2 per CU (PLK_NTT_CENTER_BLOCKS overrides)
+// resident blocks of the persistent center kernel: 2 per CU (PLK_OPT_NTT_CENTER_BLOCKS overrides)
 uint32_t center_blocks() {
-  static uint32_t nb = 0;
+  static std::atomic<uint32_t> resident{0};
+  if (const int64_t o = plk_opt(PLK_OPT_NTT_CENTER_BLOCKS)) return (uint32_t)o;
+  uint32_t nb = resident.load(std::memory_order_relaxed);
   if (!nb) {
-    const char* e = getenv("PLK_NTT_CENTER_BLOCKS");
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    nb = e ? (uint32_t)atoi(e) : (PLK_NTT_CW13 >= 8 ? 2u : 1u) * (uint32_t)cus;   // the resident blocks
-    if (!nb) nb = 512;
+    nb = (PLK_NTT_CW13 >= 8 ? 2u : 1u) * (uint32_t)(cus > 0 ? cus : 256);   // the resident blocks
+    resident.store(nb, std::memory_order_relaxed);
   }
   return nb;
 }
@@ -929,17 +924,13 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
   }
   const uint32_t tiles = (uint32_t)((1ull << k) >> TB);
   // operands shared by several products of the batch: their lo = 0 forward pass runs once, in
-  // its own launch, instead of once per product inside the center items (PLK_NTT_SHARED_FIX=0:
-  // off, 2: also next to pretransformed operands).  The extra launch moves a tile's loads and
+  // its own launch, instead of once per product inside the center items (PLK_OPT_NTT_SHARED_FIX
+  // 0: off, 2: also next to pretransformed operands).  The extra launch moves a tile's loads and
   // stores besides its pass (768 tiles: 18.6 us against 20 us less center time in the prover's
   // 2^21 batch): within the ~10 us run-to-run spread of a proof's kernel span either way
   // (tools/prove_ab_prof.sh, medians over 4-5 calls), so batches holding a pretransformed
   // operand keep the per-item passes.
-  static int shfix = -1;
-  if (shfix < 0) {
-    const char* e = getenv("PLK_NTT_SHARED_FIX");
-    shfix = e ? atoi(e) : 1;
-  }
+  const int64_t shfix = plk_opt(PLK_OPT_NTT_SHARED_FIX);
   bool anyfix = false;
   for (int j = 0; j < nj; j++) anyfix |= jobs.j[j].bfix != 0;
   WJobs cj = jobs;

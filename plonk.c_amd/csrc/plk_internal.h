@@ -19,6 +19,7 @@ static_assert(offsetof(plk_msm_result_t, log) == 8 && offsetof(plk_msm_result_t,
 void plk_set_error(const char* fmt, ...);
 int plk_ctx_retain(void);    // a device prover is alive (capi.hip): plk_shutdown keeps the tables
 void plk_ctx_release(void);
+int64_t plk_opt(int opt);    // current value of a PLK_OPT_* option (capi.hip)
 
 #define PLK_HIP(call)                                                                    \
   do {                                                                                   \

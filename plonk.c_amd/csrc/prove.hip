@@ -18,6 +18,7 @@
 // remainders, failed asserts) are computed on the device and checked once at the end.
 #include <stdio.h>
 #include <stdlib.h>
+#include <sched.h>
 #include <string.h>
 
 #include <algorithm>
@@ -1774,19 +1775,18 @@ int check_status(const plk_prover* P, const uint32_t* st, int strict, int circui
 
 int finish(plk_prover* P, int strict, int circuit, uint8_t proof[34]) {
   // trim_pack_kernel wrote P->h_res (mapped pinned) and then this call's completion word: poll it
-  // (the stream's own completion is noticed later than the word; PLK_PROVE_SYNC=1 waits for the
-  // stream instead).  A failed launch never writes it: the stream is queried now and then.
-  static int sync_only = -1;
-  if (sync_only < 0) {
-    const char* e = getenv("PLK_PROVE_SYNC");
-    sync_only = e && atoi(e) != 0;
-  }
+  // (the stream's own completion is noticed later than the word; PLK_OPT_PROVE_SYNC = 1 waits for
+  // the stream instead).  A failed launch never writes it: the stream is queried now and then.
+  // Each poll is followed by a pause, and after ~1 ms of polling by a yield, so a waiting prover
+  // does not starve the other host threads of a core.
   bool seen = false;
-  if (!sync_only) {
+  if (!plk_opt(PLK_OPT_PROVE_SYNC)) {
     const uint32_t* w = (const uint32_t*)(P->h_res + 60);
     for (uint64_t it = 1;; it++) {
       if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == P->seq) { seen = true; break; }
       if (!(it & 4095) && hipStreamQuery(P->st) != hipErrorNotReady) break;   // done (word re-read below) or failed
+      __builtin_ia32_pause();
+      if (it > 16384) sched_yield();
     }
   }
   if (!seen) {

@@ -69,7 +69,14 @@ SIGNATURES = {
     "plk_prover_prove": (C.c_int, [_vp, _vp, _u8p, _u8p, _u8p]),
     "plk_prover_rounds_dev": (C.c_int, [_vp, C.POINTER(_vp), _u8p, _u8p, C.c_int, _u8p]),
     "plk_prover_preprocess": (C.c_int, [_vp, C.POINTER(_vp)]),
+    "plk_set_option": (C.c_int, [C.c_int, C.c_int64]),
+    "plk_get_option": (C.c_int64, [C.c_int]),
 }
+
+# PLK_OPT_* (include/plonkhip.h), by the name without the prefix
+OPTIONS = {"TINY_CALLS": 1, "PROVE_SYNC": 2, "POLY_BLOCK_L": 3, "POLY_BLOCK_S": 4, "NTT_F29": 5, "NTT_SHARE": 6,
+           "NTT_SHARED_FIX": 7, "NTT_T13_MIN_K": 8, "NTT_CENTER_BLOCKS": 9, "MSM_THREADS": 10,
+           "MSM_MAX_BLOCKS": 11, "MSM_GROUPS": 12, "MSM_COPIES": 13, "MSM_HALF": 14, "MSM_SHARD_MIN": 15}
 
 PLK_PROVE_STRICT = 1
 PLK_PROVE_PREPROCESSED = 2
@@ -140,6 +147,51 @@ def _p(a):
 
 def init(device=-1):
     _check("plk_init", lib().plk_init(int(device)))
+
+
+def _opt_id(name):
+    return OPTIONS[name.upper()] if isinstance(name, str) else int(name)
+
+
+def set_option(name, value):
+    """plk_set_option: name = "NTT_F29", ... (PLK_OPT_ without the prefix) or the number"""
+    _check("plk_set_option", lib().plk_set_option(_opt_id(name), int(value)))
+
+
+def get_option(name):
+    return int(lib().plk_get_option(_opt_id(name)))
+
+
+class options:
+    """with options(NTT_F29=0, ...): set for the block, the previous values restored after"""
+
+    def __init__(self, **kw):
+        self.kw = kw
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.old[k] = get_option(k)
+            set_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            set_option(k, v)
+        return False
+
+
+def tune_from_env():
+    """bench / tools only (never called by the library or the tests' product path): apply
+    $PLK_TUNE = "NAME=value,NAME=value" through plk_set_option, for A/B runs of one build.
+    Returns the dict applied."""
+    spec = os.environ.get("PLK_TUNE", "")
+    done = {}
+    for item in filter(None, (t.strip() for t in spec.split(","))):
+        k, v = item.split("=")
+        set_option(k.strip(), int(v))
+        done[k.strip().upper()] = int(v)
+    return done
 
 
 def device_count():
@@ -393,6 +445,7 @@ class Prover:
         if self._h:
             lib().plk_prover_destroy(self._h)
             self._h = _vp()
+        self._fixed = None
 
     def __del__(self):
         try:
@@ -418,14 +471,18 @@ class Prover:
         argument blocks are cached by value (a 2^20-gate proof is ~0.5 ms: building them anew
         each call was ~5 % of it)."""
         cache = self.__dict__.setdefault("_argcache", {})
-        key = (tuple(p if isinstance(p, int) else p.data_ptr() for p in polys), bytes(bytearray(chal)),
-               bytes(bytearray(rand)))
+        ch, rd = _u8(chal).reshape(-1), _u8(rand).reshape(-1)
+        if ch.size != 5 or rd.size != 9:
+            raise ValueError("rounds_dev: chal must hold 5 values and rand 9 (got %d, %d)" % (ch.size, rd.size))
+        if len(polys) != 13:
+            raise ValueError("rounds_dev: 13 polynomials, got %d" % len(polys))
+        key = (tuple(p if isinstance(p, int) else p.data_ptr() for p in polys), ch.tobytes(), rd.tobytes())
         args = cache.get(key)
         if args is None:
             if len(cache) > 64:
                 cache.clear()
-            args = ((_vp * 13)(*key[0]), (C.c_uint8 * 5).from_buffer_copy(key[1][:5].ljust(5, b"\0")),
-                    (C.c_uint8 * 9).from_buffer_copy(key[2][:9].ljust(9, b"\0")))
+            args = ((_vp * 13)(*key[0]), (C.c_uint8 * 5).from_buffer_copy(key[1]),
+                    (C.c_uint8 * 9).from_buffer_copy(key[2]))
             cache[key] = args
         out = self.__dict__.setdefault("_out", (C.c_uint8 * 34)())
         flags = (PLK_PROVE_STRICT if strict else 0) | (PLK_PROVE_PREPROCESSED if preprocessed else 0)
@@ -436,4 +493,8 @@ class Prover:
         """plk_prover_preprocess: the round-3 transforms of q_o q_m q_l q_r s_sigma_3 l_1_x
         (entries 3 4 5 6 10 12 of the 13 device polys); None drops them."""
         arr = None if polys is None else (_vp * 13)(*[_ptr(p) for p in polys])
+        # the transforms are bound to these device addresses: hold the tensors so the caching
+        # allocator cannot hand the same addresses to another circuit's polynomials
+        self._fixed = None
         _check("plk_prover_preprocess", lib().plk_prover_preprocess(self._h, arr))
+        self._fixed = None if polys is None else list(polys)

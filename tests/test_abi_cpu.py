@@ -63,6 +63,32 @@ def test_host_argument_checks():
         plonkhip.srs_eval_at_s([1, 2, 0], [1, 1])
 
 
+def test_options_without_gpu():
+    """plk_set_option / plk_get_option (the library's only switches besides PLK_DEVICE) work with
+    no device; defaults are the production settings; out-of-range values and unknown options
+    are refused; the library source reads no other environment variable."""
+    import plonkhip as h
+    defaults = {"TINY_CALLS": 1, "PROVE_SYNC": 0, "POLY_BLOCK_L": 0, "POLY_BLOCK_S": 0, "NTT_F29": 1,
+                "NTT_SHARE": 1, "NTT_SHARED_FIX": 1, "NTT_T13_MIN_K": 21, "NTT_CENTER_BLOCKS": 0,
+                "MSM_HALF": 1, "MSM_SHARD_MIN": 1 << 16}
+    for k, v in defaults.items():
+        assert h.get_option(k) == v, k
+    with h.options(NTT_SHARED_FIX=2, POLY_BLOCK_L=4096, POLY_BLOCK_S=513):
+        assert h.get_option("NTT_SHARED_FIX") == 2 and h.get_option("POLY_BLOCK_S") == 513
+    assert h.get_option("NTT_SHARED_FIX") == 1 and h.get_option("POLY_BLOCK_L") == 0
+    for k, v in (("NTT_SHARED_FIX", 3), ("NTT_T13_MIN_K", 12), ("POLY_BLOCK_S", 3670017), (99, 0), (0, 0)):
+        with pytest.raises(h.PlonkHipError) as e:
+            h.set_option(k, v)
+        assert e.value.code == h.PLK_ERR_ARG
+    assert h.get_option(99) == -1
+    csrc = os.path.join(PKG, "csrc")
+    envs = set()
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".h")):
+            envs |= set(re.findall(r'getenv\("(\w+)"\)', open(os.path.join(csrc, f)).read()))
+    assert envs == {"PLK_DEVICE"}
+
+
 def _gcc(args, **kw):
     return subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Werror", "-I", INCLUDE] + args,
                           capture_output=True, text=True, **kw)

@@ -2,7 +2,9 @@
 RCCL) rehearsed on the one GPU of a test box: two ranks over gloo sharing cuda:0, strong scaling
 (each 2^22-point MSM split by point range, plonkhip.dist.finish_sharded).  The line must carry the
 strong-scaling config and both correctness checks -- the first MSM against a single-GPU recompute
-and the reference's own 2^22-point golden through the sharded path."""
+and the reference's own 2^22-point golden through the sharded path -- plus C5's replica leg (one
+2^20-gate proof per rank, released together by a barrier, every rank's bytes checked) and the
+MSM components named by the points a rank actually reads (2^21 per shard here)."""
 import json
 import os
 import subprocess
@@ -20,8 +22,8 @@ def test_two_rank_strong_scaling_line():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "1", "--msm-batch", "8", "--rotate-mib", "160",
-           "--no-components", "--no-cpu-baseline"]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+           "--components", "prove,msm", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]          # rank 0 prints exactly one line
@@ -30,3 +32,11 @@ def test_two_rank_strong_scaling_line():
     assert d["config"]["points_per_gpu"] * 2 == d["config"]["points_per_msm"] == 1 << 22
     assert d["checks"] == {"first_msm_single_gpu_recompute": True, "golden_2^22_reference": True}
     assert d["irregular_inputs"] == 0 and d["value"] > 0
+    c = d["components"]
+    rep = c["prove_2^20_gates_replicas"]
+    assert rep["gpus"] == 2 and rep["matches_oracle_all_ranks"] is True and rep["deterministic_all_ranks"] is True
+    assert rep["ms_slowest_rank"] > 0
+    # a shard is 2^21 points: no key may claim 2^22 for it
+    assert "msm_2^21_one_per_launch" in c and "msm_2^21_8_per_launch" in c
+    assert not any(k.startswith("msm_2^22") for k in c)
+    assert "prove_2^20_gates" not in c            # the single-GPU C5 line is not repeated at N > 1

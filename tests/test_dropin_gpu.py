@@ -3,8 +3,9 @@
 34-byte proofs must equal the golden proofs recorded from the all-CPU reference.
 
 The drop-in library (oracle/_ref/libplonkref_dropin.so) can only be BUILT where
-/root/reference exists; it travels to the GPU box with the snapshot.  Without it this module
-skips (the C-ABI parity tests still cover the hot path)."""
+/root/reference exists; it travels to the GPU box with the snapshot (oracle/_ref is git-ignored,
+not gpurun-ignored).  A missing build FAILS these tests, as in test_reference_suite.py: a silent
+skip would hide that the drop-in was never exercised."""
 import os
 
 import numpy as np
@@ -19,8 +20,8 @@ DROPIN = os.path.join(ROOT, "oracle", "_ref", "libplonkref_dropin.so")
 
 @pytest.fixture(scope="module")
 def dropin(hip):
-    if not os.path.exists(DROPIN):
-        pytest.skip("drop-in build absent (needs /root/reference at build time)")
+    assert os.path.exists(DROPIN), ("drop-in build absent: %s (make -C oracle, needs /root/reference at "
+                                    "build time; it travels to the GPU box in the snapshot)" % DROPIN)
     from pyoracle import Reference
     return Reference(DROPIN)
 

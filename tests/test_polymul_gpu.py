@@ -277,25 +277,26 @@ def _eval17(c):
 
 
 @pytest.mark.parametrize("la,lb", [(20000, 15000), (12345, 999), (50000, 50001), (3001, 7000)])
-def test_blocked_forced_vs_oracle(hip, oracle, monkeypatch, la, lb):
-    """The blocked path with small pieces (PLK_POLY_BLOCK=L,S) against the oracle's NTT."""
-    monkeypatch.setenv("PLK_POLY_BLOCK", "3001,1000")
+def test_blocked_forced_vs_oracle(hip, oracle, la, lb):
+    """The blocked path with small pieces (PLK_OPT_POLY_BLOCK_L/_S) against the oracle's NTT."""
     a, b = gen.poly_inputs(77 + la, la, lb)
-    assert hip.poly_mul(a, b) == oracle.poly_mul_ntt(a, b)
+    with hip.options(POLY_BLOCK_L=3001, POLY_BLOCK_S=1000):
+        got = hip.poly_mul(a, b)
+    assert got == oracle.poly_mul_ntt(a, b)
 
 
-def test_blocked_forced_device_api(hip, oracle, monkeypatch):
+def test_blocked_forced_device_api(hip, oracle):
     import torch
-    monkeypatch.setenv("PLK_POLY_BLOCK", "4096,513")
     la, lb = 30000, 2100
     a, b = gen.poly_inputs(5, la, lb)
     dev = torch.device("cuda:0")
     da, db = torch.from_numpy(np.frombuffer(a, np.uint8).copy()).to(dev), torch.from_numpy(np.frombuffer(b, np.uint8).copy()).to(dev)
     out = torch.full((la + lb - 1,), 0xEE, dtype=torch.uint8, device=dev)
     nz = torch.zeros(4, dtype=torch.int32, device=dev)
-    work = torch.zeros(max(16, hip.poly_mul_workspace(la, lb)), dtype=torch.uint8, device=dev)
-    hip.poly_mul_dev(da, la, db, lb, out, nz, work, torch.cuda.current_stream())
-    torch.cuda.synchronize()
+    with hip.options(POLY_BLOCK_L=4096, POLY_BLOCK_S=513):
+        work = torch.zeros(max(16, hip.poly_mul_workspace(la, lb)), dtype=torch.uint8, device=dev)
+        hip.poly_mul_dev(da, la, db, lb, out, nz, work, torch.cuda.current_stream())
+        torch.cuda.synchronize()
     n = int(nz[0].item()) or 1
     assert bytes(out[:n].cpu().numpy()) == oracle.poly_mul_ntt(a, b)
 
@@ -322,40 +323,15 @@ def test_blocked_beyond_babybear_range(hip, oracle):
     assert np.array_equal(full[rl - t:], hi[t - 1:])
 
 
-_SHFIX_SCRIPT = r"""
-import sys, numpy as np, torch
-sys.path[:0] = [sys.argv[1], sys.argv[2], sys.argv[2] + "/golden"]
-import plonkhip as hip
-import test_polymul_gpu as t
-hip.init(0)
-d = np.load(sys.argv[3])
-polys = [d["p%d" % i] for i in range(int(d["np"]))]
-spec = [tuple(int(v) for v in r) for r in d["spec"]]
-for out in t._run_batch(hip, polys, spec):
-    print(t._trim(out).hex())
-"""
-
-
-@pytest.mark.parametrize("mode", ["0", "2"])
-def test_batch_shared_operands_fix_modes(hip, oracle, tmp_path, mode):
+@pytest.mark.parametrize("mode", [0, 2])
+def test_batch_shared_operands_fix_modes(hip, oracle, mode):
     """The batch of test_batch_shared_operands with the shared operands' separate lo = 0 pass off
-    (PLK_NTT_SHARED_FIX=0: every center item transforms its operands) and forced (2), each read
-    once per process: a child process per mode."""
-    import os
-    import subprocess
-    import sys
+    (PLK_OPT_NTT_SHARED_FIX = 0: every center item transforms its operands) and forced (2)."""
     polys = [np.frombuffer(gen.poly_inputs(40 + i, n, 1)[0], np.uint8) for i, n in enumerate(_POOL)]
     spec = [(0, 1, 0), (0, 2, 0), (1, 2, 0), (0, 0, 0), (3, 4, 0), (4, 5, 0), (2, 5, 0), (0, 1, 0),
             (6, 7, 1), (0, 7, 1), (5, 5, 0), (1, 4, 0), (1, 1, 0), (3, 3, 0), (2, 4, 0)]
-    f = tmp_path / "case.npz"
-    np.savez(f, np=len(polys), spec=np.array(spec), **{"p%d" % i: p for i, p in enumerate(polys)})
-    here = os.path.dirname(os.path.abspath(__file__))
-    pkg = os.path.join(os.path.dirname(here), "plonk.c_amd")
-    env = dict(os.environ, PLK_NTT_SHARED_FIX=mode)
-    r = subprocess.run([sys.executable, "-c", _SHFIX_SCRIPT, pkg, here, str(f)], capture_output=True, text=True,
-                       env=env, timeout=300)
-    assert r.returncode == 0, r.stderr[-2000:]
-    got = r.stdout.strip().splitlines()[-len(spec):]
+    with hip.options(NTT_SHARED_FIX=mode):
+        got = [_trim(out).hex() for out in _run_batch(hip, polys, spec)]
     full = len(polys[6]) + len(polys[7]) - 1
 
     def prod(i, j):

@@ -206,21 +206,12 @@ def test_toy_size_calls_vs_oracle(hip, oracle):
 
 
 def test_toy_size_path_matches_staged_path(hip):
-    """PLK_TINY=0 (every host call staged through device copies) in a child process gives the
-    same bytes as the mapped-memory path of this process"""
-    import json
-    import os
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = ("import sys, json; sys.path[:0] = [%r, %r, %r]; import torch; import plonkhip as h; h.init(0); "
-            "import test_polyops_gpu as t; print(json.dumps(t._child_digest(h)))"
-            % (os.path.join(root, "plonk.c_amd"), os.path.join(root, "tests"), os.path.join(root, "tests", "golden")))
-    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, PLK_TINY="0"), capture_output=True,
-                       text=True, timeout=120)
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert json.loads(r.stdout.strip().splitlines()[-1]) == _child_digest(hip)
+    """PLK_OPT_TINY_CALLS = 0 (every host call staged through device copies) gives the same
+    bytes as the mapped-memory path"""
+    want = _child_digest(hip)
+    with hip.options(TINY_CALLS=0):
+        got = _child_digest(hip)
+    assert got == want
 
 
 def _child_digest(h):

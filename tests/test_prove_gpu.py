@@ -169,6 +169,7 @@ _TILE13_SCRIPT = r"""
 import sys, numpy as np, torch
 sys.path[:0] = sys.argv[1:2]
 import plonkhip as hip
+hip.set_option("NTT_T13_MIN_K", 13)   # shapes the column tables: before plk_init
 hip.init(0)
 d = np.load(sys.argv[2])
 n = int(d["n"])
@@ -179,8 +180,8 @@ print(pr.rounds_dev(polys, [int(x) for x in d["chal"]], [int(x) for x in d["rnd"
 
 
 def test_rounds_2_16_tiles13_vs_oracle(hip, oracle, tmp_path):
-    """Same instance with every transform on the 2^13-element tile engine (PLK_NTT_T13_MIN_K
-    = 13, read once per process: a child process), so the batched prover runs the tile size
+    """Same instance with every transform on the 2^13-element tile engine (PLK_OPT_NTT_T13_MIN_K
+    = 13, set before plk_init: a child process), so the batched prover runs the tile size
     that 2^21..2^23 products use at n = 2^20."""
     import os
     import subprocess
@@ -190,9 +191,8 @@ def test_rounds_2_16_tiles13_vs_oracle(hip, oracle, tmp_path):
     np.savez(f, n=c["n"], zh=c["zh"], pts=c["pts"], chal=np.array(c["chal"]), rnd=np.array(c["rnd"]),
              **{"p%d" % i: p for i, p in enumerate(c["polys"])})
     pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plonk.c_amd")
-    env = dict(os.environ, PLK_NTT_T13_MIN_K="13")
     r = subprocess.run([sys.executable, "-c", _TILE13_SCRIPT, pkg, str(f)], capture_output=True, text=True,
-                       env=env, timeout=300)
+                       timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().splitlines()[-1] == c["want"].hex()
 
@@ -228,3 +228,41 @@ def test_rounds_preprocessed_vs_plain(hip, n, seed):
     want = pr.rounds_dev(dev, chal, rnd)
     pr.preprocess(dev)
     assert pr.rounds_dev(dev, chal, rnd, preprocessed=True).hex() == want.hex()
+
+
+def test_rounds_challenge_forms_agree(hip):
+    """rounds_dev normalises chal / rand like prove(): int64 numpy arrays, lists and bytes give
+    the same proof (a raw byte copy of an int64 array would put zeros in 4 of 5 challenges); a
+    wrong count is an error, not silent padding."""
+    n = 1 << 10
+    polys, chal, rnd, zh, pts = _synthetic(n, 5, 2 * n + 8)
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    want = pr.rounds_dev(dev, list(chal), list(rnd))
+    assert pr.rounds_dev(dev, np.array(list(chal), np.int64), np.array(list(rnd), np.int64)) == want
+    assert pr.rounds_dev(dev, bytes(list(chal)), bytes(list(rnd))) == want
+    with pytest.raises(ValueError):
+        pr.rounds_dev(dev, list(chal)[:4], list(rnd))
+    with pytest.raises(ValueError):
+        pr.rounds_dev(dev, list(chal), list(rnd) + [1])
+
+
+def test_preprocessed_tensors_held_and_overwrite_needs_preprocess(hip):
+    """The preprocessed transforms are bound to device addresses: the Prover keeps the tensors it
+    was given alive (their addresses cannot be handed to another circuit), and new bytes written
+    in place at those addresses take effect after preprocess() is called again (the contract in
+    include/plonkhip.h) -- equal to the plain proof of the new bytes."""
+    n = 1 << 12
+    polys, chal, rnd, zh, pts = _synthetic(n, 9, 2 * n + 8)
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    pr.preprocess(dev)
+    assert pr._fixed is not None and all(a is b for a, b in zip(pr._fixed, dev))
+    polys2, _, _, _, _ = _synthetic(n, 10, 2 * n + 8)
+    for i in (3, 4, 5, 6, 10, 12):                     # the fixed circuit polynomials, in place
+        dev[i].copy_(torch.from_numpy(polys2[i]).to("cuda"))
+    want = pr.rounds_dev(dev, chal, rnd)                # plain: reads the new bytes
+    pr.preprocess(dev)
+    assert pr.rounds_dev(dev, chal, rnd, preprocessed=True) == want
+    pr.preprocess(None)
+    assert pr._fixed is None

@@ -15,6 +15,7 @@ import torch  # noqa: E402
 import plonkhip as hip  # noqa: E402
 from bench import make_msm_sets, single_msm_component  # noqa: E402
 
+hip.tune_from_env()   # PLK_TUNE="NAME=value,..." (plk_set_option), tuning runs only
 hip.init(0)
 dev = torch.device("cuda", 0)
 n, sets = 1 << 22, 40

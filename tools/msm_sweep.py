@@ -26,6 +26,7 @@ def main():
     log2n = int(sys.argv[1]) if len(sys.argv) > 1 else 22
     n = 1 << log2n
     dev = torch.device("cuda", 0)
+    hip.tune_from_env()   # PLK_TUNE="NAME=value,..." (plk_set_option), tuning runs only
     hip.init(0)
     st = torch.cuda.current_stream()
     sets = 40 if log2n >= 22 else 64

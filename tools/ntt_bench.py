@@ -12,6 +12,7 @@ import torch  # noqa: E402
 import plonkhip as hip  # noqa: E402
 from bench import event_avg_ms  # noqa: E402
 
+hip.tune_from_env()   # PLK_TUNE="NAME=value,..." (plk_set_option), tuning runs only
 hip.init(0)
 dev = torch.device("cuda", 0)
 st = torch.cuda.current_stream()

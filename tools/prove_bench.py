@@ -13,6 +13,7 @@ import torch  # noqa: E402
 import plonkhip as hip  # noqa: E402
 from bench import prove_component  # noqa: E402
 
+hip.tune_from_env()   # PLK_TUNE="NAME=value,..." (plk_set_option), tuning runs only
 hip.init(0)
 dev = torch.device("cuda", 0)
 pre = "--pre" in sys.argv   # the preprocessed-circuit path (plk_prover_preprocess) instead

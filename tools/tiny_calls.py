@@ -14,6 +14,7 @@ import torch  # noqa: E402,F401  (one HIP runtime per process)
 
 import plonkhip as hip  # noqa: E402
 
+hip.tune_from_env()   # PLK_TUNE="NAME=value,..." (plk_set_option), tuning runs only
 hip.init(0)
 rng = np.random.default_rng(1)
 p8 = rng.integers(0, 17, 8, dtype=np.uint8)
