@@ -41,6 +41,16 @@ enum {
 
 /* ---- lifetime ------------------------------------------------------------------------ */
 int plk_init(int device);            /* select device (<0: $PLK_DEVICE or 0); idempotent */
+/* Several GPUs in one process (SURVEY 8(b) plk_init(n_gpus), 8(e)): ids[0] is the primary
+ * device (everything runs there as after plk_init(ids[0])); plk_msm_g1 -- srs_eval_at_s, the
+ * reference's commitment -- splits an MSM of at least PLK_OPT_MSM_SHARD_MIN points into n
+ * contiguous point ranges, one per entry, each uploaded over its own device's link from its own
+ * host thread and reduced to a partial discrete log there; the N 4-byte partials are summed
+ * on the host (the result returns to the host anyway).  Ids may repeat (several shards on one
+ * GPU).  Calling again replaces the list; n = 1 goes back to one device.  PLK_DEVICE="0,1,2,3"
+ * does the same at implicit initialisation.  1 <= n <= 16. */
+int plk_init_devices(const int *ids, int n);
+int plk_devices(int *ids, int cap);  /* the shard list (or the one device); returns its length */
 void plk_shutdown(void);
 const char *plk_last_error(void);
 int plk_device_count(void);

@@ -14,4 +14,14 @@
 #include "poly.h"
 #include "srs.h"
 #include "matrix.h"
+
+/* Build-time policy for a drop-in build (no source change in the reference): with
+ * -DPLK_DROPIN_SHARD_MIN=m, srs_eval_at_s splits every MSM of >= m points over the devices of
+ * plk_init_devices / PLK_DEVICE="0,1,..." (the tests build the reference's programs with m = 1
+ * to run every commitment through the shards). */
+#ifdef PLK_DROPIN_SHARD_MIN
+__attribute__((constructor)) static void plk_dropin_shard_policy(void) {
+  (void)plk_set_option(PLK_OPT_MSM_SHARD_MIN, PLK_DROPIN_SHARD_MIN);
+}
+#endif
 #endif

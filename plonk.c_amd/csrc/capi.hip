@@ -92,6 +92,11 @@ HP hp_add(HP a, HP b) {
   return HP{xr, yr, 0};
 }
 
+// the kernel tables as built (uploaded again to every further device of plk_init_devices)
+uint32_t s_ytab[512];
+uint8_t s_exp4[PLK_GROUP_ORDER * 4];
+uint8_t s_inv[PLK_GF_P];
+
 int build_group_tables(uint8_t gen_out[3]) {
   std::vector<HP> pts;
   for (int x = 0; x < PLK_GF_P; x++)
@@ -145,6 +150,9 @@ int build_group_tables(uint8_t gen_out[3]) {
   gen_out[0] = (uint8_t)g0.x;
   gen_out[1] = (uint8_t)g0.y;
   gen_out[2] = 0;
+  memcpy(s_ytab, ytab, sizeof s_ytab);
+  memcpy(s_exp4, exp4, sizeof s_exp4);
+  memcpy(s_inv, inv, sizeof s_inv);
   return plk_msm_upload_tables(ytab, exp4, inv);
 }
 
@@ -306,6 +314,23 @@ int tick0(int n, uint8_t** out) {
   return PLK_OK;
 }
 
+// "a,b,c" -> device ids (at most PLK_MAX_SHARDS); returns the count, 0 if malformed
+int parse_devices(const char* e, int* ids) {
+  int n = 0;
+  const char* p = e;
+  while (*p && n < PLK_MAX_SHARDS) {
+    char* end = nullptr;
+    const long v = strtol(p, &end, 10);
+    if (end == p || v < 0 || v > 4095) return 0;
+    ids[n++] = (int)v;
+    p = end;
+    while (*p == ' ') p++;
+    if (*p == ',') p++;
+    else if (*p) return 0;
+  }
+  return n;
+}
+
 int init_locked(int device) {
   if (g.ready) {
     if (device >= 0 && device != g.device) {
@@ -320,15 +345,25 @@ int init_locked(int device) {
     plk_set_error("no HIP device available (libplonkhip has no CPU fallback)");
     return PLK_ERR_NODEV;
   }
-  if (device < 0) {   // implicit: $PLK_DEVICE, else the calling thread's current device
+  int list[PLK_MAX_SHARDS], nlist = 0;
+  if (device < 0) {   // implicit: $PLK_DEVICE ("2", or a list "0,1,2,3" of shards), else the current device
     const char* e = getenv("PLK_DEVICE");
-    if (e) device = atoi(e);
-    else if (hipGetDevice(&device) != hipSuccess) device = 0;
+    if (e) {
+      nlist = parse_devices(e, list);
+      if (!nlist) {
+        plk_set_error("PLK_DEVICE=\"%s\": expected a device id or a comma list of ids", e);
+        return PLK_ERR_ARG;
+      }
+      device = list[0];
+    } else if (hipGetDevice(&device) != hipSuccess) {
+      device = 0;
+    }
   }
-  if (device >= count) {
-    plk_set_error("device %d out of range (%d devices)", device, count);
-    return PLK_ERR_NODEV;
-  }
+  for (int i = 0; i < (nlist ? nlist : 1); i++)
+    if ((nlist ? list[i] : device) >= count) {
+      plk_set_error("device %d out of range (%d devices)", nlist ? list[i] : device, count);
+      return PLK_ERR_NODEV;
+    }
   PLK_HIP(hipSetDevice(device));
   PLK_HIP(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
   int rc = build_group_tables(g.gen);
@@ -340,6 +375,10 @@ int init_locked(int device) {
   g.device = device;
   g.ready = true;
   g_live_dev.store(device, std::memory_order_release);
+  if (nlist > 1) {
+    if ((rc = plk_shards_setup(list, nlist, s_ytab, s_exp4, s_inv))) return rc;
+    PLK_HIP(hipSetDevice(device));
+  }
   return PLK_OK;
 }
 
@@ -480,6 +519,38 @@ int plk_init(int device) {
   return init_locked(device);
 }
 
+int plk_init_devices(const int* ids, int n) {
+  if (!ids || n < 1 || n > PLK_MAX_SHARDS) {
+    plk_set_error("plk_init_devices: %d devices (1..%d)", n, PLK_MAX_SHARDS);
+    return PLK_ERR_ARG;
+  }
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+    plk_set_error("no HIP device available (libplonkhip has no CPU fallback)");
+    return PLK_ERR_NODEV;
+  }
+  for (int i = 0; i < n; i++)
+    if (ids[i] < 0 || ids[i] >= count) {
+      plk_set_error("plk_init_devices: device %d out of range (%d devices)", ids[i], count);
+      return PLK_ERR_NODEV;
+    }
+  std::lock_guard<std::mutex> lk(g.mu);
+  int rc = init_locked(ids[0]);   // the primary: tables, NTT, prover, every non-MSM call
+  if (rc) return rc;
+  rc = plk_shards_setup(ids, n, s_ytab, s_exp4, s_inv);
+  (void)hipSetDevice(g.device);
+  return rc;
+}
+
+int plk_devices(int* ids, int cap) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (!g.ready) return 0;
+  const int ns = plk_shards_count();
+  if (ns > 1) return plk_shards_devices(ids, cap);
+  if (ids && cap > 0) ids[0] = g.device;
+  return 1;
+}
+
 void plk_shutdown(void) {
   std::lock_guard<std::mutex> lk(g.mu);
   if (!g.ready) return;
@@ -488,6 +559,7 @@ void plk_shutdown(void) {
     return;
   }
   g_live_dev.store(-1, std::memory_order_release);
+  plk_shards_teardown();
   (void)hipSetDevice(g.device);
   (void)hipStreamSynchronize(g.st);
   (void)hipFree(g.d_pts); (void)hipFree(g.d_sc); (void)hipFree(g.d_res);
@@ -526,12 +598,13 @@ int plk_dlog_generator(uint8_t out[3]) {
   return PLK_OK;
 }
 
-int plk_msm_g1(const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t out[3]) {
-  if ((!points || !scalars) && n) { plk_set_error("plk_msm_g1: NULL input"); return PLK_ERR_ARG; }
-  if (!out) { plk_set_error("plk_msm_g1: NULL out"); return PLK_ERR_ARG; }
-  std::lock_guard<std::mutex> lk(g.mu);
-  int rc = ensure_locked();
-  if (rc) return rc;
+}  // extern "C"
+
+namespace {
+// plk_msm_g1 on the primary device alone (g.mu held): the cached SRS upload, one launch, and the
+// reference's raw fold on the device when an input is not a canonical group element
+int msm_single_locked(const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t out[3]) {
+  int rc;
   if ((rc = grow(&g.d_sc, &g.cap_sc, n + 16))) return rc;
   const size_t pb = 3 * n;
   const bool hit = n && points == g.srs_key && pb <= g.srs_cached && memcmp(points, g.h_srs, pb) == 0;
@@ -564,6 +637,29 @@ int plk_msm_g1(const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t 
   }
   memcpy(out, h.g1, 3);
   return PLK_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int plk_msm_g1(const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t out[3]) {
+  if ((!points || !scalars) && n) { plk_set_error("plk_msm_g1: NULL input"); return PLK_ERR_ARG; }
+  if (!out) { plk_set_error("plk_msm_g1: NULL out"); return PLK_ERR_ARG; }
+  std::lock_guard<std::mutex> lk(g.mu);
+  int rc = ensure_locked();
+  if (rc) return rc;
+  if (plk_shards_count() > 1 && n >= (size_t)plk_opt(PLK_OPT_MSM_SHARD_MIN)) {
+    // point-range shards on the plk_init_devices list; the exchange is a host sum of their
+    // partial logs.  An irregular encoding anywhere: the reference's raw fold is serial and
+    // order-dependent, so the whole input is folded on the primary device instead
+    uint64_t ls = 0, irr = 0;
+    if ((rc = plk_shards_msm(points, scalars, n, &ls, &irr))) return rc;
+    PLK_HIP(hipSetDevice(g.device));
+    if (irr) return msm_single_locked(points, scalars, n, out);
+    memcpy(out, s_exp4 + 4 * (ls % PLK_GROUP_ORDER), 3);
+    return PLK_OK;
+  }
+  return msm_single_locked(points, scalars, n, out);
 }
 
 int plk_poly_mul(const uint8_t* a, size_t la, const uint8_t* b, size_t lb, uint8_t* out, size_t* out_len) {

@@ -30,6 +30,14 @@ int64_t plk_opt(int opt);    // current value of a PLK_OPT_* option (capi.hip)
     }                                                                                    \
   } while (0)
 
+// shards.hip: in-process multi-device plk_msm_g1 (plk_init_devices); callers hold the library lock
+#define PLK_MAX_SHARDS 16
+int plk_shards_setup(const int* ids, int n, const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101);
+void plk_shards_teardown(void);
+int plk_shards_count(void);
+int plk_shards_devices(int* ids, int cap);
+int plk_shards_msm(const uint8_t* pts, const uint8_t* sc, size_t n, uint64_t* log_sum, uint64_t* irregular);
+
 // msm.hip
 int plk_msm_upload_tables(const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101);
 void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* groups_per_thread, int* copies,

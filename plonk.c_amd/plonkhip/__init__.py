@@ -70,6 +70,8 @@ SIGNATURES = {
     "plk_prover_rounds_dev": (C.c_int, [_vp, C.POINTER(_vp), _u8p, _u8p, C.c_int, _u8p]),
     "plk_prover_preprocess": (C.c_int, [_vp, C.POINTER(_vp)]),
     "plk_set_option": (C.c_int, [C.c_int, C.c_int64]),
+    "plk_init_devices": (C.c_int, [C.POINTER(C.c_int), C.c_int]),
+    "plk_devices": (C.c_int, [C.POINTER(C.c_int), C.c_int]),
     "plk_get_option": (C.c_int64, [C.c_int]),
 }
 
@@ -147,6 +149,20 @@ def _p(a):
 
 def init(device=-1):
     _check("plk_init", lib().plk_init(int(device)))
+
+
+def init_devices(ids):
+    """plk_init_devices: ids[0] is the primary device; plk_msm_g1 point-range shards over the
+    list (repeats allowed: several shards on one GPU)"""
+    ids = [int(i) for i in ids]
+    arr = (C.c_int * max(1, len(ids)))(*ids)
+    _check("plk_init_devices", lib().plk_init_devices(arr, len(ids)))
+
+
+def devices():
+    arr = (C.c_int * 16)()
+    n = int(lib().plk_devices(arr, 16))
+    return [arr[i] for i in range(min(n, 16))]
 
 
 def _opt_id(name):

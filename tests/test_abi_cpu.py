@@ -55,6 +55,21 @@ def test_no_cpu_fallback_without_gpu():
         plonkhip.poly_mul([1, 2], [3, 4])
 
 
+def test_init_devices_without_gpu():
+    """plk_init_devices: a malformed list is PLK_ERR_ARG before any device query; with no device
+    a valid list is PLK_ERR_NODEV (no CPU fallback); plk_devices reports nothing initialised."""
+    import plonkhip as h
+    for bad in ([], [0] * 17):
+        with pytest.raises(h.PlonkHipError) as e:
+            h.init_devices(bad)
+        assert e.value.code == h.PLK_ERR_ARG
+    if h.device_count() == 0:
+        with pytest.raises(h.PlonkHipError) as e:
+            h.init_devices([0, 0])
+        assert e.value.code == h.PLK_ERR_NODEV
+        assert h.devices() == []
+
+
 def test_host_argument_checks():
     import plonkhip
     with pytest.raises(ValueError):
