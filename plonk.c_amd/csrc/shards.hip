@@ -69,6 +69,18 @@ struct Pool {
   bool stop = false;
   const uint8_t* pts = nullptr;
   const uint8_t* sc = nullptr;
+  // a program that exits without plk_shutdown (the reference's own test programs through the
+  // drop-in): the idle workers are released and joined here -- no HIP call, the runtime may be
+  // gone already -- instead of std::thread's terminate on a joinable thread
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      stop = true;
+    }
+    go.notify_all();
+    for (auto& t : th)
+      if (t.joinable()) t.join();
+  }
 } P;
 
 int dgrow(uint8_t** p, size_t* cap, size_t need) {
