@@ -299,6 +299,7 @@ def components(torch, hip, dev, st, want):
     out = {}
     if "msm" in want:
         out.update(msm_components(torch, hip, dev, st))
+        out["msm_2^22_host_call_devices"] = msm_host_devices_component(torch, hip, dev)
     if "ntt" in want:
         out.update(ntt_components(torch, hip, dev, st))
     if "polymul" in want:
@@ -352,6 +353,42 @@ def msm_components(torch, hip, dev, st):
                                  "note": "plk_msm_g1 (what the drop-in srs_eval_at_s calls), host buffers, PCIe "
                                          "included; cached = same SRS pointer and bytes (reference: 9 commitments "
                                          "per proof over one SRS, src/plonk.h:299-301,379,522-524,620-621)"}
+    return out
+
+
+def msm_host_devices_component(torch, hip, dev, n=1 << 22):
+    """srs_eval_at_s's host-buffer call (plk_msm_g1, PCIe included) at 2^22 points on one device
+    and split over several (plk_init_devices: per-device uploads from per-shard host threads, host
+    sum of the partial logs).  On a one-GPU box the list repeats device 0 (the N-device code path,
+    one device's link); on a multi-GPU node it names every visible GPU."""
+    import numpy as np
+    ndev = torch.cuda.device_count()
+    lists = [[0], list(range(ndev))] if ndev > 1 else [[0], [0, 0], [0, 0, 0, 0]]
+    p, c = make_msm_sets(torch, n, 1, dev, 4242)
+    ph, sh = p[0].cpu().numpy(), c[0].cpu().numpy()
+    out = {"points": n, "note": "plk_msm_g1 wall time per call from host buffers; cached = same SRS pointer and "
+                                "bytes (memcmp-verified per shard), uploaded = a fresh SRS array each call; "
+                                "lists of one repeated device rehearse the multi-device path on one GPU"}
+    want = None
+    try:
+        for ids in lists:
+            hip.init_devices(ids)
+            got = hip.msm_g1(ph, sh)
+            want = want or got
+            t0 = time.perf_counter()
+            for _ in range(10):
+                ok = hip.msm_g1(ph, sh) == want
+            cached = (time.perf_counter() - t0) / 10 * 1e6
+            copies = [ph.copy() for _ in range(4)]
+            t0 = time.perf_counter()
+            for cp in copies:
+                ok &= hip.msm_g1(cp, sh) == want
+            fresh = (time.perf_counter() - t0) / 4 * 1e6
+            out["devices_" + "_".join(map(str, ids))] = {"srs_cached_us": round(cached, 1),
+                                                         "srs_uploaded_us": round(fresh, 1),
+                                                         "same_result": bool(ok and got == want)}
+    finally:
+        hip.init_devices([0])
     return out
 
 

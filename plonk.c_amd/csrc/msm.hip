@@ -539,6 +539,328 @@ __global__ __launch_bounds__(FOLD_T) void msm_serial_fold_kernel(const uint8_t* 
   res->g1[3] = 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// The same fold for long inputs, in parallel over chunks (src/srs.h:59-66).
+//
+// Every g1_add result that is not an operand passed through is g1_new(x, y) -- reduced mod 101
+// (src/g1.h:13-20, 55, 82) -- or the identity {0, 0, 1}.  So the accumulator is one of the
+// 10,202 canonical states S = {(x, y, 0) : x, y < 101} + {identity}, except right after an
+// operand passed through: acc = t when acc is "infinite" (or acc unchanged when t is), and then
+// it may be a raw byte triple.  A chunk of terms is therefore a map S -> states, computed here
+// for ALL 10,202 start states at once by one workgroup per chunk:
+//   * trajectories that reach the same state merge (owner table, step-tagged atomicMax: the
+//     lowest trajectory id wins, the others record it as parent);
+//   * trajectories on group elements (canonical on-curve points and the identity: the
+//     reference's formulas ARE the group law there) are kept symbolically in a
+//     102-slot table indexed by log - delta, and a regular term (a canonical group element of
+//     log l) costs delta += l for all of them; an irregular term materialises them first;
+//   * at most two raw trajectories exist at once (a raw state only arises as the current term
+//     or survives an infinite term), kept in a side list and merged by exact bytes.
+// Random chunk maps collapse fast: 10,202 start states -> ~500 live trajectories after 256
+// terms, to the group (regular terms) or to a handful (irregular ones) after ~1000.  A
+// single-wave pass then walks the chunk maps in order from the prefix state (one dependent
+// load per chunk), re-folding a chunk serially only when a raw state crosses its boundary.
+// ---------------------------------------------------------------------------------------
+namespace {
+constexpr int FS_N = 10202;                  // canonical states: x * 101 + y (inf 0), FS_ID = identity
+constexpr int FS_ID = 10201;
+constexpr uint32_t FS_EMPTY = 0xFFFFu;
+constexpr int FC_T = 1024;                   // threads of a chunk workgroup
+constexpr int FC_TB = 1024;                  // terms staged in LDS per refill
+constexpr int FC_SOLO = 512;                 // live trajectories at which wave 0 continues alone
+constexpr uint32_t FC_HDR_BYTES = 256;
+
+struct FoldHdr {
+  unsigned long long first;                  // first irregular point (n if none)
+  uint32_t plog;                             // log of the fold over [0, first)
+};
+
+__device__ __forceinline__ uint32_t pk(RawPt a) { return a.x | a.y << 8 | a.inf << 16; }
+__device__ __forceinline__ RawPt upk(uint32_t v) { return RawPt{v & 0xFFu, (v >> 8) & 0xFFu, (v >> 16) & 0xFFu}; }
+__device__ __forceinline__ RawPt state_of(uint32_t id) {
+  return id == FS_ID ? RawPt{0, 0, 1} : RawPt{id / 101u, id % 101u, 0};
+}
+__device__ __forceinline__ int id_of(RawPt a) {
+  if (a.inf == 0 && a.x < 101 && a.y < 101) return (int)(a.x * 101 + a.y);
+  return (a.inf == 1 && a.x == 0 && a.y == 0) ? FS_ID : -1;
+}
+// log of a canonical group element encoding, 0xFF for anything else (ytab: the dlog table)
+__device__ __forceinline__ uint32_t glog(RawPt a, const uint32_t* ytab) {
+  const uint32_t k = encode(a.x, a.y, a.inf);
+  const uint32_t d = ytab[(a.y | (a.inf & 1u) << 8) & 0x1FFu] - k;
+  return d < 256u ? d : 0xFFu;
+}
+}  // namespace
+
+// Prefix: the fold over [0, first) -- all canonical points -- as a discrete-log sum, and the
+// first irregular point (one block; every point read once).
+__global__ __launch_bounds__(FOLD_T) void msm_fold_prefix_kernel(const uint8_t* __restrict__ pts,
+                                                                 const uint8_t* __restrict__ sc, uint64_t n,
+                                                                 FoldHdr* hdr) {
+  __shared__ uint32_t tab[TAB_ENTRIES];
+  __shared__ uint32_t wsum[FOLD_T / PLK_WAVE];
+  __shared__ unsigned long long s_first;
+  for (int i = threadIdx.x; i < TAB_ENTRIES; i += FOLD_T) tab[i] = c_ytab[i];
+  if (threadIdx.x == 0) s_first = ~0ull;
+  __syncthreads();
+  uint32_t acc = 0;
+  uint64_t first = ~0ull;
+  for (uint64_t base = 0; base < n && first == ~0ull; base += (uint64_t)FOLD_T * FOLD_E) {
+    uint32_t lg[FOLD_E];
+    unsigned long long mine = ~0ull;
+#pragma unroll
+    for (int k = 0; k < FOLD_E; k++) {
+      const uint64_t i = base + (uint64_t)k * FOLD_T + threadIdx.x;
+      lg[k] = 0;
+      if (i < n) {
+        bool bad = false;
+        lg[k] = point_term<1>(encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), sc[i], tab, 0u, bad);
+        if (bad && i < mine) mine = i;
+      }
+    }
+    if (mine != ~0ull) atomicMin(&s_first, mine);
+    __syncthreads();
+    first = s_first;
+#pragma unroll
+    for (int k = 0; k < FOLD_E; k++) {
+      const uint64_t i = base + (uint64_t)k * FOLD_T + threadIdx.x;
+      if (i < first) acc += lg[k];
+    }
+    acc %= PLK_GROUP_ORDER;
+    __syncthreads();
+  }
+  const uint32_t ws = plk_wave_sum(acc);
+  if ((threadIdx.x & (PLK_WAVE - 1)) == 0) wsum[threadIdx.x / PLK_WAVE] = ws;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int w = 0; w < FOLD_T / PLK_WAVE; w++) tot += wsum[w];
+    hdr->first = first < n ? first : n;
+    hdr->plog = tot % PLK_GROUP_ORDER;
+  }
+}
+
+// One chunk [first + b L, first + (b + 1) L) per workgroup: F[b * FS_N + s] = the packed state
+// the chunk's terms take start state s to.
+__global__ __launch_bounds__(FC_T) void msm_fold_chunk_kernel(const uint8_t* __restrict__ pts,
+                                                              const uint8_t* __restrict__ sc, uint64_t n,
+                                                              uint32_t L, const FoldHdr* __restrict__ hdr,
+                                                              uint32_t* __restrict__ F) {
+  __shared__ uint32_t owner[FS_N];           // step-tagged claims; at the end: final state per trajectory
+  __shared__ uint32_t lst[2][FS_N];          // concrete trajectories: state id | trajectory id << 14
+  __shared__ uint16_t par[FS_N];             // merge parent (self = live)
+  __shared__ uint32_t ytab[TAB_ENTRIES];
+  __shared__ uint32_t invl[PLK_GF_P];
+  __shared__ uint32_t expw[PLK_GROUP_ORDER]; // EXP as packed bytes
+  __shared__ uint32_t gslot[PLK_GROUP_ORDER];
+  __shared__ uint32_t tt[FC_TB];             // term bytes | log << 24 (log 0xFF: irregular)
+  __shared__ uint32_t rawst[8], rawtid[8], stst[16], sttid[16];
+  __shared__ uint32_t s_cnt[4], s_ng, s_nr, s_ns;
+  const uint64_t first = hdr->first;
+  const uint64_t c0 = first + (uint64_t)blockIdx.x * L;
+  if (c0 >= n) return;
+  const uint64_t c1 = n - c0 < L ? n : c0 + L;
+  const uint32_t me = threadIdx.x;
+  uint32_t nt = FC_T;
+  for (uint32_t i = me; i < TAB_ENTRIES; i += nt) ytab[i] = c_ytab[i];
+  for (uint32_t i = me; i < PLK_GF_P; i += nt) invl[i] = c_inv101[i];
+  for (uint32_t i = me; i < PLK_GROUP_ORDER; i += nt)
+    expw[i] = c_exp[4 * i] | (uint32_t)c_exp[4 * i + 1] << 8 | (uint32_t)c_exp[4 * i + 2] << 16;
+  if (me < 2) s_cnt[me] = 0;
+  if (me == 0) { s_ng = PLK_GROUP_ORDER; s_nr = 0; s_ns = 0; }
+  __syncthreads();
+  const RawOps ops{invl};
+  for (uint32_t i = me; i < FS_N; i += nt) {
+    owner[i] = 0;
+    par[i] = (uint16_t)i;
+    const RawPt a = state_of(i);
+    const uint32_t lg = glog(a, ytab);
+    if (lg < PLK_GROUP_ORDER) gslot[lg] = i;            // delta = 0: slot = log
+    else lst[0][atomicAdd(&s_cnt[0], 1u)] = i | i << 14;
+  }
+  __syncthreads();
+  // block-wide barriers while many trajectories are live; once few are, wave 0 continues alone
+  // with wave-level ordering of its LDS traffic (the other waves wait at the barrier after the
+  // loop, so every barrier is reached by every wave)
+  bool solo = false;
+  auto sync = [&]() {
+    if (solo) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+      __syncthreads();
+    }
+  };
+  uint32_t cur = 0, delta = 0, step = 1;
+  for (uint64_t i = c0; i < c1; i++, step++) {
+    const uint32_t k = (uint32_t)((i - c0) % FC_TB);
+    if (k == 0) {            // stage the next terms: g1_mul(P_i, c_i) on raw bytes, and their logs
+      sync();
+      for (uint32_t j = me; j < FC_TB && i + j < c1; j += nt) {
+        const uint64_t q = i + j;
+        const RawPt t = ops.mulp(RawPt{pts[3 * q], pts[3 * q + 1], pts[3 * q + 2]}, sc[q]);
+        tt[j] = pk(t) | glog(t, ytab) << 24;
+      }
+      sync();
+    }
+    const uint32_t tv = tt[k];
+    const uint32_t tl = tv >> 24;
+    const RawPt t = upk(tv);
+    uint32_t nc = s_cnt[cur];
+    const uint32_t nr = s_nr;
+    if (tl < PLK_GROUP_ORDER) {
+      delta += tl;
+      if (delta >= PLK_GROUP_ORDER) delta -= PLK_GROUP_ORDER;
+    } else if (s_ng) {       // an irregular term: the symbolic group trajectories become concrete
+      for (uint32_t r = me; r < PLK_GROUP_ORDER; r += nt) {   // (nt = 64 once wave 0 is alone)
+        const uint32_t g = gslot[r];
+        if (g != FS_EMPTY) {
+          uint32_t e = r + delta;
+          if (e >= PLK_GROUP_ORDER) e -= PLK_GROUP_ORDER;
+          lst[cur][atomicAdd(&s_cnt[cur], 1u)] = (uint32_t)id_of(upk(expw[e])) | g << 14;
+          gslot[r] = FS_EMPTY;
+        }
+      }
+      sync();
+      if (me == 0) s_ng = 0;
+      nc = s_cnt[cur];
+    }
+    if (nc == 0 && nr == 0) continue;
+    // pass 1: apply the term; claim the resulting canonical states
+    for (uint32_t e = me; e < nc + nr; e += nt) {
+      uint32_t tid;
+      RawPt a;
+      if (e < nc) {
+        const uint32_t w = lst[cur][e];
+        tid = w >> 14;
+        a = state_of(w & 0x3FFFu);
+      } else {
+        tid = rawtid[e - nc];
+        a = upk(rawst[e - nc]);
+      }
+      const RawPt b = ops.addp(a, t);
+      const int s2 = id_of(b);
+      if (s2 >= 0) {
+        atomicMax(&owner[s2], step << 16 | (0xFFFFu - tid));
+        lst[cur][e] = (uint32_t)s2 | tid << 14;
+      } else {
+        const uint32_t j = atomicAdd(&s_ns, 1u);
+        if (j < 16) { stst[j] = pk(b); sttid[j] = tid; }
+        lst[cur][e] = ~0u;
+      }
+    }
+    sync();
+    // pass 2: losers merge into the owner; owners on group elements join the symbolic slots,
+    // the others go to the next list; raw results merge by bytes
+    if (me == 0) {
+      const uint32_t ns = s_ns < 16 ? s_ns : 16;
+      uint32_t kept = 0;
+      for (uint32_t j = 0; j < ns; j++) {
+        uint32_t q = 0;
+        while (q < kept && rawst[q] != stst[j]) q++;
+        if (q < kept) par[sttid[j]] = (uint16_t)rawtid[q];
+        else { rawst[kept] = stst[j]; rawtid[kept] = sttid[j]; kept++; }
+      }
+      s_nr = kept;
+      s_ns = 0;
+      s_cnt[cur] = 0;        // (this list is refilled by the next step's pass 2)
+    }
+    for (uint32_t e = me; e < nc + nr; e += nt) {
+      const uint32_t w = lst[cur][e];
+      if (w == ~0u) continue;
+      const uint32_t s2 = w & 0x3FFFu, tid = w >> 14;
+      const uint32_t win = 0xFFFFu - (owner[s2] & 0xFFFFu);
+      if (win != tid) { par[tid] = (uint16_t)win; continue; }
+      const uint32_t lg = glog(state_of(s2), ytab);
+      if (lg < PLK_GROUP_ORDER) {
+        const uint32_t r = lg >= delta ? lg - delta : lg + PLK_GROUP_ORDER - delta;
+        const uint32_t occ = gslot[r];
+        if (occ != FS_EMPTY) par[tid] = (uint16_t)occ;
+        else { gslot[r] = tid; atomicAdd(&s_ng, 1u); }
+      } else {
+        lst[cur ^ 1][atomicAdd(&s_cnt[cur ^ 1], 1u)] = w;
+      }
+    }
+    sync();
+    cur ^= 1;
+    if (!solo) {
+      // every wave reads the counts before wave 0 can change them again (the next step's
+      // materialisation appends before its first barrier): the decision is uniform
+      const bool few = s_cnt[cur] + s_ng + s_nr <= FC_SOLO;
+      __syncthreads();
+      if (few) {
+        if (me >= PLK_WAVE) break;
+        solo = true;
+        nt = PLK_WAVE;
+      }
+    }
+  }
+  __syncthreads();
+  nt = FC_T;
+  // (every wave: cur and delta as wave 0 left them)
+  if (me == 0) { s_cnt[2 + 0] = cur; s_cnt[2 + 1] = delta; }
+  __syncthreads();
+  cur = s_cnt[2];
+  delta = s_cnt[3];
+  // final state of every live trajectory (owner reused), then every start state through its parents
+  const uint32_t nc = s_cnt[cur], nr = s_nr;
+  for (uint32_t e = me; e < nc; e += nt) {
+    const uint32_t w = lst[cur][e];
+    owner[w >> 14] = pk(state_of(w & 0x3FFFu));
+  }
+  for (uint32_t r = me; r < PLK_GROUP_ORDER; r += nt)
+    if (gslot[r] != FS_EMPTY) owner[gslot[r]] = expw[r + delta < PLK_GROUP_ORDER ? r + delta : r + delta - PLK_GROUP_ORDER];
+  for (uint32_t e = me; e < nr; e += nt) owner[rawtid[e]] = rawst[e];
+  __syncthreads();
+  uint32_t* out = F + (size_t)blockIdx.x * FS_N;
+  for (uint32_t s0 = me; s0 < FS_N; s0 += nt) {
+    uint32_t r = s0;
+    while (par[r] != r) r = par[r];
+    out[s0] = owner[r];
+  }
+}
+
+// The chunk maps in order from the prefix state; a raw state at a chunk boundary re-folds that
+// chunk serially (one wave: terms by lane, the additions wave-uniform).
+__global__ __launch_bounds__(PLK_WAVE) void msm_fold_resolve_kernel(const uint8_t* __restrict__ pts,
+                                                                    const uint8_t* __restrict__ sc, uint64_t n,
+                                                                    uint32_t L, const FoldHdr* __restrict__ hdr,
+                                                                    const uint32_t* __restrict__ F, PlkMsmResult* res) {
+  __shared__ uint32_t invl[PLK_GF_P];
+  for (int i = threadIdx.x; i < PLK_GF_P; i += PLK_WAVE) invl[i] = c_inv101[i];
+  __syncthreads();
+  const uint64_t first = hdr->first;
+  const uint32_t pl = hdr->plog;
+  uint32_t st = c_exp[4 * pl] | (uint32_t)c_exp[4 * pl + 1] << 8 | (uint32_t)c_exp[4 * pl + 2] << 16;
+  const RawOps ops{invl}, uni{nullptr};
+  for (uint64_t c0 = first, b = 0; c0 < n; c0 += L, b++) {
+    const int id = id_of(upk(st));
+    if (id >= 0) {
+      st = (uint32_t)__builtin_amdgcn_readfirstlane((int)F[b * FS_N + (uint32_t)id]);
+      continue;
+    }
+    const uint64_t c1 = n - c0 < L ? n : c0 + L;
+    RawPt a = upk(st);
+    for (uint64_t j0 = c0; j0 < c1; j0 += PLK_WAVE) {
+      const uint64_t q = j0 + threadIdx.x;
+      const uint32_t tv = q < c1 ? pk(ops.mulp(RawPt{pts[3 * q], pts[3 * q + 1], pts[3 * q + 2]}, sc[q])) : 0u;
+      const uint32_t cnt = c1 - j0 < (uint64_t)PLK_WAVE ? (uint32_t)(c1 - j0) : (uint32_t)PLK_WAVE;
+      for (uint32_t jj = 0; jj < cnt; jj++) {
+        const RawPt au{(uint32_t)__builtin_amdgcn_readfirstlane((int)a.x), (uint32_t)__builtin_amdgcn_readfirstlane((int)a.y),
+                       (uint32_t)__builtin_amdgcn_readfirstlane((int)a.inf)};
+        a = uni.addp(au, upk((uint32_t)__builtin_amdgcn_readlane((int)tv, (int)jj)));
+      }
+    }
+    st = pk(a);
+  }
+  if (threadIdx.x != 0) return;
+  res->g1[0] = (uint8_t)(st & 0xFFu);
+  res->g1[1] = (uint8_t)((st >> 8) & 0xFFu);
+  res->g1[2] = (uint8_t)((st >> 16) & 0xFFu);
+  res->g1[3] = 0;
+}
+
 // Combine per-shard partial logs (e.g. after an RCCL all-reduce SUM of int32 logs) into
 // the final point: out = EXP[sum mod 102].
 __global__ void msm_combine_kernel(const uint32_t* __restrict__ logs, int count, uint8_t* out) {
@@ -687,10 +1009,35 @@ int plk_msm_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsm
   return plk_msm_batch_launch(d_pts, 0, d_sc, 0, n, 1, d_res, st);
 }
 
+// The exact raw fold (src/srs.h:59-66) for inputs with irregular encodings.  Short inputs: one
+// block (parallel canonical prefix, then the serial additions).  Long ones: the chunk maps
+// (msm_fold_*_kernel), whose scratch -- the chunk maps, 40.8 KB per chunk -- is stream-ordered
+// (hipMallocAsync / hipFreeAsync on the caller's stream).
+constexpr uint64_t FOLD_CHUNKED_MIN = 8192;
 int plk_msm_serial_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsmResult* d_res,
                           hipStream_t st) {
-  hipLaunchKernelGGL(msm_serial_fold_kernel, dim3(1), dim3(FOLD_T), 0, st, d_pts, d_sc, n, d_res);
-  PLK_HIP(hipGetLastError());
+  if (n < FOLD_CHUNKED_MIN) {
+    hipLaunchKernelGGL(msm_serial_fold_kernel, dim3(1), dim3(FOLD_T), 0, st, d_pts, d_sc, n, d_res);
+    PLK_HIP(hipGetLastError());
+    return PLK_OK;
+  }
+  // about one chunk per CU (one 150 KB workgroup each), 2048 .. 32768 terms per chunk
+  uint64_t L = (n + 255) / 256;
+  L = (L + 1023) & ~1023ull;
+  L = L < 2048 ? 2048 : (L > 32768 ? 32768 : L);
+  const uint64_t nch = (n + L - 1) / L;
+  const size_t ws = FC_HDR_BYTES + (size_t)nch * FS_N * 4;
+  void* w = nullptr;
+  PLK_HIP(hipMallocAsync(&w, ws, st));
+  FoldHdr* hdr = (FoldHdr*)w;
+  uint32_t* F = (uint32_t*)((uint8_t*)w + FC_HDR_BYTES);
+  hipLaunchKernelGGL(msm_fold_prefix_kernel, dim3(1), dim3(FOLD_T), 0, st, d_pts, d_sc, n, hdr);
+  hipLaunchKernelGGL(msm_fold_chunk_kernel, dim3((unsigned)nch), dim3(FC_T), 0, st, d_pts, d_sc, n, (uint32_t)L, hdr, F);
+  hipLaunchKernelGGL(msm_fold_resolve_kernel, dim3(1), dim3(PLK_WAVE), 0, st, d_pts, d_sc, n, (uint32_t)L, hdr, F,
+                     d_res);
+  const hipError_t le = hipGetLastError();
+  PLK_HIP(hipFreeAsync(w, st));
+  PLK_HIP(le);
   return PLK_OK;
 }
 

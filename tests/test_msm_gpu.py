@@ -96,32 +96,107 @@ def test_irregular_in_2_22_points(hip, oracle, where):
     assert hip.msm_g1(pts, sc) == oracle.msm(pts, sc)
 
 
-def test_irregular_first_of_2_22_is_bounded(hip, oracle):
-    """The worst case of the raw fold: the first of 2^22 points irregular, so every addition is
-    order-dependent.  The g1_mul terms are computed in parallel (15 waves) while one lane folds
-    (src/srs.h:59-66); the device fold must stay within a few times the reference's own CPU
-    time for this input (~0.63 s, gcc -O2) -- one lane doing whole g1_mul chains took seconds."""
+def _serial_dev(hip, pts, sc):
+    """plk_msm_g1_serial_dev (the exact raw fold) on device copies; returns (bytes, seconds)"""
     import time
     import torch
-    c = load_golden("msm.json")["large"][7]
-    pts, sc = gen.msm_inputs(c["seed"], c["n"], c["kind"])
-    pts = pts.copy()
-    pts[0] = (7, 7, 1)                                  # identity flag with coordinates
     dev = torch.device("cuda:0")
-    dp = torch.from_numpy(pts.reshape(-1).copy()).to(dev)
-    ds = torch.from_numpy(sc.copy()).to(dev)
+    dp = torch.from_numpy(np.ascontiguousarray(pts).reshape(-1).copy()).to(dev)
+    ds = torch.from_numpy(np.ascontiguousarray(sc).copy()).to(dev)
     res = torch.zeros(hip.MSM_RESULT_BYTES, dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream()
-    hip.msm_g1_serial_dev(dp, ds, c["n"], res, st)     # warm
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    hip.msm_g1_serial_dev(dp, ds, c["n"], res, st)
+    hip.msm_g1_serial_dev(dp, ds, sc.size, res, st)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print("serial fold, 2^22 points, irregular first: %.3f s" % dt)
     g = hip.MSM_G1_OFFSET
-    assert bytes(res[g:g + 3].cpu().numpy()) == oracle.msm(pts, sc)
-    assert dt < 2.5, dt
+    return bytes(res[g:g + 3].cpu().numpy()), dt
+
+
+def _raw_points(seed, n, frac_bad):
+    """subgroup points with a fraction replaced by raw byte triples of every irregular shape:
+    off-curve canonical coordinates, coordinates >= 101, flag bytes 1 / 2 / 255 with coordinates"""
+    pts, sc = gen.msm_inputs(seed, n, "bytes")
+    pts = pts.copy()
+    rng = np.random.default_rng(seed)
+    bad = rng.random(n) < frac_bad
+    m = int(bad.sum())
+    raw = rng.integers(0, 256, (m, 3)).astype(np.uint8)
+    shape = rng.integers(0, 4, m)
+    raw[shape == 0] %= 101
+    raw[shape == 0, 2] = 0
+    raw[shape == 1, 2] = 0
+    raw[shape == 2, 2] = rng.choice([1, 2, 255], int((shape == 2).sum()))
+    raw[shape == 3, 2] = 1
+    pts[bad] = raw
+    return pts, sc
+
+
+@pytest.mark.parametrize("n,frac", [(8192, 1.0), (9001, 0.01), (20000, 0.3), (65536, 0.001), (100003, 1.0),
+                                    (300000, 0.05)])
+def test_chunked_fold_vs_oracle(hip, oracle, n, frac):
+    """The chunked raw fold (msm_fold_*_kernel: every chunk a map over the 10,202 canonical
+    accumulator states, resolved in order) against the oracle's serial fold, from inputs that are
+    raw everywhere to a few irregular points; sizes on and off the chunk grid."""
+    pts, sc = _raw_points(n + int(frac * 1000), n, frac)
+    got, _ = _serial_dev(hip, pts, sc)
+    assert got == oracle.msm(pts, sc)
+    assert hip.msm_g1(pts, sc) == got
+
+
+@pytest.mark.parametrize("case", ["identity_runs", "raw_inf_runs", "zero_scalars", "offcurve_after_prefix"])
+def test_chunked_fold_state_edges(hip, oracle, case):
+    """Inputs that keep raw accumulator states alive across chunk boundaries (infinite terms
+    pass the accumulator through unchanged; a raw term on an infinite accumulator becomes it)
+    and a long canonical prefix before the first irregular point."""
+    n = 70000
+    pts, sc = gen.msm_inputs(77, n, "full")
+    pts, sc = pts.copy(), sc.copy()
+    if case == "identity_runs":       # raw (coordinates >= 101) term, then long runs of identities
+        pts[::5000] = (200, 150, 0)
+        sc[::5000] = 1
+        for s0 in range(1, n, 5000):
+            pts[s0:s0 + 3000] = (0, 0, 1)
+    elif case == "raw_inf_runs":      # flagged points with coordinates, scalar 1: terms are the raw bytes
+        pts[1::3] = (9, 250, 1)
+        sc[1::3] = 1
+        pts[2::7] = (0, 0, 1)
+    elif case == "zero_scalars":      # irregular points whose terms are the identity (scalar 0)
+        pts[::2] = (7, 7, 0)
+        sc[::2] = 0
+    else:
+        pts[n - 20000] = (3, 3, 0)
+        sc[n - 20000] = 2
+    got, _ = _serial_dev(hip, pts, sc)
+    assert got == oracle.msm(pts, sc), case
+
+
+@pytest.mark.parametrize("kind", ["first_flagged", "all_raw"])
+def test_irregular_2_22_beats_reference_cpu(hip, oracle, kind):
+    """The worst cases of the raw fold at 2^22 points -- the first point irregular, so every
+    addition is order-dependent, and every point a raw byte triple -- must finish faster than
+    the reference's own srs_eval_at_s (oracle/_ref: the unmodified reference, gcc -O2) on this
+    host for the same input, and give its bytes."""
+    from pyoracle import Reference
+    c = load_golden("msm.json")["large"][7]
+    if kind == "first_flagged":
+        pts, sc = gen.msm_inputs(c["seed"], c["n"], c["kind"])
+        pts = pts.copy()
+        pts[0] = (7, 7, 1)                              # identity flag with coordinates
+    else:
+        pts, sc = _raw_points(99, c["n"], 1.0)
+    _serial_dev(hip, pts[:20000], sc[:20000])           # warm
+    got, dt = _serial_dev(hip, pts, sc)
+    assert Reference.available(), "oracle/_ref/libplonkref.so missing (built where /root/reference exists)"
+    import time
+    R = Reference()
+    t0 = time.perf_counter()
+    want = R.msm(pts, sc)
+    ref_s = time.perf_counter() - t0
+    print("raw fold 2^22 (%s): device %.4f s, reference CPU %.3f s" % (kind, dt, ref_s))
+    assert got == want
+    assert dt < ref_s, (dt, ref_s)
 
 
 def test_srs_eval_degree_check(hip):
