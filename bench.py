@@ -299,7 +299,7 @@ def components(torch, hip, dev, st, want):
     out = {}
     if "msm" in want:
         out.update(msm_components(torch, hip, dev, st))
-        out["msm_2^22_host_call_devices"] = msm_host_devices_component(torch, hip, dev)
+        out["host_call_msm_2^22_devices"] = msm_host_devices_component(torch, hip, dev)
     if "ntt" in want:
         out.update(ntt_components(torch, hip, dev, st))
     if "polymul" in want:
@@ -472,25 +472,50 @@ def polymul_components(torch, hip, dev, st):
                                                           "SURVEY 8(d): la + lb + (la + lb - 1) bytes of HF")}
     # three 2^20-point transforms over F29 (a and b forward, the product inverse): 3 x 2^19 x 20
     # butterflies
-    bfly = butterfly_roofline(3 * (1 << 19) * 20, avg, "f29_dif_Gbfly_s")
+    bfly = butterfly_roofline(3 * (1 << 19) * 20, avg, "f29_dif_Gbfly_s",
+                              mix=[("f29_dif", 2 / 3), ("f29_dit", 1 / 3)])
     if bfly:
         out["poly_mul_2^19x2^19"]["roofline_butterfly"] = bfly
     return out
 
 
-def butterfly_roofline(bfly, ms, key):
-    """Compute roofline of an NTT component: radix-2 butterflies / time against the butterfly peak
-    measured by tools/bfly_peak.hip (the engine's own formulas in registers, no memory; committed
-    in profiles/r02_bfly_peak.json -- a peak, like the HBM spec peak, not a timing of this run)."""
+# Integer-VALU instruction mix of one radix-2 butterfly as the engine compiles it (ntt_wave.hip
+# F29 / FBB policies, plk_device.h primitives; counted in the gfx950 ISA): v_mad_u64_u32 and
+# 32-bit VALU ops (add / sub / min / mul_lo).  Issue rates measured by tools/isa_clock.hip at
+# 8 waves per SIMD: 4.5 cycles per v_mad_u64_u32 and 4.2 per 32-bit op per wave-instruction.
+ISA_BFLY = {"f29_dif": (3, 3), "f29_dit": (2, 5), "bb_dif": (2, 8), "bb_dit": (2, 9)}
+ISA_CYC = (4.5, 4.2)
+CU_SIMDS, CLOCK_HZ = 1024, 2.4e9   # 256 CUs x 4 SIMDs; MI355X peak engine clock (MI355X_MICROARCH.md)
+
+
+def isa_bound_gbfly(kind):
+    """hardware bound: every SIMD issuing the butterfly's instruction mix back to back"""
+    mads, ops = ISA_BFLY[kind]
+    cyc = mads * ISA_CYC[0] + ops * ISA_CYC[1]
+    return CU_SIMDS * 64 * CLOCK_HZ / cyc / 1e9
+
+
+def butterfly_roofline(bfly, ms, key, mix=None):
+    """Compute roofline of an NTT component: radix-2 butterflies / time against (a) the butterfly
+    peak measured by tools/bfly_peak.hip (the engine's own formulas in registers, no memory;
+    committed in profiles/r02_bfly_peak.json -- a peak, like the HBM spec peak, not a timing of
+    this run) and (b) the ISA bound of the same butterflies (isa_bound_gbfly; mix = [(kind,
+    share)] for a product's forward DIF + inverse DIT transforms)."""
     try:
         with open(os.path.join(ROOT, "profiles", "r02_bfly_peak.json")) as f:
             pk = json.loads([l for l in f if l.startswith("{")][0])
     except (OSError, IndexError, ValueError):
         return None
     rate = bfly / (ms * 1e-3) / 1e9
+    mix = mix or [({"f29_dif_Gbfly_s": "f29_dif", "bb_dif_Gbfly_s": "bb_dif"}[key], 1.0)]
+    # time-weighted: a share s of the butterflies at bound b costs s / b
+    isa = 1.0 / sum(sh / isa_bound_gbfly(kind) for kind, sh in mix)
     return {"bound": "valu", "achieved": round(rate, 1), "peak": pk[key], "unit": "Gbutterfly/s",
             "frac": round(rate / pk[key], 4), "butterflies": int(bfly),
-            "peak_source": "profiles/r02_bfly_peak.json (%s)" % key}
+            "isa_bound": round(isa, 1), "frac_of_isa_bound": round(rate / isa, 4),
+            "isa_mix": {k: {"v_mad_u64_u32": ISA_BFLY[k][0], "valu32": ISA_BFLY[k][1], "share": sh} for k, sh in mix},
+            "peak_source": "profiles/r02_bfly_peak.json (%s); isa_bound: instruction mix x tools/isa_clock.hip issue "
+                           "rates x 1024 SIMDs x 2.4 GHz" % key}
 
 
 def polyops_components(torch, hip, dev, st):

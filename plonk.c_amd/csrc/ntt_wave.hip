@@ -119,6 +119,21 @@ struct FBB {
     u = bb::madd(a, xw);
     x = bb::msub(a, xw);
   }
+  // stage 0 (twiddle 1): DIF whose outputs go to a column multiply or the stored result; DIT of
+  // inputs already < p (what a multiply by one would return)
+  __device__ static __forceinline__ void dif1(uint32_t& u, uint32_t& x) {
+    const uint32_t a = u, b = x;
+    u = bb::madd(a, b);
+    x = bb::msub(a, b);   // (reduced: a lo = 0 pass stores it as it is)
+  }
+  __device__ static __forceinline__ void dit1(uint32_t& u, uint32_t& x, bool) {
+    const uint32_t a = u, b = x;
+    u = bb::madd(a, b);
+    x = bb::msub(a, b);
+  }
+  __device__ static __forceinline__ void difp(uint32_t& u, uint32_t& x, uint32_t w, uint32_t, bool red) {
+    dif(u, x, w, red);
+  }
   __device__ static __forceinline__ uint32_t mul(uint32_t a, uint32_t b) { return bb::mmul(a, b); }
   __device__ static __forceinline__ uint32_t pmul(uint32_t a, uint32_t b) { return bb::mmul(a, b); }
   // a + b + c of center outputs (sum groups; c = 0 when absent)
@@ -158,6 +173,30 @@ struct F29 {
     const uint32_t xw = f29::mmul(x, w);         // any u32 x: [0, 2p)
     const uint32_t a = red ? red4(u) : u;        // a < 6p (unreduced) or < 4p
     u = a + xw;                                  // < a's bound + 2p <= 8p
+    x = a + f29::P2 - xw;
+  }
+  // the same with the twiddle's complement p - w read from the table (no subtraction)
+  __device__ static __forceinline__ void difp(uint32_t& u, uint32_t& x, uint32_t w, uint32_t pw, bool red) {
+    const uint32_t a = u, b = x;
+    const uint64_t t = (uint64_t)a * w + (uint64_t)b * pw;
+    const uint32_t m = (uint32_t)t * f29::PINV;
+    x = (uint32_t)((t + (uint64_t)m * f29::P) >> 32);
+    const uint32_t s = a + b;
+    u = red ? red4(s) : s;
+  }
+  // stage 0 (twiddle 1) of a forward pass whose outputs go to a column multiply (any u32) or to
+  // canon ([0, 8p)): a, b < 4p -> both outputs < 8p, no multiply, no reduction
+  __device__ static __forceinline__ void dif1(uint32_t& u, uint32_t& x) {
+    const uint32_t a = u, b = x;
+    u = a + b;
+    x = a + 4 * f29::P - b;
+  }
+  // stage 0 of an inverse pass: its x inputs are < 2p (a pointwise product, a column
+  // pre-multiply or canonical data), which is what the multiply by one would have returned
+  __device__ static __forceinline__ void dit1(uint32_t& u, uint32_t& x, bool red) {
+    const uint32_t xw = x;
+    const uint32_t a = red ? red4(u) : u;
+    u = a + xw;
     x = a + f29::P2 - xw;
   }
   __device__ static __forceinline__ uint32_t mul(uint32_t a, uint32_t b) { return f29::mmul(a, b); }
@@ -228,8 +267,11 @@ struct Eng {
     return base(tid, lbq(Q, inv), colsq(Q, inv));
   }
 
-  // the radix-2 stages of round Q, in registers
-  template <int Q, bool INV>
+  // the radix-2 stages of round Q, in registers.  Stage 0 has twiddle 1: DIT always skips the
+  // multiply there (its x inputs are < 2p, F::dit1), DIF when TRIV0 (a forward pass whose
+  // outputs go to the column multiply or the canonical store, F::dif1).  PW: the table holds
+  // {w, p - w} pairs (F29 DIF without the subtraction).
+  template <int Q, bool INV, bool PW = false, bool TRIV0 = false>
   __device__ static __forceinline__ void round(uint32_t (&v)[E], uint32_t b, const uint32_t* Tsm) {
     if (PLK_NTT_DIAG & 1) return;
     constexpr int LB = lbq(Q, INV), SL = s_lo(Q, INV), SH = s_hi(Q, INV);
@@ -246,12 +288,22 @@ struct Eng {
         // conflicts) and the address is linear in the register index, so it folds into the
         // ds_read offset.  (A padded W13 table read at W13[rr << (12 - s)] halved the LDS but
         // needed ~4 VALU of address math per butterfly.)
-        const uint32_t w = Tsm[(1u << s) + rr];
         // lazy-reduction flags (F29), compile-time after unrolling: DIF reduces u when the
         // pair were u outputs of the previous stage (its bit q+1 of k is 0; unknown for a
         // round's first stage); DIT reduces the a operand on the round's even stages (bound
         // 8p assumed on entry, +2p per stage)
         const bool red = INV ? (i % 2 == 0) : (i == 0 || !((k >> (q + 1)) & 1));
+        if (s == 0 && (INV || TRIV0)) {
+          if (INV) F::dit1(v[k], v[k | (1 << q)], red);
+          else F::dif1(v[k], v[k | (1 << q)]);
+          continue;
+        }
+        if constexpr (PW) {
+          const uint2 wp = reinterpret_cast<const uint2*>(Tsm)[(1u << s) + rr];
+          F::difp(v[k], v[k | (1 << q)], wp.x, wp.y, red);
+          continue;
+        }
+        const uint32_t w = Tsm[(1u << s) + rr];
         if (!INV) F::dif(v[k], v[k | (1 << q)], w, red);
         else F::dit(v[k], v[k | (1 << q)], w, red);
       }
@@ -360,18 +412,24 @@ struct Eng {
                                                   int lbt) {
     if (PLK_NTT_DIAG & 2) return;
     if (PLK_NTT_SWZ && SWZ && swz_ok(Q, INV)) {
-      // e = base | k << lb (disjoint bits) and h is linear: h(e) = h(base) ^ h(k << lb)
-      const uint32_t xw = bf ^ swz_h<Q, INV>(bf), xr = bt ^ swz_h<Q, INV>(bt);
+      // e = base | k << lb (disjoint bits) and h is linear: h(e) = h(base) ^ h(k << lb).  h only
+      // moves bits < 5 and the bits >= 5 of k << lb are disjoint from base's, so the word is
+      // (xw ^ lo_k) + hi_k: one XOR with a constant (none when lo_k = 0) and the rest in the
+      // ds_write / ds_read offset, on byte addresses (no per-element shift)
+      const uint32_t xw4 = (bf ^ swz_h<Q, INV>(bf)) << 2, xr4 = (bt ^ swz_h<Q, INV>(bt)) << 2;
+      char* bb = reinterpret_cast<char*>(buf);
 #pragma unroll
       for (int k = 0; k < E; k++) {
         const uint32_t ek = (uint32_t)k << lbf;
-        buf[xw ^ ek ^ swz_h<Q, INV>(ek)] = v[k];
+        const uint32_t lo = ((ek & 31u) ^ swz_h<Q, INV>(ek)) << 2, hi = (ek & ~31u) << 2;
+        *reinterpret_cast<uint32_t*>(bb + (lo ? (xw4 ^ lo) : xw4) + hi) = v[k];
       }
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < E; k++) {
         const uint32_t ek = (uint32_t)k << lbt;
-        v[k] = buf[xr ^ ek ^ swz_h<Q, INV>(ek)];
+        const uint32_t lo = ((ek & 31u) ^ swz_h<Q, INV>(ek)) << 2, hi = (ek & ~31u) << 2;
+        v[k] = *reinterpret_cast<const uint32_t*>(bb + (lo ? (xr4 ^ lo) : xr4) + hi);
       }
       if (!DBUF) __syncthreads();
       return;
@@ -397,14 +455,14 @@ struct Eng {
   // last round on exit.  xc selects the exchange buffer (it counts exchanges).
   // SWZ: the swizzled exchange layout where it is conflict-free (the center kernel passes false:
   // it has no VGPRs to spare for the two extra base registers)
-  template <bool INV, bool SWZ = true, int Q = 0>
+  template <bool INV, bool SWZ = true, bool PW = false, bool TRIV0 = false, int Q = 0>
   __device__ static __forceinline__ void pass(uint32_t (&v)[E], uint32_t tid, uint32_t* bufs, int xc,
                                               const uint32_t* Tsm) {
-    round<Q, INV>(v, base_q<Q>(tid, INV), Tsm);
+    round<Q, INV, PW, TRIV0>(v, base_q<Q>(tid, INV), Tsm);
     if constexpr (Q + 1 < NR) {
       exchange<Q, INV, SWZ>(v, bufs + (DBUF ? ((xc + Q) & 1) * BUF : 0), base_q<Q>(tid, INV), lbq(Q, INV),
                             base_q<Q + 1>(tid, INV), lbq(Q + 1, INV));
-      pass<INV, SWZ, Q + 1>(v, tid, bufs, xc, Tsm);
+      pass<INV, SWZ, PW, TRIV0, Q + 1>(v, tid, bufs, xc, Tsm);
     }
   }
 
@@ -467,6 +525,19 @@ __device__ __forceinline__ void load_pass_tw(uint32_t* Tsm, const uint32_t* smal
   }
 }
 
+// the same as {w, p - w} pairs (F29 forward passes)
+template <int M, int NT>
+__device__ __forceinline__ void load_pass_tw_pairs(uint32_t* Tsm, const uint32_t* small) {
+#pragma unroll
+  for (int i = 0; i < ((1 << M) + NT - 1) / NT; i++) {
+    const int j = i * NT + (int)threadIdx.x;
+    if (j < (1 << M)) {
+      const uint32_t w = small[j];
+      reinterpret_cast<uint2*>(Tsm)[j] = make_uint2(w, f29::P - w);
+    }
+  }
+}
+
 }  // namespace
 
 // Forward (DIF) pass over a batch's distinct arrays (blockIdx.y = array), u32 in place, or
@@ -477,7 +548,8 @@ template <int TB, int R, int M, bool FROM_U8, class F, bool COLT = false>
 __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, WTw tw) {
   using G = Eng<TB, R, M, F>;
   static_assert(G::NT == wt_nt(TB), "tile block size");
-  __shared__ uint32_t Tsm[1 << M];
+  constexpr bool PW = F::ADIC == f29::TWO_ADICITY;   // {w, p - w} pairs (F29's lazy DIF)
+  __shared__ __attribute__((aligned(16))) uint32_t Tsm[(PW ? 2 : 1) << M];
   __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
@@ -527,13 +599,14 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
   }
   __shared__ uint32_t lut[FROM_U8 && PLK_NTT_BYTE_LUT ? 256 : 1];
   if (FROM_U8 && PLK_NTT_BYTE_LUT && tid < 256) lut[tid] = F::byte_val(tid);
-  load_pass_tw<M, G::NT>(Tsm, tw.small);
+  if constexpr (PW) load_pass_tw_pairs<M, G::NT>(Tsm, tw.small);
+  else load_pass_tw<M, G::NT>(Tsm, tw.small);
   __syncthreads();
   if constexpr (FROM_U8 && PLK_NTT_BYTE_LUT) {
 #pragma unroll
     for (int k = 0; k < G::E; k++) v[k] = lut[v[k]];
   }
-  G::template pass<false>(v, tid, bufs, 0, Tsm);
+  G::template pass<false, true, PW, true>(v, tid, bufs, 0, Tsm);
 #pragma unroll
   for (int k = 0; k < G::E; k++) {
     uint32_t x = v[k];
@@ -608,7 +681,6 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
     const uint32_t e = b0 + ((uint32_t)k << L0);
     const uint32_t o = G::template toff_k<0, true>(p, o0, b0, k);
     v[k] = dt[o];
-    if (s1) v[k] = F::sum(v[k], s1t[o], s2 ? s2t[o] : 0u);   // uniform branch
     if (G::HIGH) {
       if constexpr (COLT) {
         cl[k] = colt[o];
@@ -618,6 +690,17 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
         ch[k] = tw.hi[ex >> 12];
       }
     }
+  }
+  if (s1) {   // a sum group's leader (uniform): its members' center outputs, all loads in flight
+    uint32_t a1[G::E], a2[G::E];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) {
+      const uint32_t o = G::template toff_k<0, true>(p, o0, b0, k);
+      a1[k] = s1t[o];
+      a2[k] = s2 ? s2t[o] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < G::E; k++) v[k] = F::sum(v[k], a1[k], a2[k]);
   }
   load_pass_tw<M, G::NT>(Tsm, tw.small);
   if (G::HIGH) {
@@ -636,20 +719,27 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   uint32_t last = 0;      // 1 + the largest index this thread left a non-zero byte at
   const uint32_t N = 1u << p.k;   // (k <= 27: every index fits 32 bits)
   const uint32_t lim = out_len < N ? (uint32_t)out_len : N;
+  const uint32_t ntop = (uint32_t)jb.ntop;   // (read once: the byte stores below may alias the job table)
+  if constexpr (!TO_U8) {
 #pragma unroll
-  for (int k = 0; k < G::E; k++) {
-    const uint32_t o = G::template toff_k<G::NR - 1, true>(p, of, bf, k);
-    if (!TO_U8) {
-      dt[o] = F::canon(v[k]);   // (the standalone inverse's last pass; poly_mul's 3-pass middle one)
-    } else {
-      // poly_mul runs its inverse with the FORWARD roots (no inverse table in LDS): that
-      // yields N c[-idx mod N], so the coefficient lands at the negated position
-      const uint32_t j = (N - ((uint32_t)tb + o)) & (N - 1);
-      if (j < lim) {
-        const uint32_t r = F::out17(v[k], ninv);
-        out8[j] = (uint8_t)r;
-        if (j < (uint32_t)jb.ntop) wrapped |= 1u << k;
-        else if (r) last = max(last, j + 1u);
+    for (int k = 0; k < G::E; k++)   // (the standalone inverse's last pass; poly_mul's 3-pass middle one)
+      dt[G::template toff_k<G::NR - 1, true>(p, of, bf, k)] = F::canon(v[k]);
+  } else {
+    // poly_mul runs its inverse with the FORWARD roots (no inverse table in LDS): that yields
+    // N c[-idx mod N], so the coefficient lands at the negated position.  Every byte is computed
+    // before the first store (the stores then issue back to back).
+    uint32_t jj[G::E], rr[G::E];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) {
+      jj[k] = (N - ((uint32_t)tb + G::template toff_k<G::NR - 1, true>(p, of, bf, k))) & (N - 1);
+      rr[k] = F::out17(v[k], ninv);
+    }
+#pragma unroll
+    for (int k = 0; k < G::E; k++) {
+      if (jj[k] < lim) {
+        out8[jj[k]] = (uint8_t)rr[k];
+        if (jj[k] < ntop) wrapped |= 1u << k;
+        else if (rr[k]) last = max(last, jj[k] + 1u);
       }
     }
   }
