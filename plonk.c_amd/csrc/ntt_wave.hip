@@ -69,6 +69,25 @@ constexpr int WT_MAX_HI13 = 10;                // ... with 2^13 tiles
 
 __device__ __forceinline__ int wphys(int e) { return e + (e >> 5); }
 
+// A tile's words (or bytes) through a buffer resource on its uniform base: every access is one
+// 32-bit VGPR offset against scalar registers (no 64-bit address per element; offsets stay below
+// 2^30 bytes), and accesses at or past `bytes` are dropped / read 0 -- the byte operands' zero
+// padding and the trimmed byte outputs without a per-element branch.
+struct TileBuf {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ explicit TileBuf(const void* base, uint32_t bytes = 0x7FFFFFF0u)
+      : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)(bytes < 0x7FFFFFF0u ? bytes : 0x7FFFFFF0u),
+                                            0x00020000)) {}
+  __device__ __forceinline__ uint32_t ld(uint32_t off) const { return __builtin_amdgcn_raw_buffer_load_b32(r, off << 2, 0, 0); }
+  __device__ __forceinline__ void st(uint32_t off, uint32_t v) const {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, off << 2, 0, 0);
+  }
+  __device__ __forceinline__ uint32_t ldb(uint32_t off) const { return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0); }
+  __device__ __forceinline__ void stb(uint32_t off, uint32_t v) const {
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, off, 0, 0);
+  }
+};
+
 struct WPass {
   int k;    // log2 N
   int lo;   // lowest bit of the pass
@@ -565,20 +584,22 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
   const uint32_t b0 = G::template base_q<0>(tid, false);
   const uint32_t o0 = G::toff(p, b0);
   uint32_t v[G::E];
+  const TileBuf bd(dt);
   if constexpr (FROM_U8) {
-    // raw bytes now (0 past the operand), their values through an LDS table after the barrier
-    const uint8_t* st = s8 + tb;
+    // raw bytes now (0 past the operand: the buffer's range ends there), their values through
+    // an LDS table after the barrier
     const uint32_t lim = ls > tb ? (uint32_t)(ls - tb < 0xFFFFFFFFull ? ls - tb : 0xFFFFFFFFull) : 0u;
+    const TileBuf bs(s8 + tb, lim);
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
       const uint32_t o = G::template toff_k<0, false>(p, o0, b0, k);
       if ((PLK_NTT_DIAG & 8) && k > 0) { v[k] = (v[0] + k) & 0xFFu; continue; }
-      v[k] = o < lim ? st[o] : 0u;
+      v[k] = bs.ldb(o);
       if (!PLK_NTT_BYTE_LUT) v[k] = F::byte_val(v[k]);
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < G::E; k++) v[k] = dt[G::template toff_k<0, false>(p, o0, b0, k)];
+    for (int k = 0; k < G::E; k++) v[k] = bd.ld(G::template toff_k<0, false>(p, o0, b0, k));
   }
   // column factor table words of the elements this thread stores (HIGH passes)
   constexpr int LF = G::lbq(G::NR - 1, false);
@@ -589,7 +610,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
       if constexpr (COLT) {
-        cl[k] = (PLK_NTT_DIAG & 16) ? 0x12345u + k : colt[G::template toff_k<G::NR - 1, false>(p, of, bf, k)];
+        cl[k] = (PLK_NTT_DIAG & 16) ? 0x12345u + k : TileBuf(colt).ld(G::template toff_k<G::NR - 1, false>(p, of, bf, k));
       } else {
         const uint32_t ex = G::col_exp(p, tile, bf + ((uint32_t)k << LF));
         cl[k] = tw.lo[ex & 4095u];
@@ -613,7 +634,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
     if constexpr (G::HIGH && COLT) x = F::mul(x, cl[k]);
     else if constexpr (G::HIGH) x = F::mul(x, F::colf(cl[k], ch[k]));
     else x = F::canon(x);   // the lo = 0 pass is the last one of a standalone transform
-    dt[G::template toff_k<G::NR - 1, false>(p, of, bf, k)] = x;
+    bd.st(G::template toff_k<G::NR - 1, false>(p, of, bf, k), x);
   }
 }
 
@@ -623,10 +644,13 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
 // with i >= la - ntop + j (ntop - j <= 16 of them): computed from the bytes by the few threads
 // that hold such j, after the pass's stores (a rare path outside the unrolled store loop).
 // Returns 1 + the largest index it left a non-zero byte at (0: none).
+// (rr: the bytes this thread's pass stored, c[j] + c[N + j] mod 17 at the wrapped positions)
 template <class G>
 __device__ __forceinline__ uint32_t wrap_fix(const WJob& jb, uint32_t wrapped, const WPass& p, uint32_t tile,
-                                          uint32_t bf, int LF, uint64_t N) {
+                                          uint32_t bf, int LF, uint64_t N, const uint32_t* rr) {
   uint32_t last = 0;
+  // the pass's own byte stores at these positions complete before they are overwritten here
+  __builtin_amdgcn_s_waitcnt(0);
   for (int k = 0; k < G::E; k++) {
     if (!(wrapped >> k & 1)) continue;
     const uint64_t idx = G::index(p, tile, bf + ((uint32_t)k << LF));
@@ -638,7 +662,7 @@ __device__ __forceinline__ uint32_t wrap_fix(const WJob& jb, uint32_t wrapped, c
       for (uint64_t i = jb.la - (uint64_t)jb.ntop + j; i < jb.la; i++) s += (a[i] % 17u) * (b[N + j - i] % 17u);
     }
     s %= 17u;
-    const uint32_t lo = (jb.out8[j] + 17u - s) % 17u;
+    const uint32_t lo = (rr[k] + 17u - s) % 17u;
     jb.out8[j] = (uint8_t)lo;
     jb.out8[N + j] = (uint8_t)s;
     if (lo) last = max(last, (uint32_t)j + 1u);
@@ -676,14 +700,15 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   constexpr int L0 = G::lbq(0, true);
   uint32_t v[G::E];
   uint32_t cl[G::HIGH ? G::E : 1], ch[G::HIGH && !COLT ? G::E : 1];
+  const TileBuf bd(dt);
 #pragma unroll
   for (int k = 0; k < G::E; k++) {
     const uint32_t e = b0 + ((uint32_t)k << L0);
     const uint32_t o = G::template toff_k<0, true>(p, o0, b0, k);
-    v[k] = dt[o];
+    v[k] = bd.ld(o);
     if (G::HIGH) {
       if constexpr (COLT) {
-        cl[k] = colt[o];
+        cl[k] = TileBuf(colt).ld(o);
       } else {
         const uint32_t ex = G::col_exp(p, tile, e);   // roots of tw (inverse or forward)
         cl[k] = tw.lo[ex & 4095u];
@@ -696,8 +721,8 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
       const uint32_t o = G::template toff_k<0, true>(p, o0, b0, k);
-      a1[k] = s1t[o];
-      a2[k] = s2 ? s2t[o] : 0u;
+      a1[k] = TileBuf(s1t).ld(o);
+      a2[k] = s2 ? TileBuf(s2t).ld(o) : 0u;
     }
 #pragma unroll
     for (int k = 0; k < G::E; k++) v[k] = F::sum(v[k], a1[k], a2[k]);
@@ -723,11 +748,13 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   if constexpr (!TO_U8) {
 #pragma unroll
     for (int k = 0; k < G::E; k++)   // (the standalone inverse's last pass; poly_mul's 3-pass middle one)
-      dt[G::template toff_k<G::NR - 1, true>(p, of, bf, k)] = F::canon(v[k]);
+      bd.st(G::template toff_k<G::NR - 1, true>(p, of, bf, k), F::canon(v[k]));
   } else {
     // poly_mul runs its inverse with the FORWARD roots (no inverse table in LDS): that yields
     // N c[-idx mod N], so the coefficient lands at the negated position.  Every byte is computed
     // before the first store (the stores then issue back to back).
+    // (the buffer's range is the output length: bytes at or past it are dropped by the store)
+    const TileBuf bo(out8, lim);
     uint32_t jj[G::E], rr[G::E];
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
@@ -736,14 +763,14 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
     }
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
-      if (jj[k] < lim) {
-        out8[jj[k]] = (uint8_t)rr[k];
-        if (jj[k] < ntop) wrapped |= 1u << k;
-        else if (rr[k]) last = max(last, jj[k] + 1u);
-      }
+      bo.stb(jj[k], rr[k]);
+      const bool in = jj[k] < lim;
+      wrapped |= (in && jj[k] < ntop) ? 1u << k : 0u;
+      last = max(last, (in && jj[k] >= ntop && rr[k]) ? jj[k] + 1u : 0u);
     }
+    if (wrapped) last = max(last, wrap_fix<G>(jb, wrapped, p, tile, bf, LF, 1ull << p.k, rr));
   }
-  if (TO_U8 && wrapped) last = max(last, wrap_fix<G>(jb, wrapped, p, tile, bf, LF, 1ull << p.k));
+
   // Trimmed length (src/poly.h:20-38).  The top coefficient of a single product is
   // a[la-1] b[lb-1] mod 17 (one term, wrapped or not); when it is non-zero -- operands with
   // non-zero leading bytes, the usual case -- the length is la + lb - 1 and one store says so.
