@@ -537,10 +537,11 @@ __device__ __forceinline__ uint32_t block_tile() {
 // the pass's stage twiddles into LDS: the first 2^M entries of the table T
 template <int M, int NT>
 __device__ __forceinline__ void load_pass_tw(uint32_t* Tsm, const uint32_t* small) {
+  const TileBuf bs(small);   // (32-bit offsets: nothing 64-bit for the compiler to hoist and spill)
 #pragma unroll
   for (int i = 0; i < ((1 << M) + NT - 1) / NT; i++) {
     const int j = i * NT + (int)threadIdx.x;
-    if (j < (1 << M)) Tsm[j] = small[j];
+    if (j < (1 << M)) Tsm[j] = bs.ld((uint32_t)j);
   }
 }
 
@@ -551,7 +552,7 @@ __device__ __forceinline__ void load_pass_tw_pairs(uint32_t* Tsm, const uint32_t
   for (int i = 0; i < ((1 << M) + NT - 1) / NT; i++) {
     const int j = i * NT + (int)threadIdx.x;
     if (j < (1 << M)) {
-      const uint32_t w = small[j];
+      const uint32_t w = TileBuf(small).ld((uint32_t)j);
       reinterpret_cast<uint2*>(Tsm)[j] = make_uint2(w, f29::P - w);
     }
   }
@@ -813,22 +814,19 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB), items = tiles * nitems_jobs;
   // trimmed-length words of the jobs that want one: zeroed here, before the last inverse pass
   if (blockIdx.x == 0 && tid < nitems_jobs && jobs.j[tid].nz) *jobs.j[tid].nz = 0u;
-  bool first = true;
+  // the twiddle table first (a "first item" flag inside the loop had the compiler hoist the
+  // table's addresses out of the loop and spill them)
+  load_pass_tw<TB, G::NT>(Tlds, twf.small);
   for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
     const uint32_t job = it / tiles, tile = it - job * tiles;
-    const uint32_t* d0 = jobs.j[job].A;
-    const uint32_t* d1 = jobs.j[job].B;
-    uint32_t* dc = jobs.j[job].C;
+    // (the lo = 0 pass: a tile is 2^TB consecutive words; 32-bit offsets from its base)
+    const uint64_t tb = (uint64_t)tile << TB;
+    const TileBuf b_a(jobs.j[job].A + tb), b_b(jobs.j[job].B + tb), b_c(jobs.j[job].C + tb);
     uint32_t va[G::E], vb[G::E];
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
-      const uint64_t idx = G::index(p, tile, b0 + ((uint32_t)k << L0));
-      va[k] = d0[idx];
-      vb[k] = d1[idx];
-    }
-    if (first) {
-      load_pass_tw<TB, G::NT>(Tlds, twf.small);
-      first = false;
+      va[k] = b_a.ld(b0 + ((uint32_t)k << L0));
+      vb[k] = b_b.ld(b0 + ((uint32_t)k << L0));
     }
     __syncthreads();
     if (!jobs.j[job].afix) G::template pass<false, false>(va, tid, bufs, 0, Tf);
@@ -839,7 +837,7 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
     for (int k = 0; k < G::E; k++) va[k] = F::pmul(va[k], vb[k]);
     G::template pass<true, false>(va, tid, bufs, 2 * G::XCH, Tf);
 #pragma unroll
-    for (int k = 0; k < G::E; k++) dc[G::index(p, tile, bf + ((uint32_t)k << LF))] = va[k];
+    for (int k = 0; k < G::E; k++) b_c.st(bf + ((uint32_t)k << LF), va[k]);
   }
 }
 
