@@ -18,6 +18,9 @@ for step in "$@"; do
     nttpmc) timeout -k 10 600 ./tools/ntt_pmc_r3.sh 20 > gpurun_out/r3_nttpmc.log 2>&1; ok $? nttpmc; cat gpurun_out/ntt_pmc/summary.txt | head -60 ;;
     bench) timeout -k 10 400 python bench.py > gpurun_out/r3_bench.json 2> gpurun_out/r3_bench.err; ok $? bench ;;
     prove) timeout -k 10 300 python tools/prove_bench.py 20 > gpurun_out/r3_prove.json 2>&1; ok $? prove; cat gpurun_out/r3_prove.json ;;
+    proveprof) rm -rf gpurun_out/pp; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pp -o run -- python3 tools/prove_bench.py 20 > gpurun_out/r3_pp.json 2>&1; ok $? proveprof
+         python3 tools/prove_breakdown.py gpurun_out/pp/run_results.db > gpurun_out/r3_prove_breakdown.txt; cat gpurun_out/r3_prove_breakdown.txt; rm -rf gpurun_out/pp ;;
+    nttbench) timeout -k 10 200 python tools/ntt_bench.py > gpurun_out/r3_ntt_bench.json 2>/dev/null; ok $? nttbench; cat gpurun_out/r3_ntt_bench.json | head -c 3000 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
