@@ -46,7 +46,7 @@ def roofline_obj(alg_bytes, ms, what):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50,
+    ap.add_argument("--steps", type=int, default=200,
                     help="timed steps; a step is ONE batched launch of --msm-batch MSMs over distinct input sets")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log2n", type=int, default=22)

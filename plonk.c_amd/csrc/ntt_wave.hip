@@ -763,11 +763,16 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
       rr[k] = F::out17(v[k], ninv);
     }
 #pragma unroll
-    for (int k = 0; k < G::E; k++) {
-      bo.stb(jj[k], rr[k]);
-      const bool in = jj[k] < lim;
-      wrapped |= (in && jj[k] < ntop) ? 1u << k : 0u;
-      last = max(last, (in && jj[k] >= ntop && rr[k]) ? jj[k] + 1u : 0u);
+    for (int k = 0; k < G::E; k++) bo.stb(jj[k], rr[k]);
+    // the wrapped positions and the trimmed length only when the job has them (uniform: the
+    // prover's batched products want neither, and the bookkeeping was ~7 VALU per element)
+    if (ntop) {   // (j < ntop <= 16 implies j < lim)
+#pragma unroll
+      for (int k = 0; k < G::E; k++) wrapped |= jj[k] < ntop ? 1u << k : 0u;
+    }
+    if (jb.nz) {
+#pragma unroll
+      for (int k = 0; k < G::E; k++) last = max(last, (jj[k] < lim && jj[k] >= ntop && rr[k]) ? jj[k] + 1u : 0u);
     }
     if (wrapped) last = max(last, wrap_fix<G>(jb, wrapped, p, tile, bf, LF, 1ull << p.k, rr));
   }

@@ -165,3 +165,32 @@ def test_f29_batch_and_range(hip):
     for bad in (12, 27):
         with pytest.raises(hip.PlonkHipError):
             hip.ntt29_dev(x[0], bad, False, st)
+
+
+@pytest.mark.parametrize("field", ["bb", "f29"])
+@pytest.mark.parametrize("k", [13, 17, 20, 21, 22, 24])
+@pytest.mark.parametrize("pattern", ["max", "alt"])
+def test_extreme_values_every_plan(hip, field, k, pattern):
+    """Inputs at the top of the field (every word p - 1) and alternating 0 / p - 1: the lazy F29
+    bounds (values < 4p forward, < 8p inverse, the multiply-free stage 0 of both directions, the
+    {w, p - w} pair butterflies) at their largest, on every pass plan; forward against the numpy
+    reference (k <= 23), inverse back to n x."""
+    import torch
+    p, gen = (P, 31) if field == "bb" else (P29, 3)
+    fwd = hip.ntt_dev if field == "bb" else hip.ntt29_dev
+    n = 1 << k
+    x = np.full(n, p - 1, np.int64)
+    if pattern == "alt":
+        x[::2] = 0
+    d = torch.from_numpy(x.astype(np.uint32).view(np.int32)).cuda()
+    st = torch.cuda.current_stream()
+    fwd(d, k, False, st)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy().view(np.uint32).astype(np.uint64)
+    assert int(got.max()) < p
+    if k <= 23:
+        assert np.array_equal(got, ntt_dif_reference(x, k, p, gen)), (field, k, pattern)
+    fwd(d, k, True, st)
+    torch.cuda.synchronize()
+    back = d.cpu().numpy().view(np.uint32).astype(np.uint64)
+    assert np.array_equal(back, (x.astype(np.uint64) * np.uint64(pow(2, k, p))) % np.uint64(p)), (field, k, pattern)
