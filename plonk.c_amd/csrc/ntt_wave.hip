@@ -56,6 +56,9 @@ namespace {
 #ifndef PLK_NTT_SWZ
 #define PLK_NTT_SWZ 1          // XOR-swizzled (bank-conflict-free) exchange layout; 0: the 1-in-32 pad
 #endif
+#ifndef PLK_NTT_CENTER_SWZ
+#define PLK_NTT_CENTER_SWZ 0   // center exchanges: 0 padded (2, swizzled only where the padding conflicts, spills)
+#endif
 #ifndef PLK_NTT_CW13
 #define PLK_NTT_CW13 8         // min waves per SIMD (launch bound): 8 = two 1024-thread blocks per CU
 #endif
@@ -413,6 +416,22 @@ struct Eng {
     }
     return true;
   }
+  // the padded layout (word e + e / 32) is conflict-free for exchange q when the 32 lanes of a
+  // half-wave hit 32 distinct banks in both the writing and the reading round
+  static constexpr bool pad_ok(int q, bool inv) {
+    for (int t = 0; t < 2; t++) {
+      bool used[32] = {};
+      for (uint32_t l = 0; l < 32; l++) {
+        uint32_t e = 0;
+        for (int i = 0; i < 5; i++)
+          if ((l >> i) & 1) e |= 1u << lane_bit(q + t, inv, i);
+        const uint32_t bank = (e + (e >> 5)) & 31u;
+        if (used[bank]) return false;
+        used[bank] = true;
+      }
+    }
+    return true;
+  }
   template <int Q, bool INV>
   __device__ static __forceinline__ uint32_t swz_h(uint32_t e) {
     constexpr Swz s = swz(Q, INV);
@@ -426,11 +445,13 @@ struct Eng {
   // registers (mapping from) -> LDS -> registers (mapping to).  Double-buffered: one barrier
   // suffices (the buffer written next was last read before the previous barrier); single
   // buffer: a second barrier before the buffer is written again.
-  template <int Q, bool INV, bool SWZ>
+  // SWZ: 0 = the padded layout, 1 = the swizzled layout wherever it is conflict-free, 2 = the
+  // swizzled layout only where the padded one conflicts (fewer live address registers: the center)
+  template <int Q, bool INV, int SWZ>
   __device__ static __forceinline__ void exchange(uint32_t (&v)[E], uint32_t* buf, uint32_t bf, int lbf, uint32_t bt,
                                                   int lbt) {
     if (PLK_NTT_DIAG & 2) return;
-    if (PLK_NTT_SWZ && SWZ && swz_ok(Q, INV)) {
+    if (PLK_NTT_SWZ && SWZ && swz_ok(Q, INV) && (SWZ == 1 || !pad_ok(Q, INV))) {
       // e = base | k << lb (disjoint bits) and h is linear: h(e) = h(base) ^ h(k << lb).  h only
       // moves bits < 5 and the bits >= 5 of k << lb are disjoint from base's, so the word is
       // (xw ^ lo_k) + hi_k: one XOR with a constant (none when lo_k = 0) and the rest in the
@@ -474,7 +495,7 @@ struct Eng {
   // last round on exit.  xc selects the exchange buffer (it counts exchanges).
   // SWZ: the swizzled exchange layout where it is conflict-free (the center kernel passes false:
   // it has no VGPRs to spare for the two extra base registers)
-  template <bool INV, bool SWZ = true, bool PW = false, bool TRIV0 = false, int Q = 0>
+  template <bool INV, int SWZ = 1, bool PW = false, bool TRIV0 = false, int Q = 0>
   __device__ static __forceinline__ void pass(uint32_t (&v)[E], uint32_t tid, uint32_t* bufs, int xc,
                                               const uint32_t* Tsm) {
     round<Q, INV, PW, TRIV0>(v, base_q<Q>(tid, INV), Tsm);
@@ -628,7 +649,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
 #pragma unroll
     for (int k = 0; k < G::E; k++) v[k] = lut[v[k]];
   }
-  G::template pass<false, true, PW, true>(v, tid, bufs, 0, Tsm);
+  G::template pass<false, 1, PW, true>(v, tid, bufs, 0, Tsm);
 #pragma unroll
   for (int k = 0; k < G::E; k++) {
     uint32_t x = v[k];
@@ -834,13 +855,13 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
       vb[k] = b_b.ld(b0 + ((uint32_t)k << L0));
     }
     __syncthreads();
-    if (!jobs.j[job].afix) G::template pass<false, false>(va, tid, bufs, 0, Tf);
+    if (!jobs.j[job].afix) G::template pass<false, PLK_NTT_CENTER_SWZ>(va, tid, bufs, 0, Tf);
     // (afix / bfix: b's transform is finished -- plk_wave_pretransform stored this pass's output
     // registers where their inputs were read -- so its lo = 0 pass is skipped)
-    if (!jobs.j[job].bfix) G::template pass<false, false>(vb, tid, bufs, G::XCH, Tf);
+    if (!jobs.j[job].bfix) G::template pass<false, PLK_NTT_CENTER_SWZ>(vb, tid, bufs, G::XCH, Tf);
 #pragma unroll
     for (int k = 0; k < G::E; k++) va[k] = F::pmul(va[k], vb[k]);
-    G::template pass<true, false>(va, tid, bufs, 2 * G::XCH, Tf);
+    G::template pass<true, PLK_NTT_CENTER_SWZ>(va, tid, bufs, 2 * G::XCH, Tf);
 #pragma unroll
     for (int k = 0; k < G::E; k++) b_c.st(bf + ((uint32_t)k << LF), va[k]);
   }
@@ -861,13 +882,14 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_fi
   const uint32_t b0 = G::template base_q<0>(tid, false);
   constexpr int L0 = G::lbq(0, false);
   uint32_t v[G::E];
+  const TileBuf bt(d + ((uint64_t)tile << TB));   // (the lo = 0 pass: consecutive words)
 #pragma unroll
-  for (int k = 0; k < G::E; k++) v[k] = d[G::index(p, tile, b0 + ((uint32_t)k << L0))];
+  for (int k = 0; k < G::E; k++) v[k] = bt.ld(b0 + ((uint32_t)k << L0));
   load_pass_tw<TB, G::NT>(Tlds, twf.small);
   __syncthreads();
   G::template pass<false, false>(v, tid, bufs, G::XCH, Tlds);
 #pragma unroll
-  for (int k = 0; k < G::E; k++) d[G::index(p, tile, b0 + ((uint32_t)k << L0))] = v[k];
+  for (int k = 0; k < G::E; k++) bt.st(b0 + ((uint32_t)k << L0), v[k]);
 }
 
 // Column-factor table of a 2-pass plan (lo = TB, M = k - TB): entry i = the high pass's factor
