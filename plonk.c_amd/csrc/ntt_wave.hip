@@ -167,6 +167,9 @@ struct FBB {
   // pointwise product's R^-1 is folded into the final scale, see ntt_group)
   __device__ static __forceinline__ uint32_t byte_val(uint32_t b) { return b % 17u; }
   __device__ static __forceinline__ uint32_t out17(uint32_t v, uint32_t ninv) { return bb::mmul(v, ninv) % 17u; }
+  // the same when the scale is already applied (the inverse column table holds it)
+  __device__ static __forceinline__ uint32_t out17s(uint32_t v) { return v % 17u; }
+  __device__ static __forceinline__ uint32_t scale(uint32_t c, uint32_t ninv) { return bb::mmul(c, ninv); }
   __device__ static __forceinline__ uint32_t canon(uint32_t v) { return v; }   // always reduced
 };
 // F29 bounds.  Montgomery REDC of t < p 2^32 lands in [0, 2p); so a product of ANY u32 with a
@@ -245,6 +248,15 @@ struct F29 {
     constexpr uint32_t C = (17u << 25) - f29::P;
     return (y + (y > (f29::P - 1) / 2 ? C : 0u)) % 17u;
   }
+  // the same when the scale is already applied (the inverse column table holds it): y < 8p, one
+  // reduction to y < 4p; the centered value is c = y - j p with j = floor((y + (p - 1) / 2) / p)
+  // (a multiply-high: exact below 6p - 1), and p = 12 mod 17, so c = y + 5 j mod 17
+  __device__ static __forceinline__ uint32_t out17s(uint32_t v) {
+    const uint32_t y = red4(v);
+    const uint32_t j = __umulhi(y + (f29::P - 1) / 2, 2454267022u) >> 28;   // ceil(2^60 / p)
+    return (y + 5u * j) % 17u;
+  }
+  __device__ static __forceinline__ uint32_t scale(uint32_t c, uint32_t ninv) { return f29::red1(f29::mmul(c, ninv)); }
 };
 
 // Tile engine: TB tile bits, R local bits per thread (E = 2^R registers, 2^(TB-R) threads
@@ -695,6 +707,8 @@ __device__ __forceinline__ uint32_t wrap_fix(const WJob& jb, uint32_t wrapped, c
 
 // Inverse (DIT) pass, u32 in place (the job's C); the final pass (TO_U8) scales by N^-1 (normal form,
 // which also leaves Montgomery form), reduces mod 17 and writes bytes for idx < out_len.
+// COLT (final passes only): the column table is the inverse one, whose factors carry that scale
+// (the pass is linear), so the bytes come from the pass's outputs directly (F::out17s).
 template <int TB, int R, int M, bool TO_U8, class F, bool COLT = false>
 __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, WTw tw, uint32_t ninv) {
   using G = Eng<TB, R, M, F>;
@@ -781,7 +795,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
       jj[k] = (N - ((uint32_t)tb + G::template toff_k<G::NR - 1, true>(p, of, bf, k))) & (N - 1);
-      rr[k] = F::out17(v[k], ninv);
+      rr[k] = COLT ? F::out17s(v[k]) : F::out17(v[k], ninv);
     }
 #pragma unroll
     for (int k = 0; k < G::E; k++) bo.stb(jj[k], rr[k]);
@@ -893,16 +907,18 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_fi
 }
 
 // Column-factor table of a 2-pass plan (lo = TB, M = k - TB): entry i = the high pass's factor
-// of the element at global index i = r 2^lo + L, w_{2^k}^(L bitrev_M(r)), fully reduced.
+// of the element at global index i = r 2^lo + L, w_{2^k}^(L bitrev_M(r)), fully reduced; with
+// ninv != 0 the product's final scale times that factor (the table of the last inverse pass).
 template <int TB, class F>
-__global__ __launch_bounds__(256) void coltab_kernel(uint32_t* __restrict__ out, int k, WTw tw) {
+__global__ __launch_bounds__(256) void coltab_kernel(uint32_t* __restrict__ out, int k, WTw tw, uint32_t ninv) {
   const uint64_t idx = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (1ull << k)) return;
   const int M = k - TB;
   const uint32_t L = (uint32_t)(idx & ((1u << TB) - 1)), r = (uint32_t)(idx >> TB);
   const uint32_t f = M ? __brev(r) >> (32 - M) : 0u;
   const uint32_t ex = (L * f) << (F::ADIC - k);
-  out[idx] = F::colf(tw.lo[ex & 4095u], tw.hi[ex >> 12]);
+  const uint32_t c = F::colf(tw.lo[ex & 4095u], tw.hi[ex >> 12]);
+  out[idx] = ninv ? F::scale(c, ninv) : c;
 }
 
 // ------------------------------------------------------------------------------ host side
@@ -942,6 +958,7 @@ int wave_plan(int k, int TB, int* Ms) {
 #endif
 constexpr int COLT_MIN_K = 13, COLT_MAX_K = 23;
 uint32_t* g_col[2][COLT_MAX_K + 1] = {};
+uint32_t* g_coli[2][COLT_MAX_K + 1] = {};   // the same times the product's final scale (ntt.hip's ninv)
 
 WTw to_wtw(const PlkTwTables& t, bool inv) {
   return inv ? WTw{t.small_i, t.lo_i, t.hi_i, nullptr} : WTw{t.small_f, t.lo_f, t.hi_f, nullptr};
@@ -952,6 +969,13 @@ WTw fwd_wtw(int k) {
   const bool f29 = F::ADIC == f29::TWO_ADICITY;
   WTw w = to_wtw(f29 ? plk_ntt_tables29() : plk_ntt_tables(), false);
   w.col = (k >= PLK_NTT_COLT_MIN_K && k >= COLT_MIN_K && k <= COLT_MAX_K) ? g_col[f29 ? 1 : 0][k] : nullptr;
+  return w;
+}
+// the same for a product's last inverse pass: the scaled column table
+template <class F>
+WTw inv_wtw(int k) {
+  WTw w = fwd_wtw<F>(k);
+  if (w.col) w.col = g_coli[F::ADIC == f29::TWO_ADICITY ? 1 : 0][k];
   return w;
 }
 
@@ -1099,12 +1123,13 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
   hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F>), dim3(grid), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, cj, twf,
                      (uint32_t)nj);
   PLK_HIP(hipGetLastError());
+  const WTw twi = inv_wtw<F>(k);
   WJobs later = jobs;   // sum groups add their members in the FIRST inverse pass only
   for (int j = 0; j < nj; j++) later.j[j].S1 = later.j[j].S2 = nullptr;
   for (int i = np - 2; i >= 0; i--) {
     const WPass p{k, lo[i]};
     const WJobs& jj = i == np - 2 ? jobs : later;
-    rc = i == 0 ? inv_m<TB, true, F>(Ms[i], p, jj, nj, twf, ninv, st)
+    rc = i == 0 ? inv_m<TB, true, F>(Ms[i], p, jj, nj, twi, ninv, st)
                 : inv_m<TB, false, F>(Ms[i], p, jj, nj, twf, 0u, st);
     if (rc) return rc;
   }
@@ -1158,19 +1183,27 @@ namespace {
 template <class F>
 int build_coltabs(int fi) {
   for (int k = COLT_MIN_K; k <= COLT_MAX_K; k++) {
-    if (g_col[fi][k]) continue;
-    PLK_HIP(hipMalloc((void**)&g_col[fi][k], 4ull << k));
-    const WTw tw = to_wtw(fi ? plk_ntt_tables29() : plk_ntt_tables(), false);
-    const unsigned blocks = (unsigned)((1ull << k) / 256);
-    if (tile_bits(k) == 13) hipLaunchKernelGGL((coltab_kernel<13, F>), dim3(blocks), dim3(256), 0, 0, g_col[fi][k], k, tw);
-    else hipLaunchKernelGGL((coltab_kernel<12, F>), dim3(blocks), dim3(256), 0, 0, g_col[fi][k], k, tw);
-    PLK_HIP(hipGetLastError());
+    // (the scale: ntt.hip's N^-1 R^2 for a 2^k product)
+    const uint32_t ninv = fi ? (uint32_t)((uint64_t)f29::hpow(1ull << k, f29::P - 2) * f29::R2 % f29::P)
+                             : (uint32_t)((uint64_t)bb::hpow(1ull << k, bb::P - 2) * bb::R2 % bb::P);
+    for (int s = 0; s < 2; s++) {
+      uint32_t*& t = s ? g_coli[fi][k] : g_col[fi][k];
+      if (t) continue;
+      PLK_HIP(hipMalloc((void**)&t, 4ull << k));
+      const WTw tw = to_wtw(fi ? plk_ntt_tables29() : plk_ntt_tables(), false);
+      const unsigned blocks = (unsigned)((1ull << k) / 256);
+      const uint32_t sc = s ? ninv : 0u;
+      if (tile_bits(k) == 13) hipLaunchKernelGGL((coltab_kernel<13, F>), dim3(blocks), dim3(256), 0, 0, t, k, tw, sc);
+      else hipLaunchKernelGGL((coltab_kernel<12, F>), dim3(blocks), dim3(256), 0, 0, t, k, tw, sc);
+      PLK_HIP(hipGetLastError());
+    }
   }
   return PLK_OK;
 }
 }  // namespace
 
-// 2 x 64 MB of column tables (BabyBear and F29, 2^13 .. 2^23 points), built on the device
+// 2 x 2 x 64 MB of column tables (BabyBear and F29, 2^13 .. 2^23 points; forward and scaled
+// inverse), built on the device
 int plk_wave_init_coltabs(void) {
   int rc = build_coltabs<FBB>(0);
   if (!rc) rc = build_coltabs<F29>(1);
@@ -1178,11 +1211,12 @@ int plk_wave_init_coltabs(void) {
   return rc;
 }
 void plk_wave_free_coltabs(void) {
-  for (auto& f : g_col)
-    for (auto& t : f) {
-      (void)hipFree(t);
-      t = nullptr;
-    }
+  for (auto* g : {&g_col, &g_coli})
+    for (auto& f : *g)
+      for (auto& t : f) {
+        (void)hipFree(t);
+        t = nullptr;
+      }
 }
 
 int plk_wave_poly_mul_batch_launch(const WJob* jobs, int nj, int k, int field, uint32_t ninv, hipStream_t st) {
