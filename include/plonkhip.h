@@ -78,7 +78,8 @@ enum {
   PLK_OPT_MSM_COPIES = 13,
   PLK_OPT_MSM_HALF = 14,
   PLK_OPT_MSM_SHARD_MIN = 15,    /* multi-device plk_msm_g1: split from this many points (2^16)      */
-  PLK_OPT_COUNT = 16
+  PLK_OPT_NTT_CENTER_SUM = 16,   /* 1: a sum group's products added in its leader's center item      */
+  PLK_OPT_COUNT = 17
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
 int64_t plk_get_option(int opt);              /* -1 for an unknown option */

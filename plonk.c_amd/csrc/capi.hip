@@ -432,6 +432,7 @@ const OptDef kOpt[PLK_OPT_COUNT] = {
     {0, 0, 8, false},                          // MSM_COPIES
     {1, 0, 1, false},                          // MSM_HALF
     {1 << 16, 1, 1ll << 40, false},            // MSM_SHARD_MIN
+    {1, 0, 1, false},                          // NTT_CENTER_SUM
 };
 struct Opts {
   std::atomic<int64_t> v[PLK_OPT_COUNT];

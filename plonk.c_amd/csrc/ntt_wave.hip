@@ -103,6 +103,15 @@ constexpr int WT_MAX_JOBS = PLK_WAVE_MAX_JOBS;
 struct WJobs {
   WJob j[WT_MAX_JOBS];
 };
+// the center launch's item order: slot i holds job[i] (-1: none) for every tile; the grid's
+// stride over the items then gives each group of blocks a fixed set of slots (the host balances
+// their pass units, center_schedule)
+constexpr int WT_SCHED_MAX = 32;
+struct WSched {
+  int n;    // slots
+  int nj;   // jobs of the batch
+  int8_t job[WT_SCHED_MAX];
+};
 // the distinct arrays of a batch that forward passes transform in place (a product's two
 // operands, or one standalone transform): u32 array d, first pass from bytes s8[0, ls)
 struct WArr {
@@ -162,6 +171,8 @@ struct FBB {
   __device__ static __forceinline__ uint32_t sum(uint32_t a, uint32_t b, uint32_t c) {
     return bb::madd(bb::madd(a, b), c);
   }
+  // a + b of two pointwise products, as a pointwise product's bound
+  __device__ static __forceinline__ uint32_t add2(uint32_t a, uint32_t b) { return bb::madd(a, b); }
   __device__ static __forceinline__ uint32_t colf(uint32_t cl, uint32_t ch) { return bb::mmul(cl, ch); }
   // a byte's value, NORMAL form (Montgomery twiddles keep a normal-form input normal; the
   // pointwise product's R^-1 is folded into the final scale, see ntt_group)
@@ -231,6 +242,8 @@ struct F29 {
   }
   // a, b < 4p: reduce one below 2p so that a b < p 2^32
   __device__ static __forceinline__ uint32_t pmul(uint32_t a, uint32_t b) { return f29::mmul(a, f29::red2(b)); }
+  // a + b of two pointwise products (< 2p each), below 2p again (an inverse pass's input bound)
+  __device__ static __forceinline__ uint32_t add2(uint32_t a, uint32_t b) { return f29::red2(a + b); }
   __device__ static __forceinline__ uint32_t colf(uint32_t cl, uint32_t ch) { return f29::red1(f29::mmul(cl, ch)); }
   // [0, 8p) -> [0, p): the stored result of a standalone transform
   __device__ static __forceinline__ uint32_t canon(uint32_t v) { return f29::red1(f29::red2(red4(v))); }
@@ -827,17 +840,17 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   }
 }
 
-// Center of poly_mul: last forward pass (lo = 0) of a and b, pointwise product, first
-// inverse pass, all in registers of one block; result written to the job's C (A, B or a
-// free array: A and B may be read by other jobs of the batch).  The last DIF round
+// Center of poly_mul: last forward pass (lo = 0) of a and b, pointwise product (plus a merged
+// sum group's member products), first inverse pass, all in registers of one block; result
+// written to the job's C (A, B or a free array: A and B may be read by other jobs of the batch).  The last DIF round
 // and the first DIT round both have local bits [0, R), so no exchange sits in between.
 // Stage twiddles: ONE table T in LDS (2^TB words): the inverse runs with the forward roots
 // (the DIT of the forward DFT; the final pass negates output positions, wt_inv_kernel), which
 // halves the block's LDS so that two blocks fit a CU.
-template <int TB, int R, class F>
+// GRP: the launch has merged sum groups (the item loop's per-pair steps; without, one pair)
+template <int TB, int R, class F, bool GRP>
 __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_center_kernel(WPass p, WJobs jobs,
-                                                                                                     WTw twf,
-                                                                                                     uint32_t nitems_jobs) {
+                                                                                                     WTw twf, WSched sc) {
   using G = Eng<TB, R, TB, F>;
   static_assert(G::NT == wt_ntc(TB), "tile block size");
   static_assert(G::lbq(G::NR - 1, false) == 0 && G::lbq(0, true) == 0, "center mapping");
@@ -849,33 +862,59 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
   constexpr int L0 = G::lbq(0, false);
   constexpr int LF = G::lbq(G::NR - 1, true);
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, true);
-  // persistent: the grid (<= 2 blocks per CU) walks the batch's (job, tile) items, so the
+  // persistent: the grid (<= 2 blocks per CU) walks the batch's (slot, tile) items, so the
   // 2^TB-word twiddle table is loaded once per block instead of once per tile
-  const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB), items = tiles * nitems_jobs;
+  const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB), items = tiles * (uint32_t)sc.n;
   // trimmed-length words of the jobs that want one: zeroed here, before the last inverse pass
-  if (blockIdx.x == 0 && tid < nitems_jobs && jobs.j[tid].nz) *jobs.j[tid].nz = 0u;
+  if (blockIdx.x == 0 && tid < (uint32_t)sc.nj && jobs.j[tid].nz) *jobs.j[tid].nz = 0u;
   // the twiddle table first (a "first item" flag inside the loop had the compiler hoist the
   // table's addresses out of the loop and spill them)
   load_pass_tw<TB, G::NT>(Tlds, twf.small);
   for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
-    const uint32_t job = it / tiles, tile = it - job * tiles;
+    const uint32_t slot = it / tiles, tile = it - slot * tiles;
+    const int job = sc.job[slot];
+    if (job < 0) continue;   // (uniform: a padding slot)
+    const WJob& J = jobs.j[job];
     // (the lo = 0 pass: a tile is 2^TB consecutive words; 32-bit offsets from its base)
     const uint64_t tb = (uint64_t)tile << TB;
-    const TileBuf b_a(jobs.j[job].A + tb), b_b(jobs.j[job].B + tb), b_c(jobs.j[job].C + tb);
+    const TileBuf b_c(J.C + tb);
     uint32_t va[G::E], vb[G::E];
+    int xc = 0;
+    // the job's pair, then a merged sum group's members' pairs: each pointwise product but the
+    // last is parked in the job's C tile (its own positions; C is no operand of the group) and
+    // added to the next one, so two register arrays suffice
+    for (int q = 0;; q++) {
+      const WJob& P = jobs.j[q ? J.cm[q - 1] : job];
+      const TileBuf b_a(P.A + tb), b_b(P.B + tb);
 #pragma unroll
-    for (int k = 0; k < G::E; k++) {
-      va[k] = b_a.ld(b0 + ((uint32_t)k << L0));
-      vb[k] = b_b.ld(b0 + ((uint32_t)k << L0));
+      for (int k = 0; k < G::E; k++) {
+        va[k] = b_a.ld(b0 + ((uint32_t)k << L0));
+        vb[k] = b_b.ld(b0 + ((uint32_t)k << L0));
+      }
+      if (q == 0) __syncthreads();   // (the previous item's last exchange read)
+      // (afix / bfix: the operand's transform is finished -- plk_wave_pretransform / wt_fixfwd_kernel
+      // stored this pass's output registers where their inputs were read -- so its pass is
+      // skipped; xc counts the exchanges so that double buffers keep alternating)
+      if (!P.afix) {
+        G::template pass<false, PLK_NTT_CENTER_SWZ>(va, tid, bufs, xc, Tf);
+        xc += G::XCH;
+      }
+      if (!P.bfix) {
+        G::template pass<false, PLK_NTT_CENTER_SWZ>(vb, tid, bufs, xc, Tf);
+        xc += G::XCH;
+      }
+#pragma unroll
+      for (int k = 0; k < G::E; k++) va[k] = F::pmul(va[k], vb[k]);
+      if (GRP && q) {
+#pragma unroll
+        for (int k = 0; k < G::E; k++) va[k] = F::add2(va[k], b_c.ld(b0 + ((uint32_t)k << L0)));
+      }
+      if (!GRP || q == J.ncm) break;
+#pragma unroll
+      for (int k = 0; k < G::E; k++) b_c.st(b0 + ((uint32_t)k << L0), va[k]);
+      __builtin_amdgcn_s_waitcnt(0);   // (the parked words are this thread's own: stored before reloaded)
     }
-    __syncthreads();
-    if (!jobs.j[job].afix) G::template pass<false, PLK_NTT_CENTER_SWZ>(va, tid, bufs, 0, Tf);
-    // (afix / bfix: b's transform is finished -- plk_wave_pretransform stored this pass's output
-    // registers where their inputs were read -- so its lo = 0 pass is skipped)
-    if (!jobs.j[job].bfix) G::template pass<false, PLK_NTT_CENTER_SWZ>(vb, tid, bufs, G::XCH, Tf);
-#pragma unroll
-    for (int k = 0; k < G::E; k++) va[k] = F::pmul(va[k], vb[k]);
-    G::template pass<true, PLK_NTT_CENTER_SWZ>(va, tid, bufs, 2 * G::XCH, Tf);
+    G::template pass<true, PLK_NTT_CENTER_SWZ>(va, tid, bufs, xc, Tf);
 #pragma unroll
     for (int k = 0; k < G::E; k++) b_c.st(bf + ((uint32_t)k << LF), va[k]);
   }
@@ -1065,6 +1104,71 @@ int inv_m(int M, WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipS
   return PLK_OK;
 }
 
+// pass units of a center job's item (the lo = 0 passes it runs; 0: no item)
+int center_units(const WJobs& cj, int j) {
+  const WJob& J = cj.j[j];
+  if (J.cskip) return 0;
+  int u = !J.afix + !J.bfix + 1;
+  for (int q = 0; q < J.ncm; q++) u += !cj.j[J.cm[q]].afix + !cj.j[J.cm[q]].bfix;
+  return u;
+}
+
+// The center launch's item order.  The grid strides over (slot, tile) items, so with tiles
+// dividing the grid, blocks [b T, (b + 1) T) take exactly the slots b, b + bins, b + 2 bins, ...
+// (bins = grid / T): the jobs go to bins by decreasing pass units, each to the bin with the
+// fewest so far (padding slots where the bins' job counts differ).  Otherwise the job order.
+WSched center_schedule(const WJobs& cj, int nj, uint32_t T, uint32_t nb) {
+  WSched s{};
+  s.nj = nj;
+  int list[WT_MAX_JOBS], units[WT_MAX_JOBS], n = 0;
+  for (int j = 0; j < nj; j++)
+    if ((units[j] = center_units(cj, j)) > 0) list[n++] = j;
+  const uint64_t G = std::min<uint64_t>((uint64_t)T * n, nb);
+  const uint32_t bins = G % T == 0 ? (uint32_t)(G / T) : 0u;
+  if (bins > 1 && (uint64_t)T * n > G) {
+    std::stable_sort(list, list + n, [&](int a, int b) { return units[a] > units[b]; });
+    int bl[WT_SCHED_MAX][WT_MAX_JOBS], cnt[WT_SCHED_MAX] = {}, load[WT_SCHED_MAX] = {}, mx = 0;
+    bool ok = bins <= WT_SCHED_MAX;
+    for (int i = 0; i < n && ok; i++) {
+      uint32_t b = 0;
+      for (uint32_t c = 1; c < bins; c++)
+        if (load[c] < load[b]) b = c;
+      bl[b][cnt[b]++] = list[i];
+      load[b] += units[list[i]];
+      mx = std::max(mx, cnt[b]);
+    }
+    if (ok && bins * (uint32_t)mx <= WT_SCHED_MAX) {
+      s.n = (int)bins * mx;
+      for (int i = 0; i < s.n; i++) {
+        const uint32_t b = (uint32_t)i % bins, r = (uint32_t)i / bins;
+        s.job[i] = (int8_t)((int)r < cnt[b] ? bl[b][r] : -1);
+      }
+      return s;
+    }
+  }
+  s.n = n;
+  for (int i = 0; i < n; i++) s.job[i] = (int8_t)list[i];
+  return s;
+}
+
+// Sum groups: the leader's center item adds its members' pointwise products (members without
+// items, the leader's inverse pass without their center outputs)
+void merge_groups(WJobs& cj, WJobs& ij, int nj) {
+  for (int L = 0; L < nj; L++) {
+    if (!ij.j[L].S1) continue;
+    int mem[2], nm = 0;
+    for (int j = 0; j < nj; j++)
+      if (j != L && (cj.j[j].C == ij.j[L].S1 || (ij.j[L].S2 && cj.j[j].C == ij.j[L].S2)) && nm < 2) mem[nm++] = j;
+    if (nm != (ij.j[L].S2 ? 2 : 1)) continue;
+    for (int q = 0; q < nm; q++) {
+      cj.j[L].cm[q] = mem[q];
+      cj.j[mem[q]].cskip = 1;
+    }
+    cj.j[L].ncm = nm;
+    ij.j[L].S1 = ij.j[L].S2 = nullptr;
+  }
+}
+
 template <int TB, class F>
 int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t st) {
   const WTw twf = fwd_wtw<F>(k);   // forward roots for the inverse too (wt_center_kernel)
@@ -1119,16 +1223,27 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
       PLK_HIP(hipGetLastError());
     }
   }
-  const uint32_t grid = std::min<uint32_t>(tiles * nj, center_blocks());
-  hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F>), dim3(grid), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, cj, twf,
-                     (uint32_t)nj);
-  PLK_HIP(hipGetLastError());
+  WJobs ij = jobs;   // the inverse passes' jobs
+  if (plk_opt(PLK_OPT_NTT_CENTER_SUM)) merge_groups(cj, ij, nj);
+  const WSched sc = center_schedule(cj, nj, tiles, center_blocks());
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)tiles * sc.n, center_blocks());
+  bool grp = false;
+  for (int j = 0; j < nj; j++) grp |= cj.j[j].ncm > 0;
+  if (grid) {
+    if (grp)
+      hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F, true>), dim3(grid), dim3(wt_ntc(TB)), 0, st, WPass{k, 0},
+                         cj, twf, sc);
+    else
+      hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F, false>), dim3(grid), dim3(wt_ntc(TB)), 0, st, WPass{k, 0},
+                         cj, twf, sc);
+    PLK_HIP(hipGetLastError());
+  }
   const WTw twi = inv_wtw<F>(k);
-  WJobs later = jobs;   // sum groups add their members in the FIRST inverse pass only
+  WJobs later = ij;   // sum groups add their members in the FIRST inverse pass only
   for (int j = 0; j < nj; j++) later.j[j].S1 = later.j[j].S2 = nullptr;
   for (int i = np - 2; i >= 0; i--) {
     const WPass p{k, lo[i]};
-    const WJobs& jj = i == np - 2 ? jobs : later;
+    const WJobs& jj = i == np - 2 ? ij : later;
     rc = i == 0 ? inv_m<TB, true, F>(Ms[i], p, jj, nj, twi, ninv, st)
                 : inv_m<TB, false, F>(Ms[i], p, jj, nj, twf, 0u, st);
     if (rc) return rc;

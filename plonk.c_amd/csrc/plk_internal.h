@@ -120,6 +120,11 @@ struct WJob {
   uint32_t* nz = nullptr;
   int bfix = 0;                    // B holds a plk_poly_mul_pretransform result
   int afix = 0;                    // (wave engine only: A finished in the batch, see wt_fixfwd_kernel)
+  // (wave engine only, set by it) a sum group whose pointwise products the leader's center item
+  // adds before its inverse pass: the members (cm, their A / B / afix / bfix) have no item
+  int cm[2] = {-1, -1};
+  int ncm = 0;
+  int cskip = 0;
 };
 constexpr int PLK_WAVE_MAX_JOBS = 12;   // jobs per launch of the wave engine (larger batches run in chunks)
 bool plk_wave_ntt_supported(int k);

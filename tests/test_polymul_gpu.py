@@ -345,3 +345,47 @@ def test_batch_shared_operands_fix_modes(hip, oracle, mode):
         else:
             want = oracle.poly_mul(polys[i].tobytes(), polys[j].tobytes())
         assert bytes.fromhex(got[k]) == want, (mode, k)
+
+
+@pytest.mark.parametrize("csum", [0, 1])
+def test_batch_center_sum_member_pair_first(hip, oracle, csum):
+    """A sum group whose only pair with both operands still to transform is a member's (a_6 a_7;
+    a_0 is shared with a later job, so its lo = 0 pass runs once beforehand): merged into the
+    leader's center item (PLK_OPT_NTT_CENTER_SUM = 1, the member's pair taking the leader's
+    place) or added in the inverse pass (0).  Same bytes either way."""
+    polys = [np.frombuffer(gen.poly_inputs(120 + i, n, 1)[0], np.uint8) for i, n in enumerate(_POOL)]
+    spec = [(0, 1, 0), (6, 7, 1), (0, 4, 0), (2, 3, 0)]
+    with hip.options(NTT_CENTER_SUM=csum):
+        outs = _run_batch(hip, polys, spec)
+    full = len(polys[0]) + len(polys[1]) - 1
+
+    def prod(i, j):
+        p = np.frombuffer(oracle.poly_mul(polys[i].tobytes(), polys[j].tobytes()), np.uint8).astype(np.int64)
+        return np.pad(p, (0, full - len(p)))
+    assert outs[0] == ((prod(0, 1) + prod(6, 7)) % 17).astype(np.uint8).tobytes()
+    assert outs[1] == b"\xEE" * full
+    for k in (2, 3):
+        i, j, _ = spec[k]
+        assert _trim(outs[k]) == oracle.poly_mul(polys[i].tobytes(), polys[j].tobytes()), k
+
+
+def test_batch_center_schedule_2_19(hip, oracle):
+    """Ten 2^18 x 2^18 products (2^19-point transforms: 128 tiles per product, 10 x 128 center
+    items on 512 resident blocks) with shared operands and a merged 3-product sum group, so the
+    items carry 1..5 lo = 0 passes and the center's slot order balances them over the blocks'
+    four item sets (center_schedule).  Every product against the oracle's NTT product."""
+    n = 1 << 18
+    polys = [np.frombuffer(gen.poly_inputs(140 + i, n, 1)[0], np.uint8) for i in range(9)]
+    spec = [(0, 1, 0), (2, 3, 1), (4, 5, 1), (0, 2, 0), (0, 0, 0), (1, 4, 0), (6, 7, 0), (7, 8, 0), (3, 6, 0),
+            (5, 8, 0)]
+    outs = _run_batch(hip, polys, spec)
+    full = 2 * n - 1
+
+    def prod(i, j):
+        p = np.frombuffer(oracle.poly_mul_ntt(polys[i].tobytes(), polys[j].tobytes()), np.uint8).astype(np.int64)
+        return np.pad(p, (0, full - len(p)))
+    want0 = (prod(0, 1) + prod(2, 3) + prod(4, 5)) % 17
+    assert outs[0] == want0.astype(np.uint8).tobytes()
+    for k in range(3, len(spec)):
+        i, j, _ = spec[k]
+        assert _trim(outs[k]) == oracle.poly_mul_ntt(polys[i].tobytes(), polys[j].tobytes()), k
