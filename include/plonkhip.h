@@ -153,7 +153,9 @@ int plk_poly_mul_dev(const uint8_t *d_a, size_t la, const uint8_t *d_b, size_t l
  * run this way; replaces a sequence of poly_mul calls, src/poly.h:106-122): products of one
  * transform size share each pass's launch, and operands given by the same pointer and length
  * are transformed once.  acc = 1 ADDS the product into the preceding job's output (a sum group:
- * a leader and up to two members of one shape; the members' out is not written).  Outputs are
+ * a leader and up to two members of its transform size, none with a longer product than the
+ * leader's; the members' out is not written; the whole sum must fit the transform's exact
+ * range, else PLK_ERR_RANGE).  Outputs are
  * untrimmed (la + lb - 1 bytes) and must not overlap any job's inputs (the last pass still reads
  * input bytes for the top coefficients of wrapped products).  d_work: at least the largest single
  * job's plk_poly_mul_workspace() (a sum group of g products: g times its member's); products run

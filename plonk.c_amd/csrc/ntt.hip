@@ -580,13 +580,16 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
   // F29 (lazy reduction, fewer VALU per butterfly) whenever every convolution term fits it
   bool use29 = plk_opt(PLK_OPT_NTT_F29) && k <= f29::TWO_ADICITY;
   for (int i = 0; i < m; i++) {
-    // a sum group of gs products must fit as a whole: gs * 64 min <= (p - 1) / 2
-    int gs = 1;
-    while (i + gs < m && g[i + gs].acc) gs++;
-    const uint64_t mn = g[i].la < g[i].lb ? g[i].la : g[i].lb;
-    if ((uint64_t)gs * mn * 128 >= f29::P) use29 = false;   // centered residues (F29::byte_val)
-    if (!use29 && (uint64_t)gs * mn * 256 >= bb::P) {
-      plk_set_error("poly_mul batch: a sum of %d products of %llu coefficients exceeds both fields", gs,
+    // a sum group must fit as a whole: 64 sum(min(la, lb)) <= (p - 1) / 2
+    uint64_t mn = 0;
+    int gs = 0;
+    do {
+      mn += g[i + gs].la < g[i + gs].lb ? g[i + gs].la : g[i + gs].lb;
+      gs++;
+    } while (i + gs < m && g[i + gs].acc);
+    if (mn * 128 >= f29::P) use29 = false;   // centered residues (F29::byte_val)
+    if (!use29 && mn * 256 >= bb::P) {
+      plk_set_error("poly_mul batch: a sum of %d products of %llu coefficients in all exceeds both fields", gs,
                     (unsigned long long)mn);
       return PLK_ERR_RANGE;
     }
@@ -656,13 +659,17 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
       L = i;
       continue;
     }
-    if (i == 0 || g[L].la != g[i].la || g[L].lb != g[i].lb || (es && es[L] != es[i]) || w[L].ngroup == 2 ||
+    // (one transform size, checked by the caller; no member longer than the leader's product,
+    // so its wrapped top, if any, is within the leader's)
+    if (i == 0 || g[i].la + g[i].lb > g[L].la + g[L].lb || w[L].ngroup == 2 ||
         L / PLK_WAVE_MAX_JOBS != i / PLK_WAVE_MAX_JOBS) {   // (a group runs in one launch chunk)
       plk_set_error("poly_mul batch: invalid sum group at job %d", i);
       return PLK_ERR_ARG;
     }
     (w[L].ngroup ? w[L].S2 : w[L].S1) = w[i].C;
     w[L].ga8[w[L].ngroup] = w[i].a8;
+    w[L].gla[w[L].ngroup] = w[i].la;
+    w[L].glb[w[L].ngroup] = w[i].lb;
     w[L].gb8[w[L].ngroup++] = w[i].b8;
     w[i].skip_inv = 1;
   }
@@ -813,9 +820,14 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
       plk_set_error("poly_mul batch: sum-group member %d is not a transform-sized product", i);
       return PLK_ERR_ARG;
     }
-    if (j.acc && (i == 0 || jobs[i - 1].la != j.la || jobs[i - 1].lb != j.lb)) {   // adds into job i-1
-      plk_set_error("poly_mul batch: sum-group member %d does not follow a product of its shape", i);
-      return PLK_ERR_ARG;
+    if (j.acc) {   // adds into the group's leader: the last non-member before it
+      int L = i - 1;
+      while (L > 0 && jobs[L].acc) L--;
+      if (i == 0 || jobs[L].acc || ks[L] != k || j.la + j.lb > jobs[L].la + jobs[L].lb) {
+        plk_set_error("poly_mul batch: sum-group member %d does not follow a product of its transform size and at "
+                      "least its length", i);
+        return PLK_ERR_ARG;
+      }
     }
     if (mn > PLK_DIRECT_MAX && k > PLK_SMALL_LOG) {
       if (mn * 256 >= bb::P || k > bb::TWO_ADICITY) {

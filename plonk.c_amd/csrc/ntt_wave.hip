@@ -688,7 +688,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
 
 // Wrapped products (la + lb - 1 = N + ntop): the last inverse pass wrote c[j] + c[N + j] mod 17
 // at j < ntop.  c[N + j] (sum group: of the group's sum) has only the terms a[i] b[N + j - i]
-// with i >= la - ntop + j (ntop - j <= 16 of them): computed from the bytes by the few threads
+// with i > N + j - lb (ntop - j <= 16 of them): computed from the bytes by the few threads
 // that hold such j, after the pass's stores (a rare path outside the unrolled store loop).
 // Returns 1 + the largest index it left a non-zero byte at (0: none).
 // (rr: the bytes this thread's pass stored, c[j] + c[N + j] mod 17 at the wrapped positions)
@@ -706,7 +706,9 @@ __device__ __forceinline__ uint32_t wrap_fix(const WJob& jb, uint32_t wrapped, c
     for (int g = 0; g <= jb.ngroup; g++) {
       const uint8_t* a = g ? jb.ga8[g - 1] : jb.a8;
       const uint8_t* b = g ? jb.gb8[g - 1] : jb.b8;
-      for (uint64_t i = jb.la - (uint64_t)jb.ntop + j; i < jb.la; i++) s += (a[i] % 17u) * (b[N + j - i] % 17u);
+      const uint64_t la = g ? jb.gla[g - 1] : jb.la, lb = g ? jb.glb[g - 1] : jb.lb;
+      if (la + lb - 1 <= N + j) continue;   // (a shorter member: no term reaches c[N + j])
+      for (uint64_t i = N + j + 1 - lb; i < la; i++) s += (a[i] % 17u) * (b[N + j - i] % 17u);
     }
     s %= 17u;
     const uint32_t lo = (rr[k] + 17u - s) % 17u;

@@ -73,8 +73,8 @@ struct PlkPolyMulJob {
   uint64_t lb;
   uint8_t* out;   // la + lb - 1 bytes
   // 1: ADD this product into the preceding job's output (a sum group: the leader and up to two
-  // members of the same shape, all of one transform size; the members' out is not written).
-  // The sum is exact while it fits the field (the caller's bound).
+  // members of one transform size, none longer than the leader's product; the members' out is
+  // not written).  The sum is exact while it fits the field (the caller's bound).
   int acc = 0;
   // optional: b's forward transform computed beforehand (plk_poly_mul_pretransform with the
   // same bytes, bt_k and bt_field): used when this product runs at 2^bt_k in field bt_field,
@@ -115,6 +115,7 @@ struct WJob {
   int ngroup = 0;
   const uint8_t* ga8[2] = {nullptr, nullptr};
   const uint8_t* gb8[2] = {nullptr, nullptr};
+  uint64_t gla[2] = {0, 0}, glb[2] = {0, 0};   // (the members' operand lengths)
   // trimmed length word (poly_new_internal's len, 0 = all zero) written by the last inverse
   // pass; the center kernel zeroes it first (nullptr: not wanted)
   uint32_t* nz = nullptr;

@@ -364,8 +364,7 @@ struct EvArgs {
   int post;          // scalar program the last block runs (EvPost)
 };
 
-__device__ void scalars_r4(uint8_t* S);
-__device__ void scalars_r5(uint8_t* S);
+__device__ void scalars_r45(uint8_t* S, uint32_t tz);
 
 // One launch per batch of evaluations: blockIdx.y = evaluation, EV_BLOCKS blocks each.  Every
 // block adds its partial sum with a ticket to its evaluation's arrival word; the last block of
@@ -441,10 +440,7 @@ __global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict
   if (atomicAdd(topw, 1u) != (uint32_t)a.ne - 1) return;
   __threadfence();
   *topw = 0;
-  if (a.post == EV_POST_R4) {   // round 4's scalars (incl. r_z) and round 5's (w_z constant)
-    scalars_r4(S);
-    scalars_r5(S);
-  }
+  if (a.post == EV_POST_R4) scalars_r45(S, S[S_TZ]);   // round 4's scalars (incl. r_z) and round 5's (w_z constant)
   if (a.post == EV_POST_ACC) stat[ST_ACC] = S[S_ACCW];   // acc_x(omega^n), src/plonk.h:366-368
 }
 
@@ -879,46 +875,58 @@ struct TrimArgs {
   int dst[11];
 };
 // ------------------------------------------------------------------ scalar programs
-__device__ void scalars_r4(uint8_t* S) {
-  const uint32_t al = S[S_ALPHA], be = S[S_BETA], ga = S[S_GAMMA], z = S[S_Z];
-  const uint32_t az = S[S_AZ], bz = S[S_BZ], cz = S[S_CZ], s1 = S[S_S1Z], s2 = S[S_S2Z];
-  const uint32_t zw = S[S_ZWZ], l1 = S[S_L1Z];
-  S[S_AB] = (uint8_t)(az * bz % HFP);
+// Rounds 4 and 5's scalar programs, run by one thread after the evaluations at z: the whole
+// 128-byte file is read at once (eight 16-byte loads in flight, not a chain of dependent byte
+// loads), the derived slots are stored at the end.  tz = t(z) (S_TZ: the caller may have just
+// stored it itself).
+__device__ void scalars_r45(uint8_t* S, uint32_t tz) {
+  uint32_t W[NSLOT / 4];
+#pragma unroll
+  for (int i = 0; i < NSLOT / 16; i++) {
+    const uint4 q = reinterpret_cast<const uint4*>(S)[i];
+    W[4 * i] = q.x; W[4 * i + 1] = q.y; W[4 * i + 2] = q.z; W[4 * i + 3] = q.w;
+  }
+  auto g = [&](int s) -> uint32_t { return (W[s >> 2] >> (8 * (s & 3))) & 0xFFu; };
+  const uint32_t al = g(S_ALPHA), be = g(S_BETA), ga = g(S_GAMMA), z = g(S_Z), v = g(S_V);
+  const uint32_t az = g(S_AZ), bz = g(S_BZ), cz = g(S_CZ), s1 = g(S_S1Z), s2 = g(S_S2Z);
+  const uint32_t zw = g(S_ZWZ), l1 = g(S_L1Z);
+  const uint32_t ab = az * bz % HFP;
   // src/plonk.h:547-556: r_2 scale
   const uint32_t x1 = (az + be * z + ga) % HFP;
-  const uint32_t x2 = (bz + be * S[S_K1] % HFP * z + ga) % HFP;
-  const uint32_t x3 = (cz + be * S[S_K2] % HFP * z + ga) % HFP;
+  const uint32_t x2 = (bz + be * g(S_K1) % HFP * z + ga) % HFP;
+  const uint32_t x3 = (cz + be * g(S_K2) % HFP * z + ga) % HFP;
   const uint32_t r2 = x1 * x2 % HFP * x3 % HFP * al % HFP;
   // src/plonk.h:569: r_4 scale
-  const uint32_t r4 = l1 * S[S_ALPHA2] % HFP;
-  S[S_R24] = (uint8_t)((r2 + r4) % HFP);
+  const uint32_t r4 = l1 * g(S_ALPHA2) % HFP;
+  const uint32_t r24 = (r2 + r4) % HFP;
   // src/plonk.h:559-566: r_3
-  S[S_BZW] = (uint8_t)(be * zw % HFP);
+  const uint32_t bzw = be * zw % HFP;
   const uint32_t y1 = (az + be * s1 + ga) % HFP, y2 = (bz + be * s2 + ga) % HFP;
-  S[S_R3] = (uint8_t)(y1 * y2 % HFP * al % HFP);
-  S[S_R3B] = (uint8_t)(S[S_R3] * S[S_BZW] % HFP);   // r_3 scale times the s_sigma_3 factor
+  const uint32_t r3 = y1 * y2 % HFP * al % HFP;
+  const uint32_t r3b = r3 * bzw % HFP;   // r_3 scale times the s_sigma_3 factor
   // r_z = r(z) (src/plonk.h:571) from the evaluations of r(x)'s terms: evaluation is a ring
   // homomorphism, so sum_i c_i p_i(z) = (sum_i c_i p_i)(z) mod 17
-  const uint32_t cs[6] = {S[S_AB], az, bz, cz, S[S_R24], S[S_R3B]};
-  const uint32_t ez[6] = {S[S_QMZ], S[S_QLZ], S[S_QRZ], S[S_QOZ], S[S_ZXZ], S[S_P3Z]};
+  const uint32_t cs[6] = {ab, az, bz, cz, r24, r3b};
+  const uint32_t ez[6] = {g(S_QMZ), g(S_QLZ), g(S_QRZ), g(S_QOZ), g(S_ZXZ), g(S_P3Z)};
   uint32_t rz = 0;
-  for (int i = 0; i < 6; i++) {
-    rz += cs[i] * ez[i];
-    S[S_VAB + i] = (uint8_t)(S[S_V] * cs[i] % HFP);   // w_z(x) takes v r(x) term by term
-  }
-  S[S_RZ] = (uint8_t)(rz % HFP);
-  S[S_NEGZWZ] = (uint8_t)hneg(zw);
-}
-
-__device__ void scalars_r5(uint8_t* S) {
+  for (int i = 0; i < 6; i++) rz += cs[i] * ez[i];
+  rz %= HFP;
   // constant term of w_z(x), src/plonk.h:584-603
-  uint32_t c = hneg(S[S_TZ]);
-  c += S[S_V] * hneg(S[S_RZ]);
-  c += S[S_V2] * hneg(S[S_AZ]);
-  c += S[S_V3] * hneg(S[S_BZ]);
-  c += S[S_V4] * hneg(S[S_CZ]);
-  c += S[S_V5] * hneg(S[S_S1Z]);
-  c += S[S_V6] * hneg(S[S_S2Z]);
+  uint32_t c = hneg(tz);
+  c += v * hneg(rz);
+  c += g(S_V2) * hneg(az);
+  c += g(S_V3) * hneg(bz);
+  c += g(S_V4) * hneg(cz);
+  c += g(S_V5) * hneg(s1);
+  c += g(S_V6) * hneg(s2);
+  S[S_AB] = (uint8_t)ab;
+  S[S_R24] = (uint8_t)r24;
+  S[S_BZW] = (uint8_t)bzw;
+  S[S_R3] = (uint8_t)r3;
+  S[S_R3B] = (uint8_t)r3b;
+  for (int i = 0; i < 6; i++) S[S_VAB + i] = (uint8_t)(v * cs[i] % HFP);   // w_z(x) takes v r(x) term by term
+  S[S_RZ] = (uint8_t)rz;
+  S[S_NEGZWZ] = (uint8_t)hneg(zw);
   S[S_W0] = (uint8_t)(c % HFP);
 }
 
@@ -1122,6 +1130,7 @@ struct plk_prover {
   uint32_t* d_tick = nullptr;      // eval arrival words (zeroed at create, re-armed by eval_kernel)
   uint8_t* d_rem = nullptr;        // Z_H division: one remainder vote per block
   int lin_sum = 0;                 // round 3: a q_l + b q_r + c q_o computed as one sum (in AQL)
+  int t2_sum = 0;                  // round 3: (a b) q_m + t_2 computed as one sum (in T2)
   uint64_t rem_blocks = 0;
   uint32_t* d_bsum = nullptr;      // scan block sums
   PlkMsmResult* d_res = nullptr;   // 9 MSM records
@@ -1628,11 +1637,20 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
                           // residues hold the 2n x 2n products exactly)
                           {P->A2, L.la, P->B2, L.la, P->T2a}, {P->C2, L.la, cZ, L.lzx, P->T2b},
                           {P->A3, L.la, P->B3, L.la, P->T3a}, {P->C3, L.la, P->ZW, L.lzw, P->T3b}};
-    PlkPolyMulJob g2[] = {{P->AB, L.lab, QM, n, P->ABQM},
-                          {P->T2a, L.l2a, P->T2b, L.la + L.lzx - 1, P->T2},
+    // (a b) q_m ADDED into t_2 = (A2 B2)(C2 z) when their sum fits F29's centered range,
+    // 64 (min(l2a, la + lzx - 1) + min(lab, n)) <= (p - 1) / 2 (n <= ~1.2 M): one 4n inverse
+    // transform fewer, one numerator term fewer (t_3 enters with -1, so it stays apart)
+    const uint64_t t2b = L.la + L.lzx - 1;
+    const int grp = plk_poly_mul_summable(L.lab, n) && plk_poly_mul_summable(L.l2a, t2b) &&
+                            (std::min(L.l2a, t2b) + std::min<uint64_t>(L.lab, n)) * 128 < f29::P
+                        ? 1
+                        : 0;
+    P->t2_sum = grp;
+    PlkPolyMulJob g2[] = {{P->T2a, L.l2a, P->T2b, t2b, P->T2},
+                          {P->AB, L.lab, QM, n, P->ABQM, grp},
                           {P->T3a, L.l2a, P->T3b, L.la + L.lzw - 1, P->T3}};
     if (pre) {   // preprocessed circuit: the fixed b operands' transforms (plk_prover_preprocess)
-      PlkPolyMulJob* const js[] = {&g1[0], &g1[1], &g1[2], &g1[3], &g1[5], &g2[0]};
+      PlkPolyMulJob* const js[] = {&g1[0], &g1[1], &g1[2], &g1[3], &g1[5], &g2[1]};
       const int which[] = {5, 6, 3, 12, 10, 4};   // q_l q_r q_o l_1_x s_sigma_3 q_m
       for (int i = 0; i < 6; i++) {
         const plk_prover::Fixed& f = P->fix[which[i]];
@@ -1651,17 +1669,25 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   const uint64_t part = n + 2;
   const uint64_t lmid = L.ltx > part ? std::min<uint64_t>(part, L.ltx - part) : 0;
   const uint64_t lhi = L.ltx > 2 * part ? L.ltx - 2 * part : 0;
-  const LcArgs num = P->lin_sum
-                         ? make_lc({{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {QC, n}, {P->T2, L.l2}, {P->T3, L.l3},
-                                    {P->T4, L.lt4}},
-                                   {S_ONE, S_ONE, S_ONE, S_ONE, S_NEG1, S_ONE}, -1, -1, S_ONE, -1, P->NUM, L.lnum)
-                         : make_lc({{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {P->BQR, L.lq1}, {P->CQO, L.lq1}, {QC, n},
-                                    {P->T2, L.l2}, {P->T3, L.l3}, {P->T4, L.lt4}},
-                                   {S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_NEG1, S_ONE}, -1, -1, S_ONE, -1,
-                                   P->NUM, L.lnum);
+  // (the sums in AQL / T2 stand for their members' terms)
+  LcArgs num = P->lin_sum
+                   ? make_lc({{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {QC, n}, {P->T2, L.l2}, {P->T3, L.l3}, {P->T4, L.lt4}},
+                             {S_ONE, S_ONE, S_ONE, S_ONE, S_NEG1, S_ONE}, -1, -1, S_ONE, -1, P->NUM, L.lnum)
+                   : make_lc({{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {P->BQR, L.lq1}, {P->CQO, L.lq1}, {QC, n},
+                              {P->T2, L.l2}, {P->T3, L.l3}, {P->T4, L.lt4}},
+                             {S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_NEG1, S_ONE}, -1, -1, S_ONE, -1, P->NUM,
+                             L.lnum);
+  if (P->t2_sum) {   // drop the ABQM term (first)
+    for (int t = 1; t < num.nt; t++) {
+      num.p[t - 1] = num.p[t];
+      num.len[t - 1] = num.len[t];
+      num.slot[t - 1] = num.slot[t];
+    }
+    num.nt--;
+  }
   // (q_c is the caller's buffer: n % 4 == 0 keeps its last dword inside it; the intermediates
   // carry >= 16 bytes of padding)
-  bool fused = P->zh_kind == 0 && (P->zh_len - 1) % 4 == 0 && L.lnum > P->zh_len - 1 && (num.nt == 8 || num.nt == 6) &&
+  bool fused = P->zh_kind == 0 && (P->zh_len - 1) % 4 == 0 && L.lnum > P->zh_len - 1 && num.nt >= 5 && num.nt <= 8 &&
                (uintptr_t)P->TX % 4 == 0 && n % 4 == 0 && (P->zh_len - 1) / 4 < (1ull << 31) && L.ltx / (P->zh_len - 1) < 8;
   for (int t = 0; t < num.nt; t++) fused = fused && (uintptr_t)num.p[t] % 4 == 0;
   if (fused) {
@@ -1671,12 +1697,13 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
 #define PLK_NUMDIV(NT_, K_)                                                                                      \
   hipLaunchKernelGGL((numdiv_kernel<NT_, K_>), dim3((unsigned)nb), dim3(256), 0, P->st, num, dS, m, P->zh_lead, P->zh_c, \
                      P->TX, ql, cq, cr, sl, P->d_rem)
-    if (num.nt == 6) {
-      if (cq + 1 <= 4) PLK_NUMDIV(6, 4);
-      else PLK_NUMDIV(6, 8);
-    } else {
-      if (cq + 1 <= 4) PLK_NUMDIV(8, 4);
-      else PLK_NUMDIV(8, 8);
+    // (5..8 terms: with / without the two sums)
+    const bool k4 = cq + 1 <= 4;
+    switch (num.nt) {
+      case 5: if (k4) PLK_NUMDIV(5, 4); else PLK_NUMDIV(5, 8); break;
+      case 6: if (k4) PLK_NUMDIV(6, 4); else PLK_NUMDIV(6, 8); break;
+      case 7: if (k4) PLK_NUMDIV(7, 4); else PLK_NUMDIV(7, 8); break;
+      default: if (k4) PLK_NUMDIV(8, 4); else PLK_NUMDIV(8, 8); break;
     }
 #undef PLK_NUMDIV
     PLK_HIP(hipGetLastError());

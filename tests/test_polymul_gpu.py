@@ -237,7 +237,7 @@ def test_batch_group_across_launch_chunks(hip, oracle):
 
 def test_batch_small_workspace_and_bad_groups(hip, oracle):
     """a workspace of one product's size runs every product (and a 2-product group needs two);
-    a member must follow a product of its own shape"""
+    a member must follow a product of its transform size and at least its length"""
     import torch
     dev = torch.device("cuda:0")
     polys = [np.frombuffer(gen.poly_inputs(90 + i, n, 1)[0], np.uint8) for i, n in enumerate(_POOL)]
@@ -260,7 +260,7 @@ def test_batch_small_workspace_and_bad_groups(hip, oracle):
     outs = run([(0, 1, 0), (6, 7, 1)], 2 * one)
     assert len(outs[0]) == len(polys[0]) + len(polys[1]) - 1
     with pytest.raises(Exception, match="does not follow"):
-        run([(2, 3, 0), (0, 1, 1)], 2 * one)              # shape differs from the preceding job
+        run([(2, 3, 0), (0, 1, 1)], 2 * one)              # longer than the preceding job
 
 
 # ---- blocked products: shapes beyond one transform's exact range --------------------------
@@ -389,3 +389,24 @@ def test_batch_center_schedule_2_19(hip, oracle):
     for k in range(3, len(spec)):
         i, j, _ = spec[k]
         assert _trim(outs[k]) == oracle.poly_mul_ntt(polys[i].tobytes(), polys[j].tobytes()), k
+
+
+@pytest.mark.parametrize("csum", [0, 1])
+def test_batch_sum_group_mixed_shapes(hip, oracle, csum):
+    """A sum group of one transform size (2^13) with shorter members: a_0 a_1 (8196 coefficients,
+    wrapped by 4) + a_2 a_3 (8095, not wrapped) + a_6 a_4 (8195, wrapped by 3) -- the wrapped top
+    coefficients come from each product's own operand lengths.  A member longer than its leader
+    is refused."""
+    polys = [np.frombuffer(gen.poly_inputs(160 + i, n, 1)[0], np.uint8) for i, n in enumerate(_POOL)]
+    spec = [(5, 5, 0), (0, 1, 0), (2, 3, 1), (6, 4, 1)]
+    with hip.options(NTT_CENTER_SUM=csum):
+        outs = _run_batch(hip, polys, spec)
+    full = len(polys[0]) + len(polys[1]) - 1
+
+    def prod(i, j):
+        p = np.frombuffer(oracle.poly_mul(polys[i].tobytes(), polys[j].tobytes()), np.uint8).astype(np.int64)
+        return np.pad(p, (0, full - len(p)))
+    assert outs[1] == ((prod(0, 1) + prod(2, 3) + prod(6, 4)) % 17).astype(np.uint8).tobytes()
+    assert _trim(outs[0]) == oracle.poly_mul(polys[5].tobytes(), polys[5].tobytes())
+    with pytest.raises(Exception, match="does not follow"):
+        _run_batch(hip, polys, [(2, 3, 0), (0, 1, 1)])
