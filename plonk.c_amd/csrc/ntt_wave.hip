@@ -732,8 +732,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
-  const WJob& jb = jobs.j[blockIdx.y];
-  if (jb.skip_inv) return;   // a sum-group member: its leader's pass adds it
+  const WJob& jb = jobs.j[blockIdx.y];   // (sum-group members are not in the grid: no inverse of their own)
   uint32_t* d = jb.C;
   uint8_t* out8 = jb.out8;
   const uint64_t out_len = jb.out_len;
@@ -1241,13 +1240,18 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
     PLK_HIP(hipGetLastError());
   }
   const WTw twi = inv_wtw<F>(k);
-  WJobs later = ij;   // sum groups add their members in the FIRST inverse pass only
-  for (int j = 0; j < nj; j++) later.j[j].S1 = later.j[j].S2 = nullptr;
+  // the inverse passes' grid: the jobs that have any (sum-group members have none)
+  WJobs ic{};
+  int ni = 0;
+  for (int j = 0; j < nj; j++)
+    if (!ij.j[j].skip_inv) ic.j[ni++] = ij.j[j];
+  WJobs later = ic;   // sum groups add their members in the FIRST inverse pass only
+  for (int j = 0; j < ni; j++) later.j[j].S1 = later.j[j].S2 = nullptr;
   for (int i = np - 2; i >= 0; i--) {
     const WPass p{k, lo[i]};
-    const WJobs& jj = i == np - 2 ? ij : later;
-    rc = i == 0 ? inv_m<TB, true, F>(Ms[i], p, jj, nj, twi, ninv, st)
-                : inv_m<TB, false, F>(Ms[i], p, jj, nj, twf, 0u, st);
+    const WJobs& jj = i == np - 2 ? ic : later;
+    rc = i == 0 ? inv_m<TB, true, F>(Ms[i], p, jj, ni, twi, ninv, st)
+                : inv_m<TB, false, F>(Ms[i], p, jj, ni, twf, 0u, st);
     if (rc) return rc;
   }
   return PLK_OK;

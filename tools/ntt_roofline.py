@@ -11,9 +11,11 @@ trim_pack_kernel); --all (default): every wt_* dispatch, aggregated per (kernel,
 Butterflies counted (the algorithmic work, radix-2 count):
   wt_fwd/wt_inv_kernel<TB, R, M, ...>: blocks x 2^(TB-1) x M  (blocks = grid_x / workgroup x grid_y;
       the high passes' one column multiply per element is NOT counted, so the fraction is a lower
-      bound; sum-group members skipped by the inverse pass are counted, an upper bound there)
+      bound; sum-group members have no inverse blocks)
   wt_center_kernel<TB, R, F>: (job, tile) items x 2^(TB-1) x TB x 3 (two forward transforms and one
-      inverse per item); the items are the next inverse pass's blocks (same batch)
+      inverse per item); the items are the next inverse pass's blocks (same batch).  An estimate:
+      fixed operands' skipped passes are counted, merged sum-group members' forward passes are
+      not (the prover's 2^21 batch: 24 counted per tile for 22 run; 2^22: 6 for 8)
 Peak: F29 / BabyBear DIF for forward passes, DIT for inverse, (2 DIF + 1 DIT) / 3 for the center."""
 import json
 import re
