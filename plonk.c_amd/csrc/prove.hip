@@ -67,6 +67,10 @@ enum Stat : int {
 };
 
 __device__ __forceinline__ uint32_t hneg(uint32_t a) { return a ? HFP - a : 0; }
+// x mod 17 for x < 69632 by 24-bit multiplies (full rate; `% 17` on a u32 takes a quarter-rate
+// multiply-high): 61681 = (2^20 + 1) / 17, so floor(x 61681 / 2^20) = floor(x / 17) for x < 2^20,
+// and x 61681 < 2^32 (checked on the host for every x < 69632).  Every call site's bound is noted.
+__device__ __forceinline__ uint32_t hmod(uint32_t x) { return x - 17u * (__umul24(x, 61681u) >> 20); }
 __device__ __forceinline__ uint32_t hpow_d(uint32_t b, uint64_t e) {
   uint32_t r = 1;
   b %= HFP;
@@ -174,8 +178,8 @@ __global__ __launch_bounds__(256) void lincomb16_kernel(LcArgs a, const uint8_t*
     uint32_t o[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-      uint32_t v = acc[k] % HFP * sc % HFP;
-      if (a.twist >= 0) v = v * (x == 0 ? (i + k == 0 ? 1u : 0u) : tw[k]) % HFP;
+      uint32_t v = hmod(hmod(acc[k]) * sc);   // (acc <= 16 terms x 16 x 255 + 32 < 69632)
+      if (a.twist >= 0) v = hmod(v * (x == 0 ? (i + k == 0 ? 1u : 0u) : tw[k]));
       o[k >> 2] |= v << (8 * (k & 3));
     }
     if (i + 16 <= a.out_len) {
@@ -250,7 +254,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a, const SlotFile f,
     {
       const uint32_t w = load4(a.zh, a.lz, i);
 #pragma unroll
-      for (int k = 0; k < 4; k++) z[k + 2] = ((w >> (8 * k)) & 0xFFu) % HFP;
+      for (int k = 0; k < 4; k++) z[k + 2] = hmod((w >> (8 * k)) & 0xFFu);
       z[0] = (i >= 2 && i - 2 < a.lz) ? a.zh[i - 2] % HFP : 0u;
       z[1] = (i >= 1 && i - 1 < a.lz) ? a.zh[i - 1] % HFP : 0u;
     }
@@ -263,19 +267,20 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a, const SlotFile f,
       const int sh = 8 * k;
       auto byte = [&](uint32_t f) { return (f >> sh) & 0xFFu; };
       const uint32_t c0 = (i + k == 0), c1 = (i + k == 1);
-      const uint32_t va = (ba0 * z[k + 2] + ba1 * z[k + 1] + byte(fa)) % HFP;
-      const uint32_t vb = (bb0 * z[k + 2] + bb1 * z[k + 1] + byte(fb)) % HFP;
-      const uint32_t vc = (bc0 * z[k + 2] + bc1 * z[k + 1] + byte(fc)) % HFP;
-      const uint32_t vz = (bz0 * z[k + 2] + bz1 * z[k + 1] + bz2 * z[k] + byte(fz)) % HFP;
+      // (hmod bounds: scalars < 17, bytes < 256: every argument < 16 (16 + 3 * 256 + 256))
+      const uint32_t va = hmod(ba0 * z[k + 2] + ba1 * z[k + 1] + byte(fa));
+      const uint32_t vb = hmod(bb0 * z[k + 2] + bb1 * z[k + 1] + byte(fb));
+      const uint32_t vc = hmod(bc0 * z[k + 2] + bc1 * z[k + 1] + byte(fc));
+      const uint32_t vz = hmod(bz0 * z[k + 2] + bz1 * z[k + 1] + bz2 * z[k] + byte(fz));
       oA |= va << sh; oB |= vb << sh; oC |= vc << sh; oZ |= vz << sh;
-      oA2 |= (va + c0 * ga + c1 * be) % HFP * al % HFP << sh;
-      oB2 |= (vb + c0 * ga + c1 * bk1) % HFP << sh;
-      oC2 |= (vc + c0 * ga + c1 * bk2) % HFP << sh;
-      oA3 |= (va + be * byte(f1) + c0 * ga) % HFP * al % HFP << sh;
-      oB3 |= (vb + be * byte(f2) + c0 * ga) % HFP << sh;
-      oC3 |= (vc + be * byte(f3) + c0 * ga) % HFP << sh;
-      oZW |= vz * (om == 0 ? c0 : tw[k]) % HFP << sh;
-      oZ1 |= (vz + c0 * 16u) % HFP * al2 % HFP << sh;
+      oA2 |= hmod((va + c0 * ga + c1 * be) * al) << sh;
+      oB2 |= hmod(vb + c0 * ga + c1 * bk1) << sh;
+      oC2 |= hmod(vc + c0 * ga + c1 * bk2) << sh;
+      oA3 |= hmod((va + be * byte(f1) + c0 * ga) * al) << sh;
+      oB3 |= hmod(vb + be * byte(f2) + c0 * ga) << sh;
+      oC3 |= hmod(vc + be * byte(f3) + c0 * ga) << sh;
+      oZW |= hmod(vz * (om == 0 ? c0 : tw[k])) << sh;
+      oZ1 |= hmod((vz + c0 * 16u) * al2) << sh;
     }
     store4(a.cA, a.la, i, oA); store4(a.cB, a.la, i, oB); store4(a.cC, a.la, i, oC);
     store4(a.A2, a.la, i, oA2); store4(a.B2, a.la, i, oB2); store4(a.C2, a.la, i, oC2);
@@ -319,8 +324,8 @@ __global__ __launch_bounds__(256) void lincomb16_batch_kernel(LcBatch b, const u
     uint32_t o[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-      uint32_t v = acc[k] % HFP * sc % HFP;
-      if (a.twist >= 0) v = v * (x == 0 ? (i + k == 0 ? 1u : 0u) : tw[k]) % HFP;
+      uint32_t v = hmod(hmod(acc[k]) * sc);   // (acc <= 16 terms x 16 x 255 + 32 < 69632)
+      if (a.twist >= 0) v = hmod(v * (x == 0 ? (i + k == 0 ? 1u : 0u) : tw[k]));
       o[k >> 2] |= v << (8 * (k & 3));
     }
     if (i + 16 <= a.out_len) {
@@ -418,17 +423,16 @@ __global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict
       acc = (acc + s) % HFP;
     }
   }
-  __shared__ uint32_t red[256];
-  red[threadIdx.x] = acc;
+  // block sum: wave shuffles, then one barrier (acc < 17: the sum fits easily)
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  __shared__ uint32_t red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
   if (threadIdx.x != 0) return;
   // the partial travels inside the atomic (no fence: a device-scope release per block costs an
   // L2 writeback each, 2048 of them took 60 us): row word = sum | arrivals << 32
-  const uint32_t mine = red[0] % HFP;
+  const uint32_t mine = (red[0] + red[1] + red[2] + red[3]) % HFP;
   unsigned long long* row = reinterpret_cast<unsigned long long*>(tick) + e * (TICK_STRIDE / 2);
   const unsigned long long old = atomicAdd(row, (unsigned long long)mine | (1ull << 32));
   if ((uint32_t)(old >> 32) != gridDim.x - 1) return;
@@ -519,7 +523,7 @@ __global__ __launch_bounds__(256) void divide_binomial4_kernel(const uint8_t* __
 #pragma unroll
         for (int b = 0; b < 4; b++) {
           if ((uint32_t)k >= skip[b]) {
-            const uint32_t v = (((w[k] >> (8 * b)) & 0xFFu) + nc * prev[b]) % HFP * li % HFP;
+            const uint32_t v = hmod((((w[k] >> (8 * b)) & 0xFFu) + nc * prev[b]) * li);   // (<= (255 + 256) x 16)
             prev[b] = v;
             o |= v << (8 * b);
           }
@@ -586,7 +590,7 @@ __device__ __forceinline__ uint32_t lc_word(const LcArgs& a, const uint32_t (&cf
   }
   uint32_t o = 0;
 #pragma unroll
-  for (int b = 0; b < 4; b++) o |= (acc[b] % HFP * sc % HFP) << (8 * b);
+  for (int b = 0; b < 4; b++) o |= hmod(hmod(acc[b]) * sc) << (8 * b);   // (acc <= 8 x 16 x 255 + 16)
   return o;
 }
 template <int NT, int KMAX>
@@ -622,7 +626,7 @@ __global__ __launch_bounds__(256) void numdiv_kernel(LcArgs a, const uint8_t* __
 #pragma unroll
       for (int b = 0; b < 4; b++) {
         if ((uint32_t)k >= skip[b]) {
-          const uint32_t v = (((w[k] >> (8 * b)) & 0xFFu) + nc * prev[b]) % HFP * li % HFP;
+          const uint32_t v = hmod((((w[k] >> (8 * b)) & 0xFFu) + nc * prev[b]) * li);   // (<= (255 + 256) x 16)
           prev[b] = v;
           o |= v << (8 * b);
         }
@@ -647,7 +651,7 @@ __global__ __launch_bounds__(256) void numdiv_kernel(LcArgs a, const uint8_t* __
 #pragma unroll
   for (int b = 0; b < 4; b++) {
     const uint64_t r = r0 + b;
-    if (r < m && r < nl && (((wr >> (8 * b)) & 0xFFu) + nc * prev[b]) % HFP) rv = 1;
+    if (r < m && r < nl && hmod(((wr >> (8 * b)) & 0xFFu) + nc * prev[b])) rv = 1;
   }
   const int vote = __syncthreads_or(rv != 0);
   if (threadIdx.x == 0) rem_part[blockIdx.x] = vote ? 1 : 0;
@@ -760,7 +764,7 @@ __global__ __launch_bounds__(SCAN_T) void lincomb_scan_kernel(LcBatch b, LinDivs
   uint32_t o[4] = {0, 0, 0, 0}, agg = 0;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    const uint32_t v = i + k < a.out_len ? acc[k] % HFP * sc % HFP : 0u;
+    const uint32_t v = i + k < a.out_len ? hmod(hmod(acc[k]) * sc) : 0u;   // (acc <= 16 x 16 x 255 + 32)
     o[k >> 2] |= v << (8 * (k & 3));
     if (i + k > 0) agg += v * pw[k];   // (i + k) mod 16 = k
   }
@@ -805,7 +809,7 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(LinDivs L, const
 #pragma unroll
   for (int k = 0; k < SCAN_E; k++) {
     const uint64_t i = base + k;
-    w[k] = (i > 0) ? ((nb8[k >> 2] >> (8 * (k & 3))) & 0xFFu) * pw[k] % HFP : 0u;
+    w[k] = (i > 0) ? hmod(((nb8[k >> 2] >> (8 * (k & 3))) & 0xFFu) * pw[k]) : 0u;   // (<= 255 x 16)
     tot += w[k];
   }
   uint32_t c = 0;
