@@ -360,10 +360,11 @@ def msm_host_devices_component(torch, hip, dev, n=1 << 22):
     """srs_eval_at_s's host-buffer call (plk_msm_g1, PCIe included) at 2^22 points on one device
     and split over several (plk_init_devices: per-device uploads from per-shard host threads, host
     sum of the partial logs).  On a one-GPU box the list repeats device 0 (the N-device code path,
-    one device's link); on a multi-GPU node it names every visible GPU."""
+    one device's link); on a multi-GPU node `all_devices` also names every visible GPU (measured in a
+    child process, tools/devices_probe.py, so that a multi-device failure cannot cost the line)."""
     import numpy as np
     ndev = torch.cuda.device_count()
-    lists = [[0], list(range(ndev))] if ndev > 1 else [[0], [0, 0], [0, 0, 0, 0]]
+    lists = [[0], [0, 0], [0, 0, 0, 0]]   # (distinct devices: a child process below)
     p, c = make_msm_sets(torch, n, 1, dev, 4242)
     ph, sh = p[0].cpu().numpy(), c[0].cpu().numpy()
     out = {"points": n, "note": "plk_msm_g1 wall time per call from host buffers; cached = same SRS pointer and "
@@ -396,6 +397,18 @@ def msm_host_devices_component(torch, hip, dev, n=1 << 22):
                                                          "same_result": bool(ok and got == want)}
     finally:
         hip.init_devices([0])
+    if ndev > 1:
+        # every visible GPU through plk_init_devices, in a child process with its own contexts and a
+        # time limit (a multi-device failure must not cost this line)
+        import subprocess
+        try:
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "devices_probe.py")], capture_output=True,
+                               text=True, timeout=240)
+            lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+            out["all_devices"] = json.loads(lines[-1]) if r.returncode == 0 and lines else {
+                "error": "exit %d: %s" % (r.returncode, r.stderr.strip()[-300:])}
+        except subprocess.TimeoutExpired:
+            out["all_devices"] = {"error": "timed out after 240 s"}
     return out
 
 
