@@ -50,8 +50,11 @@ def parse():
                     help="timed steps; a step is ONE batched launch of --msm-batch MSMs over distinct input sets")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log2n", type=int, default=22)
-    ap.add_argument("--msm-batch", type=int, default=40,
-                    help="MSMs per kernel launch (plk_msm_g1_batch_dev); every MSM is one step")
+    ap.add_argument("--msm-batch", type=int, default=160,
+                    help="MSMs per step = per kernel launch (plk_msm_g1_batch_dev).  160: at N = 8 (strong) a "
+                         "rank's share of a step is 160 x 2^19 points = 320 MiB (~55 us of streaming), so the "
+                         "timed region's fixed cost (~0.23 ms: first launch, finish, synchronize, the collective) "
+                         "stays a few %% of K = 20 steps; with 40 it was 11 %% even at N = 1")
     ap.add_argument("--rotate-mib", type=int, default=640)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -13,7 +13,7 @@ tail -1 $O/gpu_tests.log
 # the PMC pass first: bench.py reads roofline.traffic from profiles/msm_pmc_latest.json only when
 # it was measured for the current kernel source, so the bench lines below carry it
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/pmc -o run -- python3 bench.py --profile-only > $O/pmc.out 2>&1 || exit 1
-python3 tools/pmc_summary.py $O/pmc/run_results.db msm_dlog_kernel --latest 22 40 $O/msm_pmc_latest.json > $O/msm_pmc.json || exit 1
+python3 tools/pmc_summary.py $O/pmc/run_results.db msm_dlog_kernel --latest 22 160 $O/msm_pmc_latest.json > $O/msm_pmc.json || exit 1
 cp $O/msm_pmc_latest.json profiles/msm_pmc_latest.json
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail $O/bench.err; exit 1; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3 bench.py > $O/bench_traced.json 2> $O/bench_traced.err || exit 1
