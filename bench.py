@@ -696,10 +696,13 @@ def main():
         s0 = (W * B + j) % sets
         return pts[s0], sc[s0]
 
+    # the finish path once on zeroed records first: torch loads its elementwise kernels lazily
+    # (tens of ms on first use), which must not land in the timed region -- and not between the
+    # warmup steps and the timed ones either (an idle device drops its clocks: the first timed
+    # region ran ~0.13 ms slower, tools/timing_probe.py)
+    finish_sharded(ops.records_to_partials(res[:B]), n, ops, lambda j: (pts[j % sets], sc[j % sets]))
+    torch.cuda.synchronize()
     launch(0, max(W, 1) * B)                 # (records are re-armed by every launch)
-    # the finish path once on the warmup records: torch loads its elementwise kernels lazily
-    # (tens of ms on first use), which must not land in the timed region
-    finish_sharded(ops.records_to_partials(res[:max(W, 1) * B]), n, ops, lambda j: (pts[j % sets], sc[j % sets]))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
