@@ -639,6 +639,92 @@ def prove_component(torch, hip, dev, log2n, reps=5, preprocessed=False, barrier=
                     "(no 2^20-point domain in GF(17)), so parity at 2^20 is pinned through that restatement"}
 
 
+def prove_split_component(torch, hip, dev, dist, rank, world, gloo, log2n=20, reps=5):
+    """C5 strong-scaled over the ranks (round 3's independent poly_mul jobs spread
+    across GPUs as whole jobs).  Every rank holds the same proof inputs (gen.prove_instance, seed
+    51).  Rank 1 computes round 3's t_2 chain (A2 B2)(C2 z) and rank 2 the t_3 chain
+    (A3 B3)(C3 z(omega x)) (src/plonk.h:432-434, 471-473) -- at N = 2 rank 1 computes both --
+    with plk_prover_chains_dev and sends the product bytes to rank 0 (RCCL send / receive, 4 MiB
+    per chain at 2^20 gates); rank 0 runs everything else and reads them after the receive
+    (plk_prover_rounds_ext_dev).  Ranks >= 3 idle.  Timed: rank 0's wall time per proof, every
+    proof started on all ranks by one barrier; rank 0's single-GPU proof of the same instance is
+    timed beside it.  gloo (the one-GPU rehearsal): the bytes travel through host memory."""
+    n = 1 << log2n
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import gen
+    hpolys, chal, rnd, zh, pts = gen.prove_instance(n, 51, 2 * n + 8)
+    polys = [torch.from_numpy(p).to(dev) for p in hpolys]
+    pr = hip.Prover(n, zh, pts)
+    T2, T3 = hip.PLK_CHAIN_T2, hip.PLK_CHAIN_T3
+    assign = {1: T2 | T3} if world == 2 else {1: T2, 2: T3}
+    bufs = {c: torch.zeros(pr.chain_bytes(c), dtype=torch.uint8, device=dev) for c in (T2, T3)}
+    st = torch.cuda.current_stream()
+
+    def once():
+        if rank == 0:
+            reqs, host = [], []
+            for r, m in sorted(assign.items()):
+                for c in (T2, T3):
+                    if m & c:
+                        if gloo:
+                            h = torch.empty(bufs[c].numel(), dtype=torch.uint8)
+                            dist.recv(h, src=r)
+                            host.append((c, h))
+                        else:
+                            reqs.append(dist.irecv(bufs[c], src=r))
+            for q in reqs:
+                q.wait()                     # (RCCL: the current stream waits for the receive)
+            for c, h in host:
+                bufs[c].copy_(h)
+            return pr.rounds_ext_dev(polys, chal, rnd, T2 | T3, bufs[T2], bufs[T3], ready=st)
+        m = assign.get(rank, 0)
+        if m:
+            pr.chains_dev(polys, chal, rnd, m, bufs[T2] if m & T2 else None, bufs[T3] if m & T3 else None, done=st)
+            for c in (T2, T3):
+                if m & c:
+                    if gloo:
+                        dist.send(bufs[c].cpu(), dst=0)
+                    else:
+                        dist.send(bufs[c], dst=0)
+            torch.cuda.synchronize()
+        return None
+
+    single = None
+    if rank == 0:
+        first = pr.rounds_dev(polys, chal, rnd)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            pr.rounds_dev(polys, chal, rnd)
+            ts.append(time.perf_counter() - t0)
+        single = min(ts)
+    dist.barrier()
+    out = once()                             # (the first send / receive sets up the peer channel)
+    torch.cuda.synchronize()
+    t, outs = [], []
+    for _ in range(reps):
+        dist.barrier()
+        t0 = time.perf_counter()
+        o = once()
+        if rank == 0:
+            t.append(time.perf_counter() - t0)
+            outs.append(o)
+    dist.barrier()
+    pr.close()
+    if rank != 0:
+        return None
+    t.sort()
+    return {"gpus": min(world, 3), "ms": round(t[0] * 1e3, 3), "median_ms": round(t[len(t) // 2] * 1e3, 3),
+            "single_gpu_ms": round(single * 1e3, 3), "speedup": round(single / t[0], 3),
+            "matches_oracle": _prove_golden(n, out), "same_as_single_gpu": all(o == first for o in [out] + outs),
+            "transport": "gloo through host memory (one-GPU rehearsal)" if gloo else "RCCL send / receive",
+            "note": "one 2^20-gate proof strong-scaled: rank 1 computes round 3's t_2 chain (A2 B2)(C2 z) and rank "
+                    "2 the t_3 chain (A3 B3)(C3 z(omega x)) (N = 2: rank 1 both) from the same inputs, "
+                    "plk_prover_chains_dev, and sends the 4 MiB products to rank 0, which runs the rest "
+                    "(plk_prover_rounds_ext_dev); ms = rank 0's wall time per proof, all ranks released by one "
+                    "barrier; single_gpu_ms = rank 0 alone on the same instance"}
+
+
 def main():
     args = parse()
     import torch
@@ -846,6 +932,10 @@ def main():
                 "note": "one independent 2^20-gate proof per GPU, all ranks released by one barrier and timing "
                         "concurrently, no exchange; ms = the slowest rank's best call; matches_oracle: every rank's "
                         "34 bytes equal the recorded answer of the CPU restatement (tests/golden/prove_2_20.json)"}
+        # C5 strong-scaled: one proof over up to 3 GPUs (round 3's two product chains on ranks 1, 2)
+        sp = prove_split_component(torch, hip, dev, dist, rank, world, backend != "nccl")
+        if rank == 0:
+            comp["prove_2^20_gates_split"] = sp
     if rank == 0 and comps:
         comp.update(components(torch, hip, dev, st, comps - ({"prove"} if world > 1 else set())))
         if "msm" in comps:

@@ -278,6 +278,28 @@ int plk_prover_rounds_dev(plk_prover_t *p, const uint8_t *const d_polys[13], con
 #define PLK_PROVE_PREPROCESSED 2
 int plk_prover_preprocess(plk_prover_t *p, const uint8_t *const d_polys[13]);
 
+/* Strong-scaled proof over several GPUs (round 3's independent poly_mul jobs spread
+ * across GPUs as whole jobs).  Two of round 3's product chains depend only on the proof's inputs:
+ *   PLK_CHAIN_T2: t_2 = (A2 B2)(C2 z_x)            (src/plonk.h:432-434, re-associated)
+ *   PLK_CHAIN_T3: t_3 = (A3 B3)(C3 z_x(omega x))   (src/plonk.h:471-473)
+ * A helper GPU computes them from the same inputs as the proving GPU with plk_prover_chains_dev;
+ * their bytes travel to the proving GPU (e.g. an RCCL send / receive), whose
+ * plk_prover_rounds_ext_dev skips those chains and reads the bytes instead.  The proof bytes are
+ * identical to plk_prover_rounds_dev's.  Buffers: plk_prover_chain_bytes(p, chain) bytes each,
+ * 16-byte aligned, device memory of the prover's GPU. */
+#define PLK_CHAIN_T2 1
+#define PLK_CHAIN_T3 2
+size_t plk_prover_chain_bytes(const plk_prover_t *p, int chain);
+/* Enqueue rounds 1-3's preparation and the chains in `which` on the prover's stream, products
+ * into d_t2 / d_t3; the stream `done` (NULL: none) waits for them.  Returns without waiting. */
+int plk_prover_chains_dev(plk_prover_t *p, const uint8_t *const d_polys[13], const uint8_t chal[5],
+                          const uint8_t rand9[9], int which, uint8_t *d_t2, uint8_t *d_t3, void *done);
+/* plk_prover_rounds_dev with the chains in `which` read from d_t2 / d_t3, after everything
+ * enqueued on stream `ready` (NULL: nothing) at the time of the call -- e.g. their receive. */
+int plk_prover_rounds_ext_dev(plk_prover_t *p, const uint8_t *const d_polys[13], const uint8_t chal[5],
+                              const uint8_t rand9[9], int flags, int which, const uint8_t *d_t2,
+                              const uint8_t *d_t3, void *ready, uint8_t proof[34]);
+
 #ifdef __cplusplus
 }
 #endif

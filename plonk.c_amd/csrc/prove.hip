@@ -1150,6 +1150,7 @@ struct plk_prover {
   void* work = nullptr;
   size_t work_bytes = 0;
   hipStream_t st = nullptr;
+  hipEvent_t ev = nullptr;         // cross-stream hand-offs of the strong-scaled proof entry points
   // mapped pinned host memory: 64 proof bytes + NSTAT status words (trim_pack_kernel)
   uint8_t* h_res = nullptr;
   uint8_t* d_res_host = nullptr;   // its device address
@@ -1486,6 +1487,7 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   P->work_bytes = ws;
   P->st = nullptr;
   hipError_t e = hipStreamCreateWithFlags(&P->st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMemsetAsync(P->mem, 0, P->mem_bytes, P->st);
   if (e == hipSuccess) e = hipMemcpyAsync(P->d_srs, d->srs_g1, 3 * P->srs_len, hipMemcpyHostToDevice, P->st);
   if (e == hipSuccess) e = hipMemcpyAsync(P->d_zh, d->z_h, zl, hipMemcpyHostToDevice, P->st);
@@ -1527,6 +1529,7 @@ void plk_prover_destroy(plk_prover_t* P) {
   (void)hipFree(P->mem);
   if (P->h_res) (void)hipHostFree(P->h_res);
   (void)hipFree(P->fix_mem);
+  if (P->ev) (void)hipEventDestroy(P->ev);
   if (P->st) (void)hipStreamDestroy(P->st);
   delete P;
   plk_ctx_release();
@@ -1540,7 +1543,19 @@ namespace {
 
 // rounds 1-5 (src/plonk.h:277-655) on polys[13] = f_a f_b f_c q_o q_m q_l q_r q_c s1 s2 s3 acc_x l_1_x
 // (each of length <= n, zero padded to n).  Enqueued on P->st; status words in P->d_stat.
-int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const uint8_t rnd[9], bool pre = false) {
+// Strong-scaled proofs (several GPUs, plk_prover_chains_dev / plk_prover_rounds_ext_dev): the
+// round-3 chains t_2 = (A2 B2)(C2 z) and t_3 = (A3 B3)(C3 z(omega x)) depend only on the proof's
+// inputs, so another GPU can compute them from the same inputs while this one runs the rest.
+struct RoundsMode {
+  int ext = 0;                          // chains (PLK_CHAIN_*) whose products come from t2 / t3
+  const uint8_t *t2 = nullptr, *t3 = nullptr;
+  hipEvent_t ready = nullptr;           // the stream waits for it before reading t2 / t3
+  int only = 0;                         // helper: just these chains (into o2 / o3), then return
+  uint8_t *o2 = nullptr, *o3 = nullptr;
+};
+
+int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const uint8_t rnd[9], bool pre = false,
+           const RoundsMode& md = RoundsMode{}) {
   const uint64_t n = P->n;
   const Lens L = lens_for(n, P->zh_len);
   const uint8_t *FA = pl[0], *FB = pl[1], *FC = pl[2], *QO = pl[3], *QM = pl[4], *QL = pl[5], *QR = pl[6],
@@ -1620,54 +1635,78 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
         make_lc({{cZ, L.lzx}}, {S_ONE}, S_NEG1, -1, S_ALPHA2, -1, P->Z1, L.lz1)}));  // alpha^2 (z - 1)
   }
   {
+    // Chains: 1 = t_2's (A2 B2, C2 z -> T2), 2 = t_3's (A3 B3, C3 z(omega x) -> T3).  `local`: the
+    // chains this call computes itself; a helper call computes only md.only.
+    const int local = md.only ? md.only : (PLK_CHAIN_T2 | PLK_CHAIN_T3) & ~md.ext;
     // a_x q_l + b_x q_r + c_x q_o as ONE sum group (one inverse transform) when the sum fits
     // F29's centered range: 3 * 64 n <= (p - 1) / 2 (n <= 1,223,338)
     const int lin = plk_poly_mul_summable(L.la, n) && (uint64_t)3 * L.la * 128 < f29::P ? 1 : 0;
     P->lin_sum = lin;
-    // (order: the center launch's blocks 0-255 take the even jobs and 256-511 the odd ones; with
-    // a_x, b_x, z_x transformed once for their two products each, both halves carry 12 of the
-    // batch's 24 tile passes; with the preprocessed circuit 13 / 12 of 25)
-    PlkPolyMulJob g1[] = {{cA, L.la, QL, n, P->AQL},          {cB, L.la, QR, n, P->BQR, lin},
-                          {cC, L.la, QO, n, P->CQO, lin},      {P->Z1, L.lz1, L1, n, P->T4},
-                          {cA, L.la, cB, L.la, P->AB},
-                          // the 17th poly_mul, z_x s_sigma_3 (src/plonk.h:560), as z_x * s3:
-                          // its scalar beta z_omega_z (a round-4 value) moves into r(x)'s
-                          // lincomb (S_R3B), so the product joins this batch
-                          {cZ, L.lzx, S3, n, P->P3},
-                          // t_2 = ((A2 B2) C2) z and t_3 = ((A3 B3) C3) z(omega x)
-                          // (src/plonk.h:432-434, 471-473) re-associated as (A2 B2)(C2 z):
-                          // C2 z and C3 z(omega x) join this batch and the 4n products
-                          // come in one batch (associativity over GF(17); the centered F29
-                          // residues hold the 2n x 2n products exactly)
-                          {P->A2, L.la, P->B2, L.la, P->T2a}, {P->C2, L.la, cZ, L.lzx, P->T2b},
-                          {P->A3, L.la, P->B3, L.la, P->T3a}, {P->C3, L.la, P->ZW, L.lzw, P->T3b}};
-    // (a b) q_m ADDED into t_2 = (A2 B2)(C2 z) when their sum fits F29's centered range,
-    // 64 (min(l2a, la + lzx - 1) + min(lab, n)) <= (p - 1) / 2 (n <= ~1.2 M): one 4n inverse
-    // transform fewer, one numerator term fewer (t_3 enters with -1, so it stays apart)
+    // (order: the center launch balances the jobs over its two block halves by pass units,
+    // center_schedule; a_x, b_x, z_x are transformed once for their two products each)
+    // fixed: the d_polys index of a job's b operand when it is a preprocessed circuit polynomial
+    struct J {
+      PlkPolyMulJob j;
+      int fixed;
+    };
+    std::vector<J> g1, g2;
+    if (!md.only) {
+      g1.push_back({{cA, L.la, QL, n, P->AQL}, 5});
+      g1.push_back({{cB, L.la, QR, n, P->BQR, lin}, 6});
+      g1.push_back({{cC, L.la, QO, n, P->CQO, lin}, 3});
+      g1.push_back({{P->Z1, L.lz1, L1, n, P->T4}, 12});
+      g1.push_back({{cA, L.la, cB, L.la, P->AB}, -1});
+      // the 17th poly_mul, z_x s_sigma_3 (src/plonk.h:560), as z_x * s3: its scalar beta
+      // z_omega_z (a round-4 value) moves into r(x)'s lincomb (S_R3B), so the product joins this batch
+      g1.push_back({{cZ, L.lzx, S3, n, P->P3}, 10});
+    }
+    // t_2 = ((A2 B2) C2) z and t_3 = ((A3 B3) C3) z(omega x) (src/plonk.h:432-434, 471-473)
+    // re-associated as (A2 B2)(C2 z): C2 z and C3 z(omega x) join this batch and the 4n products
+    // come in one batch (associativity over GF(17); the centered F29 residues hold the 2n x 2n
+    // products exactly)
+    if (local & PLK_CHAIN_T2) {
+      g1.push_back({{P->A2, L.la, P->B2, L.la, P->T2a}, -1});
+      g1.push_back({{P->C2, L.la, cZ, L.lzx, P->T2b}, -1});
+    }
+    if (local & PLK_CHAIN_T3) {
+      g1.push_back({{P->A3, L.la, P->B3, L.la, P->T3a}, -1});
+      g1.push_back({{P->C3, L.la, P->ZW, L.lzw, P->T3b}, -1});
+    }
+    // (a b) q_m ADDED into t_2 = (A2 B2)(C2 z) when both run here and their sum fits F29's
+    // centered range, 64 (min(l2a, la + lzx - 1) + min(lab, n)) <= (p - 1) / 2 (n <= ~1.2 M): one
+    // 4n inverse transform fewer, one numerator term fewer (t_3 enters with -1, so it stays apart)
     const uint64_t t2b = L.la + L.lzx - 1;
-    const int grp = plk_poly_mul_summable(L.lab, n) && plk_poly_mul_summable(L.l2a, t2b) &&
+    const int grp = !md.only && (local & PLK_CHAIN_T2) && plk_poly_mul_summable(L.lab, n) &&
+                            plk_poly_mul_summable(L.l2a, t2b) &&
                             (std::min(L.l2a, t2b) + std::min<uint64_t>(L.lab, n)) * 128 < f29::P
                         ? 1
                         : 0;
     P->t2_sum = grp;
-    PlkPolyMulJob g2[] = {{P->T2a, L.l2a, P->T2b, t2b, P->T2},
-                          {P->AB, L.lab, QM, n, P->ABQM, grp},
-                          {P->T3a, L.l2a, P->T3b, L.la + L.lzw - 1, P->T3}};
+    if (local & PLK_CHAIN_T2) g2.push_back({{P->T2a, L.l2a, P->T2b, t2b, md.only ? md.o2 : P->T2}, -1});
+    if (!md.only) g2.push_back({{P->AB, L.lab, QM, n, P->ABQM, grp}, 4});
+    if (local & PLK_CHAIN_T3) g2.push_back({{P->T3a, L.l2a, P->T3b, L.la + L.lzw - 1, md.only ? md.o3 : P->T3}, -1});
     if (pre) {   // preprocessed circuit: the fixed b operands' transforms (plk_prover_preprocess)
-      PlkPolyMulJob* const js[] = {&g1[0], &g1[1], &g1[2], &g1[3], &g1[5], &g2[1]};
-      const int which[] = {5, 6, 3, 12, 10, 4};   // q_l q_r q_o l_1_x s_sigma_3 q_m
-      for (int i = 0; i < 6; i++) {
-        const plk_prover::Fixed& f = P->fix[which[i]];
-        if (f.t && f.src == pl[which[i]] && js[i]->b == pl[which[i]]) {
-          js[i]->bt = f.t;
-          js[i]->bt_k = f.k;
-          js[i]->bt_field = f.field;
+      for (auto* g : {&g1, &g2})
+        for (J& x : *g) {
+          if (x.fixed < 0) continue;
+          const plk_prover::Fixed& f = P->fix[x.fixed];
+          if (f.t && f.src == pl[x.fixed] && x.j.b == pl[x.fixed]) {
+            x.j.bt = f.t;
+            x.j.bt_k = f.k;
+            x.j.bt_field = f.field;
+          }
         }
-      }
     }
-    RC(plk_poly_mul_batch_launch(g1, 10, P->work, P->work_bytes, P->st));
-    RC(plk_poly_mul_batch_launch(g2, 3, P->work, P->work_bytes, P->st));
+    for (auto* g : {&g1, &g2}) {
+      std::vector<PlkPolyMulJob> jobs;
+      for (const J& x : *g) jobs.push_back(x.j);
+      if (!jobs.empty()) RC(plk_poly_mul_batch_launch(jobs.data(), (int)jobs.size(), P->work, P->work_bytes, P->st));
+    }
+    if (md.only) return PLK_OK;   // helper: the chains' products are enqueued
   }
+  const uint8_t* const T2 = (md.ext & PLK_CHAIN_T2) ? md.t2 : P->T2;
+  const uint8_t* const T3 = (md.ext & PLK_CHAIN_T3) ? md.t3 : P->T3;
+  if (md.ext && md.ready) PLK_HIP(hipStreamWaitEvent(P->st, md.ready, 0));   // their bytes have arrived
   // t(x) = numerator / Z_H; t_lo / t_mid / t_hi = poly_slice(t_x, ...) with part n + 2
   // (src/plonk.h:494-519)
   const uint64_t part = n + 2;
@@ -1675,10 +1714,10 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   const uint64_t lhi = L.ltx > 2 * part ? L.ltx - 2 * part : 0;
   // (the sums in AQL / T2 stand for their members' terms)
   LcArgs num = P->lin_sum
-                   ? make_lc({{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {QC, n}, {P->T2, L.l2}, {P->T3, L.l3}, {P->T4, L.lt4}},
+                   ? make_lc({{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {QC, n}, {T2, L.l2}, {T3, L.l3}, {P->T4, L.lt4}},
                              {S_ONE, S_ONE, S_ONE, S_ONE, S_NEG1, S_ONE}, -1, -1, S_ONE, -1, P->NUM, L.lnum)
                    : make_lc({{P->ABQM, L.labqm}, {P->AQL, L.lq1}, {P->BQR, L.lq1}, {P->CQO, L.lq1}, {QC, n},
-                              {P->T2, L.l2}, {P->T3, L.l3}, {P->T4, L.lt4}},
+                              {T2, L.l2}, {T3, L.l3}, {P->T4, L.lt4}},
                              {S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_ONE, S_NEG1, S_ONE}, -1, -1, S_ONE, -1, P->NUM,
                              L.lnum);
   if (P->t2_sum) {   // drop the ABQM term (first)
@@ -1845,6 +1884,67 @@ int plk_prover_rounds_dev(plk_prover_t* P, const uint8_t* const d_polys[13], con
   for (int i = 0; i < 13; i++)
     if (!d_polys[i]) { plk_set_error("plk_prover_rounds_dev: polynomial %d is NULL", i); return PLK_ERR_ARG; }
   int rc = rounds(P, d_polys, chal, rand9, (flags & PLK_PROVE_PREPROCESSED) != 0);
+  if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
+  return finish(P, (flags & PLK_PROVE_STRICT) != 0, 0, proof);
+}
+
+size_t plk_prover_chain_bytes(const plk_prover_t* P, int which) {
+  if (!P || (which != PLK_CHAIN_T2 && which != PLK_CHAIN_T3)) return 0;
+  const Lens L = lens_for(P->n, P->zh_len);
+  return (size_t)(which == PLK_CHAIN_T2 ? L.l2 : L.l3) + 64;   // (the numerator reads whole dwords)
+}
+
+namespace {
+int check_chain_args(const char* fn, const plk_prover_t* P, const uint8_t* const* d_polys, const uint8_t* chal,
+                     const uint8_t* rand9, int which, const void* t2, const void* t3) {
+  if (!P || !d_polys || !chal || !rand9) { plk_set_error("%s: NULL argument", fn); return PLK_ERR_ARG; }
+  for (int i = 0; i < 13; i++)
+    if (!d_polys[i]) { plk_set_error("%s: polynomial %d is NULL", fn, i); return PLK_ERR_ARG; }
+  if (which & ~(PLK_CHAIN_T2 | PLK_CHAIN_T3)) { plk_set_error("%s: bad chain mask %d", fn, which); return PLK_ERR_ARG; }
+  if (((which & PLK_CHAIN_T2) && !t2) || ((which & PLK_CHAIN_T3) && !t3)) {
+    plk_set_error("%s: NULL chain buffer", fn);
+    return PLK_ERR_ARG;
+  }
+  if (((uintptr_t)t2 | (uintptr_t)t3) % 16) { plk_set_error("%s: chain buffers must be 16-byte aligned", fn); return PLK_ERR_ARG; }
+  return PLK_OK;
+}
+// records an event on `from` and makes `to` wait for it (cross-stream, same device)
+int stream_after(hipStream_t to, hipStream_t from, hipEvent_t ev) {
+  PLK_HIP(hipEventRecord(ev, from));
+  PLK_HIP(hipStreamWaitEvent(to, ev, 0));
+  return PLK_OK;
+}
+}  // namespace
+
+int plk_prover_chains_dev(plk_prover_t* P, const uint8_t* const d_polys[13], const uint8_t chal[5],
+                          const uint8_t rand9[9], int which, uint8_t* d_t2, uint8_t* d_t3, void* done) {
+  int rc = check_chain_args("plk_prover_chains_dev", P, d_polys, chal, rand9, which, d_t2, d_t3);
+  if (rc) return rc;
+  if (!which) return PLK_OK;
+  RoundsMode md;
+  md.only = which;
+  md.o2 = d_t2;
+  md.o3 = d_t3;
+  rc = rounds(P, d_polys, chal, rand9, false, md);
+  if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
+  if (done) return stream_after((hipStream_t)done, P->st, P->ev);
+  return PLK_OK;
+}
+
+int plk_prover_rounds_ext_dev(plk_prover_t* P, const uint8_t* const d_polys[13], const uint8_t chal[5],
+                              const uint8_t rand9[9], int flags, int which, const uint8_t* d_t2, const uint8_t* d_t3,
+                              void* ready, uint8_t proof[34]) {
+  int rc = check_chain_args("plk_prover_rounds_ext_dev", P, d_polys, chal, rand9, which, d_t2, d_t3);
+  if (rc) return rc;
+  RoundsMode md;
+  md.ext = which;
+  md.t2 = d_t2;
+  md.t3 = d_t3;
+  if (which && ready) {   // everything enqueued on `ready` so far (the bytes' arrival) before they are read
+    PLK_HIP(hipEventRecord(P->ev, (hipStream_t)ready));
+    md.ready = P->ev;
+  }
+  rc = rounds(P, d_polys, chal, rand9, (flags & PLK_PROVE_PREPROCESSED) != 0, md);
   if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
   return finish(P, (flags & PLK_PROVE_STRICT) != 0, 0, proof);
 }

@@ -69,6 +69,10 @@ SIGNATURES = {
     "plk_prover_prove": (C.c_int, [_vp, _vp, _u8p, _u8p, _u8p]),
     "plk_prover_rounds_dev": (C.c_int, [_vp, C.POINTER(_vp), _u8p, _u8p, C.c_int, _u8p]),
     "plk_prover_preprocess": (C.c_int, [_vp, C.POINTER(_vp)]),
+    "plk_prover_chain_bytes": (_sz, [_vp, C.c_int]),
+    "plk_prover_chains_dev": (C.c_int, [_vp, C.POINTER(_vp), _u8p, _u8p, C.c_int, _vp, _vp, _vp]),
+    "plk_prover_rounds_ext_dev": (C.c_int, [_vp, C.POINTER(_vp), _u8p, _u8p, C.c_int, C.c_int, _vp, _vp, _vp,
+                                            _u8p]),
     "plk_set_option": (C.c_int, [C.c_int, C.c_int64]),
     "plk_init_devices": (C.c_int, [C.POINTER(C.c_int), C.c_int]),
     "plk_devices": (C.c_int, [C.POINTER(C.c_int), C.c_int]),
@@ -83,6 +87,8 @@ OPTIONS = {"TINY_CALLS": 1, "PROVE_SYNC": 2, "POLY_BLOCK_L": 3, "POLY_BLOCK_S": 
 
 PLK_PROVE_STRICT = 1
 PLK_PROVE_PREPROCESSED = 2
+PLK_CHAIN_T2 = 1   # t_2 = (A2 B2)(C2 z_x), src/plonk.h:432-434
+PLK_CHAIN_T3 = 2   # t_3 = (A3 B3)(C3 z_x(omega x)), src/plonk.h:471-473
 
 
 class PlonkDesc(C.Structure):
@@ -482,11 +488,8 @@ class Prover:
         _check("plk_prover_prove", lib().plk_prover_prove(self._h, C.byref(cir), _p(ch), _p(rd), _p(out)))
         return bytes(out)
 
-    def rounds_dev(self, polys, chal, rand, strict=False, preprocessed=False):
-        """polys: 13 device tensors / pointers (n bytes each).  preprocessed: use the fixed
-        polynomials' transforms from `preprocess` (same addresses, unchanged bytes).  The ctypes
-        argument blocks are cached by value (a 2^20-gate proof is ~0.5 ms: building them anew
-        each call was ~5 % of it)."""
+    def _args(self, polys, chal, rand):
+        """ctypes argument blocks of (polys, chal, rand), cached by value"""
         cache = self.__dict__.setdefault("_argcache", {})
         ch, rd = _u8(chal).reshape(-1), _u8(rand).reshape(-1)
         if ch.size != 5 or rd.size != 9:
@@ -501,9 +504,43 @@ class Prover:
             args = ((_vp * 13)(*key[0]), (C.c_uint8 * 5).from_buffer_copy(key[1]),
                     (C.c_uint8 * 9).from_buffer_copy(key[2]))
             cache[key] = args
+        return args
+
+    def rounds_dev(self, polys, chal, rand, strict=False, preprocessed=False):
+        """polys: 13 device tensors / pointers (n bytes each).  preprocessed: use the fixed
+        polynomials' transforms from `preprocess` (same addresses, unchanged bytes).  The ctypes
+        argument blocks are cached by value (a 2^20-gate proof is ~0.5 ms: building them anew
+        each call was ~5 % of it)."""
+        args = self._args(polys, chal, rand)
         out = self.__dict__.setdefault("_out", (C.c_uint8 * 34)())
         flags = (PLK_PROVE_STRICT if strict else 0) | (PLK_PROVE_PREPROCESSED if preprocessed else 0)
         _check("plk_prover_rounds_dev", lib().plk_prover_rounds_dev(self._h, args[0], args[1], args[2], flags, out))
+        return bytes(out)
+
+    # ---- strong-scaled proof (plk_prover_chains_dev / plk_prover_rounds_ext_dev)
+    def chain_bytes(self, chain):
+        """buffer size for one chain's product (PLK_CHAIN_T2 or PLK_CHAIN_T3)"""
+        return int(lib().plk_prover_chain_bytes(self._h, int(chain)))
+
+    def chains_dev(self, polys, chal, rand, which, t2=None, t3=None, done=None):
+        """Helper GPU: enqueue the preparation and the chains in `which` (PLK_CHAIN_* mask) into
+        the device buffers t2 / t3 (chain_bytes each); stream `done` waits for them."""
+        args = self._args(polys, chal, rand)
+        _check("plk_prover_chains_dev", lib().plk_prover_chains_dev(
+            self._h, args[0], args[1], args[2], int(which), _ptr(t2) if t2 is not None else None,
+            _ptr(t3) if t3 is not None else None, _stream(done) if done is not None else None))
+
+    def rounds_ext_dev(self, polys, chal, rand, which, t2=None, t3=None, ready=None, strict=False,
+                       preprocessed=False):
+        """rounds_dev with the chains in `which` read from t2 / t3 (computed by chains_dev on
+        another GPU from the same inputs) once everything enqueued on stream `ready` so far has
+        run.  Same 34 bytes as rounds_dev."""
+        args = self._args(polys, chal, rand)
+        out = (C.c_uint8 * 34)()
+        flags = (PLK_PROVE_STRICT if strict else 0) | (PLK_PROVE_PREPROCESSED if preprocessed else 0)
+        _check("plk_prover_rounds_ext_dev", lib().plk_prover_rounds_ext_dev(
+            self._h, args[0], args[1], args[2], flags, int(which), _ptr(t2) if t2 is not None else None,
+            _ptr(t3) if t3 is not None else None, _stream(ready) if ready is not None else None, out))
         return bytes(out)
 
     def preprocess(self, polys):

@@ -3,7 +3,8 @@ RCCL) rehearsed on the one GPU of a test box: two ranks over gloo sharing cuda:0
 (each 2^22-point MSM split by point range, plonkhip.dist.finish_sharded).  The line must carry the
 strong-scaling config and both correctness checks -- the first MSM against a single-GPU recompute
 and the reference's own 2^22-point golden through the sharded path -- plus C5's replica leg (one
-2^20-gate proof per rank, released together by a barrier, every rank's bytes checked) and the
+2^20-gate proof per rank, released together by a barrier, every rank's bytes checked), C5
+strong-scaled (round 3's t_2 / t_3 chains on ranks 1 / 2, their bytes sent to rank 0) and the
 MSM components named by the points a rank actually reads (2^21 per shard here)."""
 import json
 import os
@@ -36,7 +37,27 @@ def test_two_rank_strong_scaling_line():
     rep = c["prove_2^20_gates_replicas"]
     assert rep["gpus"] == 2 and rep["matches_oracle_all_ranks"] is True and rep["deterministic_all_ranks"] is True
     assert rep["ms_slowest_rank"] > 0
+    sp = c["prove_2^20_gates_split"]
+    assert sp["gpus"] == 2 and sp["matches_oracle"] is True and sp["same_as_single_gpu"] is True and sp["ms"] > 0
     # a shard is 2^21 points: no key may claim 2^22 for it
     assert "msm_2^21_one_per_launch" in c and "msm_2^21_8_per_launch" in c
     assert not any(k.startswith("msm_2^22") for k in c)
     assert "prove_2^20_gates" not in c            # the single-GPU C5 line is not repeated at N > 1
+
+
+def test_three_rank_split_proof():
+    """C5 strong-scaled over three ranks: rank 1 computes the t_2 chain, rank 2 the t_3 chain, rank
+    0 the rest; the proof equals the single-GPU proof and the recorded answer."""
+    env = dict(os.environ, PLK_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+           "--master-addr", "127.0.0.1", "--master-port", "29563", os.path.join(ROOT, "bench.py"),
+           "--gpus", "3", "--steps", "2", "--warmup", "1", "--msm-batch", "4", "--rotate-mib", "96",
+           "--components", "prove", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    sp = d["components"]["prove_2^20_gates_split"]
+    assert sp["gpus"] == 3 and sp["matches_oracle"] is True and sp["same_as_single_gpu"] is True
+    assert d["components"]["prove_2^20_gates_replicas"]["matches_oracle_all_ranks"] is True

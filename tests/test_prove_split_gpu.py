@@ -1,0 +1,82 @@
+"""Strong-scaled proof entry points (plk_prover_chains_dev / plk_prover_rounds_ext_dev, SURVEY §8e:
+round 3's product chains t_2 = (A2 B2)(C2 z) and t_3 = (A3 B3)(C3 z(omega x)),
+src/plonk.h:432-434, 471-473, computed by another prover from the same inputs).  Rehearsed on one
+GPU: the helper provers run on their own streams of the same device, and the proving call reads
+their products after an event on the helper's stream -- the same hand-off the multi-GPU bench leg
+makes over RCCL.  The proof bytes must equal the single-prover proof and, at n = 2^20, the
+recorded answer of the CPU restatement (tests/golden/prove_2_20.json)."""
+import pytest
+import torch
+
+import gen
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _split_proof(hip, n, polys, chal, rnd, zh, pts, which, helpers=1, preprocessed=False):
+    """which: chain mask the helpers compute; helpers = 1 (one prover for every chain in `which`)
+    or 2 (one prover per chain)"""
+    main = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    if preprocessed:
+        main.preprocess(dev)
+    t2 = torch.zeros(main.chain_bytes(hip.PLK_CHAIN_T2), dtype=torch.uint8, device="cuda")
+    t3 = torch.zeros(main.chain_bytes(hip.PLK_CHAIN_T3), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.Stream()
+    masks = [which] if helpers == 1 else [m for m in (hip.PLK_CHAIN_T2, hip.PLK_CHAIN_T3) if which & m]
+    hs = [hip.Prover(n, zh, pts) for _ in masks]
+    for h, m in zip(hs, masks):
+        h.chains_dev(dev, chal, rnd, m, t2 if m & hip.PLK_CHAIN_T2 else None, t3 if m & hip.PLK_CHAIN_T3 else None,
+                     done=st)
+    got = main.rounds_ext_dev(dev, chal, rnd, which, t2 if which & hip.PLK_CHAIN_T2 else None,
+                              t3 if which & hip.PLK_CHAIN_T3 else None, ready=st, preprocessed=preprocessed)
+    want = main.rounds_dev(dev, chal, rnd)
+    for h in hs:
+        h.close()
+    main.close()
+    return got, want
+
+
+@pytest.mark.parametrize("which,helpers", [(1, 1), (2, 1), (3, 1), (3, 2)])
+def test_split_matches_single_prover(hip, which, helpers):
+    n = 1 << 16
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, 41, 2 * n + 8)
+    got, want = _split_proof(hip, n, polys, chal, rnd, zh, pts, which, helpers)
+    assert got.hex() == want.hex()
+
+
+@pytest.mark.parametrize("n,seed", [(1 << 12, 7), (64, 3)])
+def test_split_small_sizes(hip, n, seed):
+    """12-bit tiles and products below the transform engine (direct / small kernels)"""
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, seed, 2 * n + 8)
+    got, want = _split_proof(hip, n, polys, chal, rnd, zh, pts, 3, 2)
+    assert got.hex() == want.hex()
+
+
+def test_split_2_20_vs_golden(hip):
+    """Config C5: both chains on helper provers, plain and preprocessed main prover"""
+    g = load_golden("prove_2_20.json")
+    n = g["n"]
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, g["seed"], g["srs_len"])
+    got, want = _split_proof(hip, n, polys, chal, rnd, zh, pts, 3, 2)
+    assert got.hex() == want.hex() == g["proof"]
+    got, _ = _split_proof(hip, n, polys, chal, rnd, zh, pts, 3, 1, preprocessed=True)
+    assert got.hex() == g["proof"]
+
+
+def test_split_argument_errors(hip):
+    n = 1 << 10
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, 5, 2 * n + 8)
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    assert pr.chain_bytes(hip.PLK_CHAIN_T2) > 6 * n and pr.chain_bytes(hip.PLK_CHAIN_T3) > 6 * n
+    assert pr.chain_bytes(4) == 0
+    with pytest.raises(hip.PlonkHipError):
+        pr.chains_dev(dev, chal, rnd, hip.PLK_CHAIN_T2, None, None)        # no buffer for the chain
+    with pytest.raises(hip.PlonkHipError):
+        pr.rounds_ext_dev(dev, chal, rnd, 4)                               # bad mask
+    buf = torch.zeros(pr.chain_bytes(hip.PLK_CHAIN_T3) + 16, dtype=torch.uint8, device="cuda")
+    with pytest.raises(hip.PlonkHipError):
+        pr.rounds_ext_dev(dev, chal, rnd, hip.PLK_CHAIN_T3, None, buf[1:])  # misaligned
+    pr.close()
