@@ -291,11 +291,13 @@ int plk_prover_preprocess(plk_prover_t *p, const uint8_t *const d_polys[13]);
 #define PLK_CHAIN_T3 2
 size_t plk_prover_chain_bytes(const plk_prover_t *p, int chain);
 /* Enqueue rounds 1-3's preparation and the chains in `which` on the prover's stream, products
- * into d_t2 / d_t3; the stream `done` (NULL: none) waits for them.  Returns without waiting. */
+ * into d_t2 / d_t3; the stream `done` (NULL: the null stream) waits for them.  Returns without
+ * waiting. */
 int plk_prover_chains_dev(plk_prover_t *p, const uint8_t *const d_polys[13], const uint8_t chal[5],
                           const uint8_t rand9[9], int which, uint8_t *d_t2, uint8_t *d_t3, void *done);
 /* plk_prover_rounds_dev with the chains in `which` read from d_t2 / d_t3, after everything
- * enqueued on stream `ready` (NULL: nothing) at the time of the call -- e.g. their receive. */
+ * enqueued on stream `ready` (NULL: the null stream) at the time of the call -- e.g. their
+ * receive. */
 int plk_prover_rounds_ext_dev(plk_prover_t *p, const uint8_t *const d_polys[13], const uint8_t chal[5],
                               const uint8_t rand9[9], int flags, int which, const uint8_t *d_t2,
                               const uint8_t *d_t3, void *ready, uint8_t proof[34]);

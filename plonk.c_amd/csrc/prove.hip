@@ -1927,8 +1927,7 @@ int plk_prover_chains_dev(plk_prover_t* P, const uint8_t* const d_polys[13], con
   md.o3 = d_t3;
   rc = rounds(P, d_polys, chal, rand9, false, md);
   if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
-  if (done) return stream_after((hipStream_t)done, P->st, P->ev);
-  return PLK_OK;
+  return stream_after((hipStream_t)done, P->st, P->ev);   // (NULL: the null stream, torch's default)
 }
 
 int plk_prover_rounds_ext_dev(plk_prover_t* P, const uint8_t* const d_polys[13], const uint8_t chal[5],
@@ -1940,7 +1939,7 @@ int plk_prover_rounds_ext_dev(plk_prover_t* P, const uint8_t* const d_polys[13],
   md.ext = which;
   md.t2 = d_t2;
   md.t3 = d_t3;
-  if (which && ready) {   // everything enqueued on `ready` so far (the bytes' arrival) before they are read
+  if (which) {   // everything enqueued on `ready` so far (the bytes' arrival; NULL: the null stream) before they are read
     PLK_HIP(hipEventRecord(P->ev, (hipStream_t)ready));
     md.ready = P->ev;
   }

@@ -524,23 +524,24 @@ class Prover:
 
     def chains_dev(self, polys, chal, rand, which, t2=None, t3=None, done=None):
         """Helper GPU: enqueue the preparation and the chains in `which` (PLK_CHAIN_* mask) into
-        the device buffers t2 / t3 (chain_bytes each); stream `done` waits for them."""
+        the device buffers t2 / t3 (chain_bytes each); stream `done` (None: the null stream,
+        torch's default) waits for them."""
         args = self._args(polys, chal, rand)
         _check("plk_prover_chains_dev", lib().plk_prover_chains_dev(
             self._h, args[0], args[1], args[2], int(which), _ptr(t2) if t2 is not None else None,
-            _ptr(t3) if t3 is not None else None, _stream(done) if done is not None else None))
+            _ptr(t3) if t3 is not None else None, _stream(done)))
 
     def rounds_ext_dev(self, polys, chal, rand, which, t2=None, t3=None, ready=None, strict=False,
                        preprocessed=False):
         """rounds_dev with the chains in `which` read from t2 / t3 (computed by chains_dev on
-        another GPU from the same inputs) once everything enqueued on stream `ready` so far has
-        run.  Same 34 bytes as rounds_dev."""
+        another GPU from the same inputs) once everything enqueued on stream `ready` (None: the
+        null stream) so far has run.  Same 34 bytes as rounds_dev."""
         args = self._args(polys, chal, rand)
         out = (C.c_uint8 * 34)()
         flags = (PLK_PROVE_STRICT if strict else 0) | (PLK_PROVE_PREPROCESSED if preprocessed else 0)
         _check("plk_prover_rounds_ext_dev", lib().plk_prover_rounds_ext_dev(
             self._h, args[0], args[1], args[2], flags, int(which), _ptr(t2) if t2 is not None else None,
-            _ptr(t3) if t3 is not None else None, _stream(ready) if ready is not None else None, out))
+            _ptr(t3) if t3 is not None else None, _stream(ready), out))
         return bytes(out)
 
     def preprocess(self, polys):

@@ -14,7 +14,7 @@ from conftest import load_golden
 pytestmark = pytest.mark.gpu
 
 
-def _split_proof(hip, n, polys, chal, rnd, zh, pts, which, helpers=1, preprocessed=False):
+def _split_proof(hip, n, polys, chal, rnd, zh, pts, which, helpers=1, preprocessed=False, side_stream=True):
     """which: chain mask the helpers compute; helpers = 1 (one prover for every chain in `which`)
     or 2 (one prover per chain)"""
     main = hip.Prover(n, zh, pts)
@@ -23,7 +23,7 @@ def _split_proof(hip, n, polys, chal, rnd, zh, pts, which, helpers=1, preprocess
         main.preprocess(dev)
     t2 = torch.zeros(main.chain_bytes(hip.PLK_CHAIN_T2), dtype=torch.uint8, device="cuda")
     t3 = torch.zeros(main.chain_bytes(hip.PLK_CHAIN_T3), dtype=torch.uint8, device="cuda")
-    st = torch.cuda.Stream()
+    st = torch.cuda.Stream() if side_stream else torch.cuda.current_stream()   # (the default: the null stream)
     masks = [which] if helpers == 1 else [m for m in (hip.PLK_CHAIN_T2, hip.PLK_CHAIN_T3) if which & m]
     hs = [hip.Prover(n, zh, pts) for _ in masks]
     for h, m in zip(hs, masks):
@@ -38,11 +38,12 @@ def _split_proof(hip, n, polys, chal, rnd, zh, pts, which, helpers=1, preprocess
     return got, want
 
 
-@pytest.mark.parametrize("which,helpers", [(1, 1), (2, 1), (3, 1), (3, 2)])
-def test_split_matches_single_prover(hip, which, helpers):
+@pytest.mark.parametrize("which,helpers,side", [(1, 1, True), (2, 1, True), (3, 1, True), (3, 2, True), (3, 1, False)])
+def test_split_matches_single_prover(hip, which, helpers, side):
+    """side = False: the hand-off through torch's default (null) stream, as the bench leg does"""
     n = 1 << 16
     polys, chal, rnd, zh, pts = gen.prove_instance(n, 41, 2 * n + 8)
-    got, want = _split_proof(hip, n, polys, chal, rnd, zh, pts, which, helpers)
+    got, want = _split_proof(hip, n, polys, chal, rnd, zh, pts, which, helpers, side_stream=side)
     assert got.hex() == want.hex()
 
 
@@ -70,7 +71,7 @@ def test_split_argument_errors(hip):
     polys, chal, rnd, zh, pts = gen.prove_instance(n, 5, 2 * n + 8)
     pr = hip.Prover(n, zh, pts)
     dev = [torch.from_numpy(p).to("cuda") for p in polys]
-    assert pr.chain_bytes(hip.PLK_CHAIN_T2) > 6 * n and pr.chain_bytes(hip.PLK_CHAIN_T3) > 6 * n
+    assert pr.chain_bytes(hip.PLK_CHAIN_T2) > 4 * n and pr.chain_bytes(hip.PLK_CHAIN_T3) > 4 * n   # (t_2, t_3: ~4n + 6 coefficients)
     assert pr.chain_bytes(4) == 0
     with pytest.raises(hip.PlonkHipError):
         pr.chains_dev(dev, chal, rnd, hip.PLK_CHAIN_T2, None, None)        # no buffer for the chain
