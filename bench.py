@@ -18,7 +18,9 @@ tests/golden/msm.json large[7]; both results are reported.
 
 Also reported (rank 0, `components`): one 2^22 MSM per launch, the 2^16-point MSM (config C2),
 the 2^20 forward NTT (config C3) and poly_mul 2^19 x 2^19 with their rooflines, the 2^20-gate
-prove (C5), and the reference CPU path timed on this host (MSM, schoolbook poly_mul, toy prove).
+prove (C5: plain, preprocessed, and the pieces of its strong-scaled form; at N > 1 replicas on
+every GPU and one proof strong-scaled over up to 3 GPUs), and the reference CPU path timed on this
+host (MSM, schoolbook poly_mul, toy prove).
 
     python bench.py [--gpus N --steps K --warmup W --log2n 22 --weak]
 """
@@ -62,7 +64,7 @@ def parse():
     ap.add_argument("--components", default="all",
                     help="all | none | comma list of: msm, ntt, polymul, polyops, prove, cpu -- what rank 0 "
                          "reports beside the headline; at N > 1 'prove' (in 'all') runs C5's replica leg "
-                         "(one concurrent proof per GPU)")
+                         "(one concurrent proof per GPU) and its strong-scaled leg (one proof over up to 3 GPUs)")
     ap.add_argument("--profile-only", action="store_true",
                     help="just launch the timed MSM loop (for rocprofv3 runs)")
     ap.add_argument("--weak", action="store_true",
@@ -312,6 +314,7 @@ def components(torch, hip, dev, st, want):
     if "prove" in want:
         out["prove_2^20_gates"] = prove_component(torch, hip, dev, 20)
         out["prove_2^20_gates_preprocessed"] = prove_component(torch, hip, dev, 20, preprocessed=True)
+        out["prove_2^20_gates_split_pieces"] = prove_split_pieces(torch, hip, dev, 20)
     return out
 
 
@@ -639,11 +642,58 @@ def prove_component(torch, hip, dev, log2n, reps=5, preprocessed=False, barrier=
                     "(no 2^20-point domain in GF(17)), so parity at 2^20 is pinned through that restatement"}
 
 
+def prove_split_pieces(torch, hip, dev, log2n, reps=5):
+    """The pieces of the strong-scaled proof (prove_split_component) timed on this one GPU: rank 0's
+    proof with both chains' products already received (plk_prover_rounds_ext_dev, wall time per
+    synchronous call) and a helper's chains alone (plk_prover_chains_dev, wall time to the
+    products' completion).  With the chains' transfer (4 MiB each over xGMI) hidden behind rank 0's
+    own work, rank 0's time is the strong-scaled proof's time: both chains received at 3 GPUs,
+    t_3 received at 2."""
+    n = 1 << log2n
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import gen
+    hpolys, chal, rnd, zh, pts = gen.prove_instance(n, 51, 2 * n + 8)
+    polys = [torch.from_numpy(p).to(dev) for p in hpolys]
+    pr = hip.Prover(n, zh, pts)
+    T2, T3 = hip.PLK_CHAIN_T2, hip.PLK_CHAIN_T3
+    bufs = {c: torch.zeros(pr.chain_bytes(c), dtype=torch.uint8, device=dev) for c in (T2, T3)}
+    single = pr.rounds_dev(polys, chal, rnd)
+    pr.chains_dev(polys, chal, rnd, T2 | T3, bufs[T2], bufs[T3])
+    torch.cuda.synchronize()
+
+    def best(fn):
+        fn()
+        t = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            t.append(time.perf_counter() - t0)
+        return round(min(t) * 1e3, 3)
+
+    def chains(m):
+        pr.chains_dev(polys, chal, rnd, m, bufs[T2] if m & T2 else None, bufs[T3] if m & T3 else None)
+        torch.cuda.synchronize()
+
+    out = {"single_gpu_ms": best(lambda: pr.rounds_dev(polys, chal, rnd)),
+           "rank0_with_chains_received_ms": best(lambda: pr.rounds_ext_dev(polys, chal, rnd, T2 | T3, bufs[T2], bufs[T3])),
+           "rank0_with_t3_received_ms": best(lambda: pr.rounds_ext_dev(polys, chal, rnd, T3, None, bufs[T3])),
+           "helper_t2_chain_ms": best(lambda: chains(T2)), "helper_t3_chain_ms": best(lambda: chains(T3)),
+           "helper_both_chains_ms": best(lambda: chains(T2 | T3)),
+           "chain_bytes": pr.chain_bytes(T2),
+           "same_proof": pr.rounds_ext_dev(polys, chal, rnd, T2 | T3, bufs[T2], bufs[T3]) == single,
+           "note": "one GPU: the strong-scaled proof's pieces (DESIGN 6b); rank0_*: the proving GPU's wall time "
+                   "per proof once the chains' products are on it; helper_*: a helper GPU's chain(s) from the "
+                   "same inputs, to completion; the multi-GPU time adds the chain products' transfer "
+                   "(chain_bytes each) where it is not hidden behind rank 0's own work"}
+    pr.close()
+    return out
+
+
 def prove_split_component(torch, hip, dev, dist, rank, world, gloo, log2n=20, reps=5):
     """C5 strong-scaled over the ranks (round 3's independent poly_mul jobs spread
     across GPUs as whole jobs).  Every rank holds the same proof inputs (gen.prove_instance, seed
     51).  Rank 1 computes round 3's t_2 chain (A2 B2)(C2 z) and rank 2 the t_3 chain
-    (A3 B3)(C3 z(omega x)) (src/plonk.h:432-434, 471-473) -- at N = 2 rank 1 computes both --
+    (A3 B3)(C3 z(omega x)) (src/plonk.h:432-434, 471-473) -- at N = 2 rank 1 only t_3 --
     with plk_prover_chains_dev and sends the product bytes to rank 0 (RCCL send / receive, 4 MiB
     per chain at 2^20 gates); rank 0 runs everything else and reads them after the receive
     (plk_prover_rounds_ext_dev).  Ranks >= 3 idle.  Timed: rank 0's wall time per proof, every
@@ -656,7 +706,10 @@ def prove_split_component(torch, hip, dev, dist, rank, world, gloo, log2n=20, re
     polys = [torch.from_numpy(p).to(dev) for p in hpolys]
     pr = hip.Prover(n, zh, pts)
     T2, T3 = hip.PLK_CHAIN_T2, hip.PLK_CHAIN_T3
-    assign = {1: T2 | T3} if world == 2 else {1: T2, 2: T3}
+    # N = 2: one helper chain (t_3); rank 0 keeps t_2 and its (a b) q_m sum group -- the one-GPU
+    # pieces (prove_split_pieces) put rank 0 with t_3 received at ~0.35 ms, while one helper with
+    # both chains would deliver 8 MiB after ~0.23 ms of chains
+    assign = {1: T3} if world == 2 else {1: T2, 2: T3}
     bufs = {c: torch.zeros(pr.chain_bytes(c), dtype=torch.uint8, device=dev) for c in (T2, T3)}
     st = torch.cuda.current_stream()
 
@@ -676,7 +729,10 @@ def prove_split_component(torch, hip, dev, dist, rank, world, gloo, log2n=20, re
                 q.wait()                     # (RCCL: the current stream waits for the receive)
             for c, h in host:
                 bufs[c].copy_(h)
-            return pr.rounds_ext_dev(polys, chal, rnd, T2 | T3, bufs[T2], bufs[T3], ready=st)
+            got = 0
+            for m in assign.values():
+                got |= m
+            return pr.rounds_ext_dev(polys, chal, rnd, got, bufs[T2], bufs[T3], ready=st)
         m = assign.get(rank, 0)
         if m:
             pr.chains_dev(polys, chal, rnd, m, bufs[T2] if m & T2 else None, bufs[T3] if m & T3 else None, done=st)
@@ -719,7 +775,7 @@ def prove_split_component(torch, hip, dev, dist, rank, world, gloo, log2n=20, re
             "matches_oracle": _prove_golden(n, out), "same_as_single_gpu": all(o == first for o in [out] + outs),
             "transport": "gloo through host memory (one-GPU rehearsal)" if gloo else "RCCL send / receive",
             "note": "one 2^20-gate proof strong-scaled: rank 1 computes round 3's t_2 chain (A2 B2)(C2 z) and rank "
-                    "2 the t_3 chain (A3 B3)(C3 z(omega x)) (N = 2: rank 1 both) from the same inputs, "
+                    "2 the t_3 chain (A3 B3)(C3 z(omega x)) (N = 2: rank 1 t_3 only) from the same inputs, "
                     "plk_prover_chains_dev, and sends the 4 MiB products to rank 0, which runs the rest "
                     "(plk_prover_rounds_ext_dev); ms = rank 0's wall time per proof, all ranks released by one "
                     "barrier; single_gpu_ms = rank 0 alone on the same instance"}
