@@ -81,3 +81,69 @@ def test_split_argument_errors(hip):
     with pytest.raises(hip.PlonkHipError):
         pr.rounds_ext_dev(dev, chal, rnd, hip.PLK_CHAIN_T3, None, buf[1:])  # misaligned
     pr.close()
+
+
+def _oracle_want(oracle, n, polys, chal, rnd, zh, pts):
+    from prove_ref import Prover as RefProver
+    return RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes()).rounds(polys, chal, rnd, strict=False)
+
+
+def _split_on(hip, n, dev, chal, rnd, zh, pts, which=3, strict=False):
+    """helpers on the null stream, the proving prover reading after it"""
+    main, helper = hip.Prover(n, zh, pts), hip.Prover(n, zh, pts)
+    t2 = torch.zeros(main.chain_bytes(hip.PLK_CHAIN_T2), dtype=torch.uint8, device="cuda")
+    t3 = torch.zeros(main.chain_bytes(hip.PLK_CHAIN_T3), dtype=torch.uint8, device="cuda")
+    try:
+        helper.chains_dev(dev, chal, rnd, which, t2, t3)
+        return main.rounds_ext_dev(dev, chal, rnd, which, t2, t3, strict=strict)
+    finally:
+        helper.close()
+        main.close()
+
+
+@pytest.mark.parametrize("n,seed", [(8, 1), (1000, 4), (3000, 5)])
+def test_split_vs_oracle(hip, oracle, n, seed):
+    """the split proof against the CPU restatement (oracle/prove_ref.py) directly"""
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, seed, 2 * n + 8)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    assert _split_on(hip, n, dev, chal, rnd, zh, pts).hex() == _oracle_want(oracle, n, polys, chal, rnd, zh, pts).hex()
+
+
+def test_split_unaligned_inputs(hip, oracle):
+    """odd device addresses: both sides fall back from prep_kernel to the poly_mul + lincomb
+    preparation; the numerator then runs as a lincomb + division instead of numdiv_kernel"""
+    n = 1000
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, 4, 2 * n + 8)
+    backing = [torch.zeros(n + 16, dtype=torch.uint8, device="cuda") for _ in polys]
+    dev = []
+    for b, p in zip(backing, polys):
+        b[3:3 + n] = torch.from_numpy(p).to("cuda")
+        dev.append(b[3:3 + n])
+    for which in (1, 2, 3):
+        assert _split_on(hip, n, dev, chal, rnd, zh, pts, which).hex() == \
+            _oracle_want(oracle, n, polys, chal, rnd, zh, pts).hex()
+
+
+def test_split_general_divisor(hip, oracle):
+    """Z_H not of the form x^m + c (the general long division after the received chains)"""
+    import numpy as np
+    n = 3
+    polys, chal, rnd, _, pts = gen.prove_instance(n, 11, 16)
+    zh = np.frombuffer(oracle.poly_mul(oracle.poly_mul([16, 1], [13, 1]), [1, 1]), np.uint8)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    assert _split_on(hip, n, dev, chal, rnd, zh, pts).hex() == _oracle_want(oracle, n, polys, chal, rnd, zh, pts).hex()
+
+
+def test_split_reference_exits(hip):
+    """strict: the synthetic numerator is not divisible by Z_H (the reference exits) -- an error
+    through the split path too; an SRS too short for w_z(x) -> PLK_ERR_RANGE"""
+    n = 64
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, 21, 2 * n + 8)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    with pytest.raises(hip.PlonkHipError):
+        _split_on(hip, n, dev, chal, rnd, zh, pts, strict=True)
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, 21, n + 3)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    with pytest.raises(hip.PlonkHipError) as e:
+        _split_on(hip, n, dev, chal, rnd, zh, pts)
+    assert e.value.code == hip.PLK_ERR_RANGE
