@@ -1,6 +1,11 @@
-# breakdown of bench.py's timed region (launch loop / finish / sync) -- lab only
+"""Breakdown of bench.py's timed region on one GPU (lab tool): the launch loop, the
+records -> partials step, the finish (its nonzero() is the host's wait for the device) and the
+final synchronize, for 4 consecutive timed regions of K = 20 steps of B MSMs (B from $B, default
+40).  The first region of a process was ~0.13 ms slower than the rest (clocks after an idle gap).
+
+    B=160 python tools/timing_probe.py
+"""
 import sys, time, os, json
-sys.argv = ["bench.py"] + sys.argv[1:]
 sys.path.insert(0, "."); sys.path.insert(0, "plonk.c_amd")
 import torch, plonkhip as hip
 from plonkhip.dist import finish_sharded, gpu_ops
@@ -31,4 +36,4 @@ for rep in range(4):
     torch.cuda.synchronize()
     t4 = time.perf_counter()
     e2 = torch.cuda.Event(); e2.record(st); torch.cuda.synchronize()
-    print(json.dumps({"B": B, "launch_loop_ms": round((t1-t0)*1e3,3), "r2p_ms": round((t2-t1)*1e3,3), "finish_ms": round((t3-t2)*1e3,3), "sync_ms": round((t4-t3)*1e3,3), "total_ms": round((t4-t0)*1e3,3), "kernels_ms_est": None}), flush=True)
+    print(json.dumps({"B": B, "launch_loop_ms": round((t1-t0)*1e3,3), "r2p_ms": round((t2-t1)*1e3,3), "finish_ms": round((t3-t2)*1e3,3), "sync_ms": round((t4-t3)*1e3,3), "total_ms": round((t4-t0)*1e3,3)}), flush=True)
