@@ -236,11 +236,13 @@ static int np_mul_raw(const uint8_t *a, size_t la, const uint8_t *b, size_t lb, 
 /* returns trimmed length, or 0 on allocation failure / size out of range.  Products longer
  * than 2^23 split the longer operand into chunks whose products fit 2^23 points and add the
  * shifted chunk products mod 17 (exact: each chunk product is). */
+size_t orc_poly_mul_ntt_blocked(const uint8_t *a, size_t la, const uint8_t *b, size_t lb, uint8_t *out, size_t ms);
+
 size_t orc_poly_mul_ntt(const uint8_t *a, size_t la, const uint8_t *b, size_t lb, uint8_t *out) {
   const size_t NMAX = (size_t)1 << 23;
   size_t rl = la + lb - 1;
   size_t mn = la < lb ? la : lb;
-  if (mn * 256 >= NP) return 0;
+  if (mn * 256 >= NP) return orc_poly_mul_ntt_blocked(a, la, b, lb, out, (NP - 1) / 256);
   if (rl <= NMAX) return np_mul_raw(a, la, b, lb, out) ? trim(out, rl) : 0;
   if (la < lb) {   /* a := the longer operand */
     const uint8_t *t = a; a = b; b = t;
@@ -254,6 +256,31 @@ size_t orc_poly_mul_ntt(const uint8_t *a, size_t la, const uint8_t *b, size_t lb
     const size_t cl = la - s < h ? la - s : h;
     if (!np_mul_raw(a + s, cl, b, lb, part)) { free(part); return 0; }
     for (size_t i = 0; i < cl + lb - 1; i++) out[s + i] = (uint8_t)((out[s + i] + part[i]) % P_HF);
+  }
+  free(part);
+  return trim(out, rl);
+}
+
+/* Both operands too long for one exact product (min(la, lb) * 256 >= 998244353): the shorter
+ * one in pieces of at most ms coefficients (ms * 256 < 998244353), each piece times the longer
+ * operand by orc_poly_mul_ntt, the shifted piece products added mod 17 (exact: each is).  An
+ * independent decomposition of the device's blocked products (other prime, other piece sizes);
+ * small ms only to test the piece bookkeeping against the schoolbook. */
+size_t orc_poly_mul_ntt_blocked(const uint8_t *a, size_t la, const uint8_t *b, size_t lb, uint8_t *out, size_t ms) {
+  if (la == 0 || lb == 0 || ms == 0 || ms * 256 >= NP) return 0;
+  if (la < lb) {   /* b := the shorter operand */
+    const uint8_t *t = a; a = b; b = t;
+    size_t u = la; la = lb; lb = u;
+  }
+  const size_t rl = la + lb - 1;
+  uint8_t *part = malloc(la + ms);
+  if (!part) return 0;
+  memset(out, 0, rl);
+  for (size_t s = 0; s < lb; s += ms) {
+    const size_t bl = lb - s < ms ? lb - s : ms;
+    memset(part, 0, la + bl - 1);
+    if (!orc_poly_mul_ntt(a, la, b + s, bl, part)) { free(part); return 0; }
+    for (size_t i = 0; i < la + bl - 1; i++) out[s + i] = (uint8_t)((out[s + i] + part[i]) % P_HF);
   }
   free(part);
   return trim(out, rl);

@@ -105,6 +105,8 @@ class Oracle(_Lib):
         L.orc_dlog_generator.argtypes = [_u8p]
         L.orc_poly_mul_ntt.restype = C.c_size_t
         L.orc_poly_mul_ntt.argtypes = [_u8p, C.c_size_t, _u8p, C.c_size_t, _u8p]
+        L.orc_poly_mul_ntt_blocked.restype = C.c_size_t
+        L.orc_poly_mul_ntt_blocked.argtypes = [_u8p, C.c_size_t, _u8p, C.c_size_t, _u8p, C.c_size_t]
         L.orc_poly_divide.restype = C.c_int
         L.orc_poly_divide.argtypes = [_u8p, C.c_size_t, _u8p, C.c_size_t, _u8p,
                                       C.POINTER(C.c_size_t), _u8p, C.POINTER(C.c_size_t)]
@@ -148,6 +150,15 @@ class Oracle(_Lib):
         n = self.lib.orc_poly_mul_ntt(_ptr(a), len(a), _ptr(b), len(b), _ptr(out))
         if n == 0:
             raise ValueError("orc_poly_mul_ntt: size out of range")
+        return bytes(out[:n])
+
+    def poly_mul_ntt_blocked(self, a, b, piece):
+        """orc_poly_mul_ntt_blocked: the shorter operand in pieces of at most `piece` coefficients"""
+        a, b = _u8(a), _u8(b)
+        out = np.zeros(len(a) + len(b) - 1, np.uint8)
+        n = self.lib.orc_poly_mul_ntt_blocked(_ptr(a), len(a), _ptr(b), len(b), _ptr(out), int(piece))
+        if n == 0:
+            raise ValueError("orc_poly_mul_ntt_blocked: bad arguments")
         return bytes(out[:n])
 
     def poly_divide(self, num, den):
@@ -215,6 +226,15 @@ class Reference(_Lib):
         out = np.zeros(3, np.uint8)
         self.lib.ref_msm(_ptr(pts), _ptr(sc), sc.size, _ptr(out))
         return bytes(out)
+
+    def poly_mul_ntt_blocked(self, a, b, piece):
+        """orc_poly_mul_ntt_blocked: the shorter operand in pieces of at most `piece` coefficients"""
+        a, b = _u8(a), _u8(b)
+        out = np.zeros(len(a) + len(b) - 1, np.uint8)
+        n = self.lib.orc_poly_mul_ntt_blocked(_ptr(a), len(a), _ptr(b), len(b), _ptr(out), int(piece))
+        if n == 0:
+            raise ValueError("orc_poly_mul_ntt_blocked: bad arguments")
+        return bytes(out[:n])
 
     def poly_divide(self, num, den):
         num, den = _u8(num), _u8(den)

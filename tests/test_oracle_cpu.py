@@ -169,6 +169,15 @@ def test_poly_mul_ntt_beyond_two_adicity(oracle):
     assert ok
 
 
+@pytest.mark.parametrize("la,lb,piece", [(3000, 2000, 700), (1999, 2001, 1), (500, 4000, 499), (4096, 4096, 4096)])
+def test_poly_mul_ntt_blocked_vs_schoolbook(oracle, la, lb, piece):
+    """the checker's both-operands blocking (the regime beyond one exact product, used by the
+    8 M x 8 M GPU test) against the schoolbook restatement of src/poly.h:106-122, piece sizes
+    forced small"""
+    a, b = gen.poly_inputs(la + 3 * lb, la, lb)
+    assert oracle.poly_mul_ntt_blocked(a, b, piece) == oracle.poly_mul(a, b)
+
+
 def test_polyops_goldens(oracle):
     """the oracle's poly_divide / poly_eval / matrix restatements vs the reference's outputs
     (tests/golden/polyops.json)"""

@@ -302,11 +302,13 @@ def test_blocked_forced_device_api(hip, oracle):
 
 
 def test_blocked_beyond_babybear_range(hip, oracle):
-    """8,000,000 x 8,000,000 (min * 256 >= 15 2^27 + 1: no single transform is exact): the
-    product at all 17 points of GF(17) equals a(x) b(x), and the lowest / highest 3000
-    coefficients equal the oracle's products of the operands' first / last 3000 coefficients
-    (they depend on nothing else).  Parity unpinned by the reference at this size (its
-    schoolbook loop would take days); the checks are size-independent properties."""
+    """8,000,000 x 8,000,000 (min * 256 >= 15 2^27 + 1: no single transform is exact): every
+    byte equals the oracle's product -- an independent blocked decomposition (both operands in
+    pieces, NTTs over 998244353, orc_poly_mul_ntt_blocked, itself checked against the schoolbook
+    restatement in tests/test_oracle_cpu.py; ~8 s of host time) -- and, as size-independent
+    properties, the product at all 17 points of GF(17) equals a(x) b(x) and the lowest / highest
+    3000 coefficients equal the products of the operands' first / last 3000 coefficients.  The
+    reference itself cannot be run at this size (its schoolbook loop would take days)."""
     la = lb = 8_000_000
     a, b = gen.poly_inputs(8008, la, lb)
     got = hip.poly_mul(a, b)
@@ -321,6 +323,7 @@ def test_blocked_beyond_babybear_range(hip, oracle):
     hi = np.frombuffer(oracle.poly_mul_ntt(a[-t:], b[-t:]), np.uint8)
     hi = np.pad(hi, (0, 2 * t - 1 - len(hi)))
     assert np.array_equal(full[rl - t:], hi[t - 1:])
+    assert got == oracle.poly_mul_ntt(a, b)
 
 
 @pytest.mark.parametrize("mode", [0, 2])
