@@ -705,45 +705,16 @@ def prove_split_component(torch, hip, dev, dist, rank, world, gloo, log2n=20, re
     hpolys, chal, rnd, zh, pts = gen.prove_instance(n, 51, 2 * n + 8)
     polys = [torch.from_numpy(p).to(dev) for p in hpolys]
     pr = hip.Prover(n, zh, pts)
+    from plonkhip.dist import split_proof_step
     T2, T3 = hip.PLK_CHAIN_T2, hip.PLK_CHAIN_T3
-    # N = 2: one helper chain (t_3); rank 0 keeps t_2 and its (a b) q_m sum group -- the one-GPU
-    # pieces (prove_split_pieces) put rank 0 with t_3 received at ~0.35 ms, while one helper with
-    # both chains would deliver 8 MiB after ~0.23 ms of chains
-    assign = {1: T3} if world == 2 else {1: T2, 2: T3}
     bufs = {c: torch.zeros(pr.chain_bytes(c), dtype=torch.uint8, device=dev) for c in (T2, T3)}
     st = torch.cuda.current_stream()
 
     def once():
-        if rank == 0:
-            reqs, host = [], []
-            for r, m in sorted(assign.items()):
-                for c in (T2, T3):
-                    if m & c:
-                        if gloo:
-                            h = torch.empty(bufs[c].numel(), dtype=torch.uint8)
-                            dist.recv(h, src=r)
-                            host.append((c, h))
-                        else:
-                            reqs.append(dist.irecv(bufs[c], src=r))
-            for q in reqs:
-                q.wait()                     # (RCCL: the current stream waits for the receive)
-            for c, h in host:
-                bufs[c].copy_(h)
-            got = 0
-            for m in assign.values():
-                got |= m
-            return pr.rounds_ext_dev(polys, chal, rnd, got, bufs[T2], bufs[T3], ready=st)
-        m = assign.get(rank, 0)
-        if m:
-            pr.chains_dev(polys, chal, rnd, m, bufs[T2] if m & T2 else None, bufs[T3] if m & T3 else None, done=st)
-            for c in (T2, T3):
-                if m & c:
-                    if gloo:
-                        dist.send(bufs[c].cpu(), dst=0)
-                    else:
-                        dist.send(bufs[c], dst=0)
-            torch.cuda.synchronize()
-        return None
+        # (N = 2: rank 1 computes t_3 only, rank 0 keeps t_2 and its (a b) q_m sum group -- the
+        # one-GPU pieces, prove_split_pieces, put rank 0 with t_3 received at ~0.33 ms, while one
+        # helper with both chains would deliver 8 MiB after ~0.24 ms of chains)
+        return split_proof_step(pr, polys, chal, rnd, bufs, rank, world, st, via_host=gloo)
 
     single = None
     if rank == 0:

@@ -159,3 +159,57 @@ class gpu_ops:
         res = torch.zeros(self.hip.MSM_RESULT_BYTES, dtype=torch.uint8, device=scalars.device)
         self.hip.msm_g1_serial_dev(points, scalars, scalars.numel(), res, self.stream)
         return bytes(res[self.hip.MSM_G1_OFFSET:self.hip.MSM_G1_OFFSET + 3].cpu().numpy())
+
+
+# ---- one proof strong-scaled over up to 3 ranks (bench.py prove_split_component)
+CHAIN_T2, CHAIN_T3 = 1, 2   # PLK_CHAIN_T2 / PLK_CHAIN_T3: t_2 = (A2 B2)(C2 z), t_3 = (A3 B3)(C3 z(omega x))
+
+
+def chain_assignment(world):
+    """helper rank -> the round-3 chains it computes (src/plonk.h:432-434, 471-473): at N = 2 rank 1
+    takes t_3 (rank 0 keeps t_2 with its (a b) q_m sum group); at N >= 3 rank 1 t_2 and rank 2 t_3;
+    other ranks idle."""
+    if world < 2:
+        return {}
+    return {1: CHAIN_T3} if world == 2 else {1: CHAIN_T2, 2: CHAIN_T3}
+
+
+def split_proof_step(prover, polys, chal, rnd, bufs, rank, world, stream=None, via_host=False, group=None):
+    """One strong-scaled proof.  Helpers: prover.chains_dev(...) into bufs, then send the bytes to
+    rank 0; rank 0: receive them into bufs, then prover.rounds_ext_dev(...) reads them after the
+    receive (everything enqueued on `stream`).  bufs = {CHAIN_T2: tensor, CHAIN_T3: tensor}
+    (plk_prover_chain_bytes each, on this rank's device).  via_host: move the bytes through host
+    memory (gloo, which has no device send / receive).  Returns the proof bytes on rank 0, None
+    elsewhere; every rank's part is complete on return."""
+    import torch
+    dist = _dist()
+    assign = chain_assignment(world)
+    if rank == 0:
+        reqs, host = [], []
+        for r, m in sorted(assign.items()):
+            for c in (CHAIN_T2, CHAIN_T3):
+                if m & c:
+                    if via_host:
+                        h = torch.empty(bufs[c].numel(), dtype=torch.uint8)
+                        dist.recv(h, src=r, group=group)
+                        host.append((c, h))
+                    else:
+                        reqs.append(dist.irecv(bufs[c], src=r, group=group))
+        for q in reqs:
+            q.wait()                         # (RCCL: the current stream waits for the receive)
+        for c, h in host:
+            bufs[c].copy_(h)
+        got = 0
+        for m in assign.values():
+            got |= m
+        return prover.rounds_ext_dev(polys, chal, rnd, got, bufs[CHAIN_T2], bufs[CHAIN_T3], ready=stream)
+    m = assign.get(rank, 0)
+    if m:
+        prover.chains_dev(polys, chal, rnd, m, bufs[CHAIN_T2] if m & CHAIN_T2 else None,
+                          bufs[CHAIN_T3] if m & CHAIN_T3 else None, done=stream)
+        for c in (CHAIN_T2, CHAIN_T3):
+            if m & c:
+                dist.send(bufs[c].cpu() if via_host else bufs[c], dst=0, group=group)
+        if bufs[CHAIN_T2].is_cuda:
+            torch.cuda.synchronize()
+    return None

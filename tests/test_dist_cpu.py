@@ -129,3 +129,80 @@ def test_shard_ranges_cover_exactly():
                 assert b == c
             sizes = [b - a for a, b in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+# ---- the strong-scaled proof's choreography (plonkhip.dist.split_proof_step, what bench.py's
+# prove_split_component runs over RCCL) with a stand-in prover: helpers fill their chain buffers
+# with known bytes, rank 0's "proof" is a digest of the chains it received
+_CHAIN_LEN = 4099
+
+
+def _chain_bytes(c, chal):
+    import torch
+    return (torch.arange(_CHAIN_LEN, dtype=torch.int64) * (7 * c + chal[0]) % 251).to(torch.uint8)
+
+
+class MockProver:
+    def chains_dev(self, polys, chal, rnd, which, t2=None, t3=None, done=None):
+        for c, buf in ((1, t2), (2, t3)):
+            if which & c:
+                buf.copy_(_chain_bytes(c, chal))
+
+    def rounds_ext_dev(self, polys, chal, rnd, which, t2=None, t3=None, ready=None):
+        import hashlib
+        h = hashlib.sha256(bytes([which]))
+        for c, buf in ((1, t2), (2, t3)):
+            if which & c:
+                h.update(buf.numpy().tobytes())
+        return h.digest()
+
+
+def _split_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "plonk.c_amd"))
+    sys.path.insert(0, here)
+    import torch
+    import torch.distributed as dist
+
+    from plonkhip.dist import split_proof_step
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from test_dist_cpu import MockProver
+    bufs = {c: torch.zeros(_CHAIN_LEN, dtype=torch.uint8) for c in (1, 2)}
+    outs = [split_proof_step(MockProver(), [], [5, 1, 2, 3, 4], [0] * 9, bufs, rank, world, via_host=True)
+            for _ in range(2)]
+    q.put((rank, [o.hex() if o is not None else None for o in outs]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_split_proof_choreography(world):
+    """rank 1 (N = 2: t_3; N >= 3: t_2) and rank 2 (t_3) send their chains, rank 0 proves with
+    exactly those, the other ranks idle; two proofs back to back keep the sends and receives
+    paired"""
+    import hashlib
+
+    from plonkhip.dist import chain_assignment
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    union = 0
+    for m in chain_assignment(world).values():
+        union |= m
+    assert union == (2 if world == 2 else 3)
+    h = hashlib.sha256(bytes([union]))
+    for c in (1, 2):
+        if union & c:
+            h.update(_chain_bytes(c, [5]).numpy().tobytes())
+    assert got[0] == [h.digest().hex()] * 2
+    assert all(got[r] == [None, None] for r in range(1, world))
