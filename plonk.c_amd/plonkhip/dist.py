@@ -177,7 +177,8 @@ def chain_assignment(world):
 def split_proof_step(prover, polys, chal, rnd, bufs, rank, world, stream=None, via_host=False, group=None):
     """One strong-scaled proof.  Helpers: prover.chains_dev(...) into bufs, then send the bytes to
     rank 0; rank 0: receive them into bufs, then prover.rounds_ext_dev(...) reads them after the
-    receive (everything enqueued on `stream`).  bufs = {CHAIN_T2: tensor, CHAIN_T3: tensor}
+    receive.  `stream`: torch's current stream (the one a device receive's wait() orders and a
+    device send follows; None = the null stream).  bufs = {CHAIN_T2: tensor, CHAIN_T3: tensor}
     (plk_prover_chain_bytes each, on this rank's device).  via_host: move the bytes through host
     memory (gloo, which has no device send / receive).  Returns the proof bytes on rank 0, None
     elsewhere; every rank's part is complete on return."""
