@@ -159,13 +159,15 @@ def graph_avg_ms(torch, fn, reps, rounds=3):
 
 def cpu_baseline(pts_np, sc_np, budget_s, gpu_g1):
     """Reference CPU MSM (oracle/_ref = the unmodified reference srs_eval_at_s, -O2) on this
-    host, 1 thread; falls back to the oracle restatement if the reference build is absent."""
+    host, 1 thread.  No silent substitute: without the reference build the baseline is an
+    error entry (and main() records a failed check), never a timing of the restatement."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from pyoracle import Oracle, Reference
-    if Reference.available():
-        impl, kind = Reference(), "reference"
-    else:
-        impl, kind = Oracle(), "port"
+    from pyoracle import Reference
+    if not Reference.available():
+        return {"error": "oracle/_ref/libplonkref.so is absent (built by `make -C oracle` where /root/reference "
+                         "exists; it travels with the tree): the reference CPU baseline was not measured",
+                "kind": "reference", "value": None}
+    impl, kind = Reference(), "reference"
     t0 = time.perf_counter()
     out = impl.msm(pts_np, sc_np)
     dt = time.perf_counter() - t0
@@ -591,7 +593,7 @@ def _prove_golden(n, out):
     return out.hex() == g["proof"] if g["n"] == n and g["seed"] == 51 else None
 
 
-def prove_component(torch, hip, dev, log2n, reps=5, preprocessed=False, barrier=None):
+def prove_component(torch, hip, dev, log2n, reps=9, preprocessed=False, barrier=None):
     """C5: plonk_prove rounds 1-5 (src/plonk.h:277-655) at n = 2^log2n gates on the device
     prover: 17 poly_mul (largest (3n+4) x (n+3) -> NTT 2^(log2n+3)), 9 commitments, 3
     divisions, evaluations.  Synthetic interpolated polynomials (GF(17) has no subgroup of
@@ -632,7 +634,10 @@ def prove_component(torch, hip, dev, log2n, reps=5, preprocessed=False, barrier=
                              "l_1_x (PLONK's preprocessed input) computed once by plk_prover_preprocess before the "
                              "timed calls; everything that depends on the witness, blinding or challenges runs in "
                              "every call, and the proof bytes are the same as without"} if preprocessed else {}
-    return {"ms": round(t[0] * 1e3, 3), "median_ms": round(t[len(t) // 2] * 1e3, 3), "gates": n, **extra,
+    # ms = the MEDIAN of the synchronous calls (the honest figure for one call; box-to-box spread
+    # ~3 %); best_ms beside it
+    return {"ms": round(t[len(t) // 2] * 1e3, 3), "median_ms": round(t[len(t) // 2] * 1e3, 3),
+            "best_ms": round(t[0] * 1e3, 3), "calls": reps, "gates": n, **extra,
             "deterministic": out == first, "matches_oracle": _prove_golden(n, out),
             "device_mib": round(pr.device_bytes() / 2**20, 1),
             "note": "rounds 1-5 of plonk_prove, synthetic interpolated polys (gen.prove_instance, seed 51), SRS len 2n+8, "
@@ -936,6 +941,7 @@ def main():
         torch.cuda.synchronize()
         line["cpu_baseline"] = cpu_baseline(pts[first_set].cpu().numpy(), sc[first_set].cpu().numpy(),
                                             args.cpu_seconds, g1s[0])
+        check["cpu_baseline_reference"] = "error" not in line["cpu_baseline"]
     comps = wanted_components(args)
     comp = {}
     if world > 1 and "prove" in comps:

@@ -79,7 +79,10 @@ enum {
   PLK_OPT_MSM_HALF = 14,
   PLK_OPT_MSM_SHARD_MIN = 15,    /* multi-device plk_msm_g1: split from this many points (2^16)      */
   PLK_OPT_NTT_CENTER_SUM = 16,   /* 1: a sum group's products added in its leader's center item      */
-  PLK_OPT_COUNT = 17
+  PLK_OPT_MSM_HOST_LANES = 17,   /* one device: plk_msm_g1 of >= MSM_SHARD_MIN points runs its SRS memcmp,
+                                    staging and uploads on this many host threads (1: one); read by
+                                    plk_init / plk_init_devices */
+  PLK_OPT_COUNT = 18
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
 int64_t plk_get_option(int opt);              /* -1 for an unknown option */

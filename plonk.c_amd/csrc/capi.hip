@@ -5,8 +5,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "plk_device.h"
@@ -331,6 +333,14 @@ int parse_devices(const char* e, int* ids) {
   return n;
 }
 
+// the single-device plk_msm_g1's host lanes: PLK_OPT_MSM_HOST_LANES shards of `device`
+int setup_lanes(int device) {
+  const int nl = (int)std::min<int64_t>(plk_opt(PLK_OPT_MSM_HOST_LANES), PLK_MAX_SHARDS);
+  int ids[PLK_MAX_SHARDS];
+  for (int i = 0; i < nl; i++) ids[i] = device;
+  return plk_shards_setup(ids, nl, s_ytab, s_exp4, s_inv, true);
+}
+
 int init_locked(int device) {
   if (g.ready) {
     if (device >= 0 && device != g.device) {
@@ -372,13 +382,30 @@ int init_locked(int device) {
   PLK_HIP(hipMalloc((void**)&g.d_res, sizeof(PlkMsmResult)));
   PLK_HIP(hipMemset(g.d_res, 0, sizeof(PlkMsmResult)));
   PLK_HIP(hipMalloc((void**)&g.d_nz, 16));
+  if (nlist > 1 || plk_opt(PLK_OPT_MSM_HOST_LANES) > 1) {
+    // the shards first: a failure leaves the library uninitialised (every later call retries
+    // and reports it) instead of published and quietly running on one device.  One device:
+    // host lanes of it (PLK_OPT_MSM_HOST_LANES), so that plk_msm_g1's memcmp and staging run
+    // on several host threads
+    rc = nlist > 1 ? plk_shards_setup(list, nlist, s_ytab, s_exp4, s_inv, false) : setup_lanes(device);
+    (void)hipSetDevice(device);
+    if (rc) {
+      const std::string why = g_err;
+      plk_shards_teardown();
+      (void)hipFree(g.d_res);
+      (void)hipFree(g.d_nz);
+      g.d_res = nullptr;
+      g.d_nz = nullptr;
+      plk_ntt_free_tables();
+      (void)hipStreamDestroy(g.st);
+      g.st = nullptr;
+      plk_set_error("%s", why.c_str());
+      return rc;
+    }
+  }
   g.device = device;
   g.ready = true;
   g_live_dev.store(device, std::memory_order_release);
-  if (nlist > 1) {
-    if ((rc = plk_shards_setup(list, nlist, s_ytab, s_exp4, s_inv))) return rc;
-    PLK_HIP(hipSetDevice(device));
-  }
   return PLK_OK;
 }
 
@@ -433,6 +460,7 @@ const OptDef kOpt[PLK_OPT_COUNT] = {
     {1, 0, 1, false},                          // MSM_HALF
     {1 << 16, 1, 1ll << 40, false},            // MSM_SHARD_MIN
     {1, 0, 1, false},                          // NTT_CENTER_SUM
+    {4, 1, PLK_MAX_SHARDS, false},             // MSM_HOST_LANES (read at plk_init / plk_init_devices)
 };
 struct Opts {
   std::atomic<int64_t> v[PLK_OPT_COUNT];
@@ -538,7 +566,7 @@ int plk_init_devices(const int* ids, int n) {
   std::lock_guard<std::mutex> lk(g.mu);
   int rc = init_locked(ids[0]);   // the primary: tables, NTT, prover, every non-MSM call
   if (rc) return rc;
-  rc = plk_shards_setup(ids, n, s_ytab, s_exp4, s_inv);
+  rc = n > 1 ? plk_shards_setup(ids, n, s_ytab, s_exp4, s_inv, false) : setup_lanes(g.device);
   (void)hipSetDevice(g.device);
   return rc;
 }
@@ -547,7 +575,7 @@ int plk_devices(int* ids, int cap) {
   std::lock_guard<std::mutex> lk(g.mu);
   if (!g.ready) return 0;
   const int ns = plk_shards_count();
-  if (ns > 1) return plk_shards_devices(ids, cap);
+  if (ns > 1 && !plk_shards_are_lanes()) return plk_shards_devices(ids, cap);
   if (ids && cap > 0) ids[0] = g.device;
   return 1;
 }

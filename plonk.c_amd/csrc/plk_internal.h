@@ -32,7 +32,11 @@ int64_t plk_opt(int opt);    // current value of a PLK_OPT_* option (capi.hip)
 
 // shards.hip: in-process multi-device plk_msm_g1 (plk_init_devices); callers hold the library lock
 #define PLK_MAX_SHARDS 16
-int plk_shards_setup(const int* ids, int n, const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101);
+// lanes: the entries all name the primary device and stand for host threads of the single-device
+// plk_msm_g1 (PLK_OPT_MSM_HOST_LANES), not a plk_init_devices list (plk_devices reports one device)
+int plk_shards_setup(const int* ids, int n, const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101,
+                     bool lanes);
+bool plk_shards_are_lanes(void);
 void plk_shards_teardown(void);
 int plk_shards_count(void);
 int plk_shards_devices(int* ids, int cap);

@@ -30,6 +30,13 @@
 #include "plk_device.h"
 #include "plk_internal.h"
 
+// Diagnostic builds only (plonk.c_amd/Makefile `diag`): 1 drops plk_prover_chains_dev's ordering of
+// `done` behind the chains, 2 drops plk_prover_rounds_ext_dev's wait for `ready` -- the hand-off
+// orderings tests/test_split_streams_gpu.py must catch.  0 in the library.
+#ifndef PLK_DIAG_DROP_HANDOFF
+#define PLK_DIAG_DROP_HANDOFF 0
+#endif
+
 namespace {
 
 constexpr uint32_t HFP = 17;
@@ -1674,10 +1681,14 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     }
     // (a b) q_m ADDED into t_2 = (A2 B2)(C2 z) when both run here and their sum fits F29's
     // centered range, 64 (min(l2a, la + lzx - 1) + min(lab, n)) <= (p - 1) / 2 (n <= ~1.2 M): one
-    // 4n inverse transform fewer, one numerator term fewer (t_3 enters with -1, so it stays apart)
+    // 4n inverse transform fewer, one numerator term fewer (t_3 enters with -1, so it stays apart).
+    // A group runs in ONE transform size: t_2 has 4n + 6 coefficients and (a b) q_m 3n + 2, so for
+    // many n (2100, 5000, 600000, ...) the two plans differ and (a b) q_m stays its own job.
     const uint64_t t2b = L.la + L.lzx - 1;
     const int grp = !md.only && (local & PLK_CHAIN_T2) && plk_poly_mul_summable(L.lab, n) &&
                             plk_poly_mul_summable(L.l2a, t2b) &&
+                            plk_poly_mul_transform_plan(L.lab, n, nullptr) ==
+                                plk_poly_mul_transform_plan(L.l2a, t2b, nullptr) &&
                             (std::min(L.l2a, t2b) + std::min<uint64_t>(L.lab, n)) * 128 < f29::P
                         ? 1
                         : 0;
@@ -1921,12 +1932,18 @@ int plk_prover_chains_dev(plk_prover_t* P, const uint8_t* const d_polys[13], con
   int rc = check_chain_args("plk_prover_chains_dev", P, d_polys, chal, rand9, which, d_t2, d_t3);
   if (rc) return rc;
   if (!which) return PLK_OK;
+  // write-after-read: the previous call's d_t2 / d_t3 may still be read by work on `done` (e.g.
+  // an RCCL send of the last products): this call's products are written only after it
+  if ((rc = stream_after(P->st, (hipStream_t)done, P->ev))) return rc;
   RoundsMode md;
   md.only = which;
   md.o2 = d_t2;
   md.o3 = d_t3;
   rc = rounds(P, d_polys, chal, rand9, false, md);
   if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
+#if PLK_DIAG_DROP_HANDOFF & 1   // diagnostic build only (tests/test_split_streams_gpu.py): no ordering
+  return PLK_OK;
+#endif
   return stream_after((hipStream_t)done, P->st, P->ev);   // (NULL: the null stream, torch's default)
 }
 
@@ -1939,8 +1956,8 @@ int plk_prover_rounds_ext_dev(plk_prover_t* P, const uint8_t* const d_polys[13],
   md.ext = which;
   md.t2 = d_t2;
   md.t3 = d_t3;
-  if (which) {   // everything enqueued on `ready` so far (the bytes' arrival; NULL: the null stream) before they are read
-    PLK_HIP(hipEventRecord(P->ev, (hipStream_t)ready));
+  if (which && !(PLK_DIAG_DROP_HANDOFF & 2)) {   // everything enqueued on `ready` so far (the bytes'
+    PLK_HIP(hipEventRecord(P->ev, (hipStream_t)ready));   // arrival; NULL: the null stream) before they are read
     md.ready = P->ev;
   }
   rc = rounds(P, d_polys, chal, rand9, (flags & PLK_PROVE_PREPROCESSED) != 0, md);

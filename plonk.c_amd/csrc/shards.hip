@@ -69,6 +69,7 @@ struct Pool {
   bool stop = false;
   const uint8_t* pts = nullptr;
   const uint8_t* sc = nullptr;
+  bool lanes = false;   // host lanes of the one primary device (not a plk_init_devices list)
   // a program that exits without plk_shutdown (the reference's own test programs through the
   // drop-in): the idle workers are released and joined here -- no HIP call, the runtime may be
   // gone already -- instead of std::thread's terminate on a joinable thread
@@ -230,10 +231,13 @@ void plk_shards_teardown(void) {
   P.sh.clear();
   P.stop = false;
   P.pending = 0;
+  P.lanes = false;
 }
 
-int plk_shards_setup(const int* ids, int n, const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101) {
+int plk_shards_setup(const int* ids, int n, const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101,
+                     bool lanes) {
   plk_shards_teardown();
+  P.lanes = false;
   if (n <= 1) return PLK_OK;   // one device: the single-device path, no shards
   int prev = -1;
   (void)hipGetDevice(&prev);
@@ -269,6 +273,7 @@ int plk_shards_setup(const int* ids, int n, const uint32_t* ytab, const uint8_t*
   }
   if (!rc) {
     P.gen = 0;
+    P.lanes = lanes;
     for (int i = 1; i < n; i++) P.th.emplace_back(worker, i);
   } else {
     for (auto& s : P.sh) free_shard(s);
@@ -279,6 +284,7 @@ int plk_shards_setup(const int* ids, int n, const uint32_t* ytab, const uint8_t*
 }
 
 int plk_shards_count(void) { return (int)P.sh.size(); }
+bool plk_shards_are_lanes(void) { return P.lanes; }
 
 int plk_shards_devices(int* ids, int cap) {
   const int n = (int)P.sh.size();

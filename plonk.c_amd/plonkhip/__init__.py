@@ -83,7 +83,7 @@ SIGNATURES = {
 OPTIONS = {"TINY_CALLS": 1, "PROVE_SYNC": 2, "POLY_BLOCK_L": 3, "POLY_BLOCK_S": 4, "NTT_F29": 5, "NTT_SHARE": 6,
            "NTT_SHARED_FIX": 7, "NTT_T13_MIN_K": 8, "NTT_CENTER_BLOCKS": 9, "MSM_THREADS": 10,
            "MSM_MAX_BLOCKS": 11, "MSM_GROUPS": 12, "MSM_COPIES": 13, "MSM_HALF": 14, "MSM_SHARD_MIN": 15,
-           "NTT_CENTER_SUM": 16}
+           "NTT_CENTER_SUM": 16, "MSM_HOST_LANES": 17}
 
 PLK_PROVE_STRICT = 1
 PLK_PROVE_PREPROCESSED = 2
@@ -522,10 +522,28 @@ class Prover:
         """buffer size for one chain's product (PLK_CHAIN_T2 or PLK_CHAIN_T3)"""
         return int(lib().plk_prover_chain_bytes(self._h, int(chain)))
 
+    def _check_chain_bufs(self, which, t2, t3):
+        """a chain buffer in `which` must be a device tensor of at least chain_bytes on this
+        prover's device (an undersized one would be written / read past its end on the GPU);
+        raw integer pointers are passed through unchecked"""
+        for chain, t in ((PLK_CHAIN_T2, t2), (PLK_CHAIN_T3, t3)):
+            if not (int(which) & chain) or t is None or isinstance(t, int):
+                continue
+            need = self.chain_bytes(chain)
+            have = t.numel() * t.element_size()
+            if have < need:
+                raise ValueError("chain %d buffer holds %d bytes, chain_bytes is %d" % (chain, have, need))
+            if not t.is_cuda:
+                raise ValueError("chain %d buffer is not a device tensor" % chain)
+            dev = getattr(self, "device", None)
+            if dev is not None and t.device.index != dev:
+                raise ValueError("chain %d buffer is on device %s, the prover on %d" % (chain, t.device, dev))
+
     def chains_dev(self, polys, chal, rand, which, t2=None, t3=None, done=None):
         """Helper GPU: enqueue the preparation and the chains in `which` (PLK_CHAIN_* mask) into
         the device buffers t2 / t3 (chain_bytes each); stream `done` (None: the null stream,
         torch's default) waits for them."""
+        self._check_chain_bufs(which, t2, t3)
         args = self._args(polys, chal, rand)
         _check("plk_prover_chains_dev", lib().plk_prover_chains_dev(
             self._h, args[0], args[1], args[2], int(which), _ptr(t2) if t2 is not None else None,
@@ -536,6 +554,7 @@ class Prover:
         """rounds_dev with the chains in `which` read from t2 / t3 (computed by chains_dev on
         another GPU from the same inputs) once everything enqueued on stream `ready` (None: the
         null stream) so far has run.  Same 34 bytes as rounds_dev."""
+        self._check_chain_bufs(which, t2, t3)
         args = self._args(polys, chal, rand)
         out = (C.c_uint8 * 34)()
         flags = (PLK_PROVE_STRICT if strict else 0) | (PLK_PROVE_PREPROCESSED if preprocessed else 0)

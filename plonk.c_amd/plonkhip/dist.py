@@ -174,16 +174,23 @@ def chain_assignment(world):
     return {1: CHAIN_T3} if world == 2 else {1: CHAIN_T2, 2: CHAIN_T3}
 
 
-def split_proof_step(prover, polys, chal, rnd, bufs, rank, world, stream=None, via_host=False, group=None):
+def split_proof_step(prover, polys, chal, rnd, bufs, rank, world, stream=None, via_host=False, group=None,
+                     comm=None):
     """One strong-scaled proof.  Helpers: prover.chains_dev(...) into bufs, then send the bytes to
     rank 0; rank 0: receive them into bufs, then prover.rounds_ext_dev(...) reads them after the
     receive.  `stream`: torch's current stream (the one a device receive's wait() orders and a
     device send follows; None = the null stream).  bufs = {CHAIN_T2: tensor, CHAIN_T3: tensor}
     (plk_prover_chain_bytes each, on this rank's device).  via_host: move the bytes through host
-    memory (gloo, which has no device send / receive).  Returns the proof bytes on rank 0, None
-    elsewhere; every rank's part is complete on return."""
+    memory (gloo, which has no device send / receive).  comm: the torch.distributed-like module to
+    use (default: torch.distributed itself; tests inject a stand-in with RCCL's stream semantics).
+    Returns the proof bytes on rank 0, None elsewhere; every rank's part is complete on return.
+
+    Stream ordering of the device branch (RCCL): a receive's wait() makes `stream` wait for the
+    bytes, and rounds_ext_dev(ready=stream) makes the prover's stream wait for `stream` before its
+    numerator (the only reader of the chains); on a helper, chains_dev(done=stream) makes `stream`
+    wait for the chains, so the send (ordered behind `stream`) reads finished products."""
     import torch
-    dist = _dist()
+    dist = comm if comm is not None else _dist()
     assign = chain_assignment(world)
     if rank == 0:
         reqs, host = [], []

@@ -1,0 +1,87 @@
+"""A torch.distributed stand-in with RCCL's stream semantics, for ONE process that plays every rank
+on one GPU (tests/test_split_streams_gpu.py).  It exists so that the device branch of
+plonkhip.dist.split_proof_step -- the branch an 8-GPU node takes over RCCL -- runs on a one-GPU box,
+with the same ordering hazards:
+
+* send(t): RCCL's send kernel runs on the communicator's own stream behind an event of the caller's
+  CURRENT stream; it reads `t` when that stream gets there, not when send() returns.  Here: the side
+  stream waits for an event of the current stream and copies `t` into a staging tensor (the "wire").
+* irecv(t): the bytes land on the communicator's stream; work.wait() makes the CURRENT stream wait
+  for them and returns at once (no host block).  Here: the side stream spins first (`delay` cycles
+  of torch.cuda._sleep, so the bytes arrive late), then copies the staged bytes into `t`; wait()
+  is current_stream().wait_event.
+
+A consumer that does not order itself behind the current stream at the right point reads bytes
+that are not there yet -- exactly what a missing ready= / done= ordering would do over RCCL.
+"""
+import torch
+
+DELAY_CYCLES = 20_000_000   # the receive's spin on the side stream (milliseconds of device time)
+
+
+class _Work:
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
+class NcclSemantics:
+    def __init__(self, delay=DELAY_CYCLES):
+        self.side = torch.cuda.Stream()
+        self.delay = delay
+        self.wire = {}          # dst rank -> [(staged tensor, event after its copy)], in send order
+
+    def send(self, t, dst, group=None):
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self.side.wait_event(ev)
+        staged = torch.empty_like(t)
+        with torch.cuda.stream(self.side):
+            staged.copy_(t)
+        staged.record_stream(self.side)
+        done = torch.cuda.Event()
+        done.record(self.side)
+        self.wire.setdefault(dst, []).append((staged, done))
+
+    def irecv(self, t, src, group=None):
+        # (this stand-in serves rank 0's receives in send order; the choreography sends each chain once)
+        staged, done = self.wire[0].pop(0)
+        self.side.wait_event(done)
+        with torch.cuda.stream(self.side):
+            torch.cuda._sleep(self.delay)
+            t.copy_(staged)
+        t.record_stream(self.side)
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        return _Work(ev)
+
+    def recv(self, t, src, group=None):
+        raise AssertionError("the device branch must not take the host-memory receive")
+
+
+def split_proof(hip, n, polys, chal, rnd, zh, pts, world, comm=None):
+    """One strong-scaled proof through plonkhip.dist.split_proof_step's DEVICE branch
+    (via_host=False), every rank a prover of its own on this GPU, helpers stepped first (their
+    sends precede rank 0's receives, as on a real node where they run concurrently).  Returns
+    (rank 0's proof, the single-prover proof of the same inputs)."""
+    from plonkhip.dist import split_proof_step
+    comm = comm or NcclSemantics()
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    provers = [hip.Prover(n, zh, pts) for _ in range(world)]
+    try:
+        cb = {c: provers[0].chain_bytes(c) for c in (hip.PLK_CHAIN_T2, hip.PLK_CHAIN_T3)}
+        bufs = [{c: torch.zeros(b, dtype=torch.uint8, device="cuda") for c, b in cb.items()} for _ in range(world)]
+        stream = torch.cuda.current_stream()
+        torch.cuda.synchronize()
+        for r in range(1, world):
+            split_proof_step(provers[r], dev, chal, rnd, bufs[r], r, world, stream, via_host=False, comm=comm)
+        got = split_proof_step(provers[0], dev, chal, rnd, bufs[0], 0, world, stream, via_host=False, comm=comm)
+        torch.cuda.synchronize()
+        want = provers[0].rounds_dev(dev, chal, rnd)
+        return got, want
+    finally:
+        torch.cuda.synchronize()
+        for p in provers:
+            p.close()

@@ -59,8 +59,10 @@ def _synthetic(n, seed, srs_len):
     return gen.prove_instance(n, seed, srs_len)
 
 
-@pytest.mark.parametrize("n,seed", [(8, 1), (37, 2), (256, 3), (1000, 4), (3000, 5)])
+@pytest.mark.parametrize("n,seed", [(8, 1), (37, 2), (256, 3), (1000, 4), (3000, 5), (2100, 6), (5000, 7)])
 def test_rounds_shape_vs_oracle(hip, oracle, n, seed):
+    """(n = 2100 and 5000: t_2 (4n + 6 coefficients) and (a b) q_m (3n + 2) need different
+    transform sizes there, so they must not form one sum group -- ADVICE r3.)"""
     srs_len = 2 * n + 8
     polys, chal, rnd, zh, pts = _synthetic(n, seed, srs_len)
     ref = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes())

@@ -109,6 +109,17 @@ def test_split_vs_oracle(hip, oracle, n, seed):
     assert _split_on(hip, n, dev, chal, rnd, zh, pts).hex() == _oracle_want(oracle, n, polys, chal, rnd, zh, pts).hex()
 
 
+@pytest.mark.parametrize("n,seed", [(2100, 6), (5000, 7)])
+def test_split_vs_oracle_group_sizes(hip, oracle, n, seed):
+    """sizes where t_2 and (a b) q_m land on different transform sizes (no sum group): rank 0
+    keeping t_2 (the N = 2 split, only t_3 received) and receiving both"""
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, seed, 2 * n + 8)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    want = _oracle_want(oracle, n, polys, chal, rnd, zh, pts).hex()
+    for which in (hip.PLK_CHAIN_T3, hip.PLK_CHAIN_T2 | hip.PLK_CHAIN_T3):
+        assert _split_on(hip, n, dev, chal, rnd, zh, pts, which).hex() == want
+
+
 def test_split_unaligned_inputs(hip, oracle):
     """odd device addresses: both sides fall back from prep_kernel to the poly_mul + lincomb
     preparation; the numerator then runs as a lincomb + division instead of numdiv_kernel"""
