@@ -305,6 +305,23 @@ int plk_prover_rounds_ext_dev(plk_prover_t *p, const uint8_t *const d_polys[13],
                               const uint8_t rand9[9], int flags, int which, const uint8_t *d_t2,
                               const uint8_t *d_t3, void *ready, uint8_t proof[34]);
 
+/* The same split driven from C in one process, over the plk_init_devices list (no RCCL, no
+ * caller-side hand-off): plk_prover_attach_helpers(p, k) creates k helper provers on list entries
+ * 1..k (k = 1: t_3 on ids[1]; k = 2: t_2 on ids[1] and t_3 on ids[2]; 0 detaches; call from p's
+ * device).  Afterwards plk_prover_rounds_dev and plk_prover_prove run every proof split: p's
+ * stream records an event after the work already enqueued on it (the inputs); each helper's stream
+ * waits for it, copies the 7 polynomials its chains read (f_a f_b f_c s_sigma_1..3 acc_x) to its
+ * own GPU when that is another device (hipMemcpyPeerAsync), runs the chains, copies their products
+ * into receive buffers on p's GPU (hipMemcpyPeerAsync on the helper's stream) and records an event;
+ * p's stream waits for those events only before its numerator.  Ids may repeat (the one-GPU
+ * rehearsal: helpers on their own streams of the same device).  Same proof bytes.
+ * plk_prover_rounds_multi_dev takes the inputs already resident on every device: d_polys holds
+ * ndev = 1 + k sets of 13 pointers, set 0 on p's device, set h on helper h's (no input copies). */
+int plk_prover_attach_helpers(plk_prover_t *p, int k);
+int plk_prover_helpers(const plk_prover_t *p);   /* the k attached (0: none) */
+int plk_prover_rounds_multi_dev(plk_prover_t *p, const uint8_t *const *d_polys, int ndev, const uint8_t chal[5],
+                                const uint8_t rand9[9], int flags, uint8_t proof[34]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -63,6 +63,8 @@ struct Ctx {
   // small-op staging (poly_divide / poly_eval / interpolate): one device arena
   uint8_t* d_ops = nullptr;
   size_t cap_ops = 0;
+  // further devices holding the kernel tables (helper provers, plk_ctx_prepare_device)
+  bool dev_tables[PLK_MAX_DEVICES] = {};
 } g;
 
 // the initialised device, published after init_locked (-1: not initialised), so that device
@@ -510,6 +512,27 @@ void plk_ctx_release(void) {
   if (g.live_provers > 0) g.live_provers--;
 }
 
+// A further device runs the library's kernels (a helper prover of plk_prover_attach_helpers):
+// its NTT root / column tables and the MSM __constant__ tables are built there once.  Returns
+// with the calling thread's current device unchanged.
+int plk_ctx_prepare_device(int dev) {
+  int rc = ensure_dev();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (dev < 0 || dev >= PLK_MAX_DEVICES || dev >= plk_device_count()) {
+    plk_set_error("device %d out of range", dev);
+    return PLK_ERR_NODEV;
+  }
+  if (dev == g.device || g.dev_tables[dev]) return PLK_OK;
+  const int prev = plk_cur_device();
+  PLK_HIP(hipSetDevice(dev));
+  rc = plk_ntt_init_tables();
+  if (!rc) rc = plk_msm_upload_tables(s_ytab, s_exp4, s_inv);
+  (void)hipSetDevice(prev);
+  if (!rc) g.dev_tables[dev] = true;
+  return rc;
+}
+
 extern "C" {
 
 const char* plk_last_error(void) { return g_err; }
@@ -598,7 +621,9 @@ void plk_shutdown(void) {
   if (g.h_tiny) (void)hipHostFree(g.h_tiny);
   (void)hipFree(g.d_tick0);
   free(g.h_srs);
-  plk_ntt_free_tables();
+  plk_ntt_free_tables();   // (every device's)
+  for (bool& b : g.dev_tables) b = false;
+  (void)hipSetDevice(g.device);
   (void)hipStreamDestroy(g.st);
   // reset field by field: the mutex (held here) stays as it is
   g.ready = false;

@@ -358,6 +358,9 @@ __global__ __launch_bounds__(256) void polymul_direct_kernel(const uint8_t* lg, 
 }
 
 // ------------------------------------------------------------------------------ host side
+// Root tables live on every device that runs transforms (the primary of plk_init, and the helper
+// devices of a multi-device prover, plk_prover_attach_helpers): one set per device id, picked by
+// the calling thread's current device at launch.
 namespace {
 
 struct TwHost {
@@ -367,28 +370,40 @@ struct TwHost {
   uint32_t* d_hi_f = nullptr;
   uint32_t* d_lo_i = nullptr;
   uint32_t* d_hi_i = nullptr;
-} g_tw;
+};
+struct DevTw {
+  TwHost bb, f29;
+};
+DevTw g_tw[PLK_MAX_DEVICES];
 
-Tw tw_fwd() { return Tw{g_tw.d_small_f, g_tw.d_lo_f, g_tw.d_hi_f}; }
-Tw tw_inv() { return Tw{g_tw.d_small_i, g_tw.d_lo_i, g_tw.d_hi_i}; }
+DevTw& cur_tw() { return g_tw[plk_cur_device()]; }
+Tw tw_fwd() { const TwHost& t = cur_tw().bb; return Tw{t.d_small_f, t.d_lo_f, t.d_hi_f}; }
+Tw tw_inv() { const TwHost& t = cur_tw().bb; return Tw{t.d_small_i, t.d_lo_i, t.d_hi_i}; }
+PlkTwTables to_tables(const TwHost& t) {
+  return PlkTwTables{t.d_small_f, t.d_small_i, t.d_lo_f, t.d_hi_f, t.d_lo_i, t.d_hi_i};
+}
+void free_tw(TwHost& t) {
+  for (uint32_t* p : {t.d_small_f, t.d_small_i, t.d_lo_f, t.d_hi_f, t.d_lo_i, t.d_hi_i}) (void)hipFree(p);
+  t = TwHost{};
+}
 
 }  // namespace
 
-static struct {
-  uint32_t *d_small_f = nullptr, *d_small_i = nullptr, *d_lo_f = nullptr, *d_hi_f = nullptr, *d_lo_i = nullptr,
-           *d_hi_i = nullptr;
-} g_tw29;
-
-PlkTwTables plk_ntt_tables29(void) {
-  return PlkTwTables{g_tw29.d_small_f, g_tw29.d_small_i, g_tw29.d_lo_f, g_tw29.d_hi_f, g_tw29.d_lo_i, g_tw29.d_hi_i};
+int plk_cur_device(void) {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= PLK_MAX_DEVICES) d = 0;
+  return d;
 }
 
-PlkTwTables plk_ntt_tables(void) {
-  return PlkTwTables{g_tw.d_small_f, g_tw.d_small_i, g_tw.d_lo_f, g_tw.d_hi_f, g_tw.d_lo_i, g_tw.d_hi_i};
-}
+PlkTwTables plk_ntt_tables29(void) { return to_tables(cur_tw().f29); }
+PlkTwTables plk_ntt_tables(void) { return to_tables(cur_tw().bb); }
 
+// the tables of the CURRENT device (idempotent per device)
 int plk_ntt_init_tables(void) {
-  if (g_tw.d_small_f) return PLK_OK;
+  const int dev = plk_cur_device();
+  TwHost& T = g_tw[dev].bb;
+  TwHost& T29 = g_tw[dev].f29;
+  if (T.d_small_f) return PLK_OK;
   // tiles of 2^12 rows with two arrays exceed the default 64 KB dynamic-LDS limit
   const int lds_max = 150 * 1024;   // leaves room for the kernels' static LDS
   PLK_HIP(hipFuncSetAttribute((const void*)polymul_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
@@ -429,6 +444,11 @@ int plk_ntt_init_tables(void) {
       y = y * si2 % bb::P;
     }
   }
+  auto up = [](uint32_t** d, const std::vector<uint32_t>& h) -> int {
+    PLK_HIP(hipMalloc((void**)d, h.size() * 4));
+    PLK_HIP(hipMemcpy(*d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    return PLK_OK;
+  };
   {
     // F29 tables, same layouts (root of order 2^26; hi holds 2^14 entries)
     const uint32_t w26 = f29::hpow(f29::GENERATOR, (f29::P - 1) >> f29::TWO_ADICITY);
@@ -461,39 +481,46 @@ int plk_ntt_init_tables(void) {
       x = x * st4 % f29::P;
       y = y * st4i % f29::P;
     }
-    auto up2 = [](uint32_t** d, const std::vector<uint32_t>& h) -> int {
-      PLK_HIP(hipMalloc((void**)d, h.size() * 4));
-      PLK_HIP(hipMemcpy(*d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-      return PLK_OK;
-    };
     int rc2;
-    if ((rc2 = up2(&g_tw29.d_small_f, sf2)) || (rc2 = up2(&g_tw29.d_small_i, si2)) || (rc2 = up2(&g_tw29.d_lo_f, lf2)) ||
-        (rc2 = up2(&g_tw29.d_hi_f, hf2)) || (rc2 = up2(&g_tw29.d_lo_i, li2)) || (rc2 = up2(&g_tw29.d_hi_i, hi2)))
+    if ((rc2 = up(&T29.d_small_f, sf2)) || (rc2 = up(&T29.d_small_i, si2)) || (rc2 = up(&T29.d_lo_f, lf2)) ||
+        (rc2 = up(&T29.d_hi_f, hf2)) || (rc2 = up(&T29.d_lo_i, li2)) || (rc2 = up(&T29.d_hi_i, hi2))) {
+      free_tw(T29);
       return rc2;
+    }
   }
   uint32_t m17[17];
   for (int v = 0; v < 17; v++) m17[v] = bb::to_mont((uint32_t)v);
-  PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_mont17), m17, sizeof m17));
-  auto up = [](uint32_t** d, const std::vector<uint32_t>& h) -> int {
-    PLK_HIP(hipMalloc((void**)d, h.size() * 4));
-    PLK_HIP(hipMemcpy(*d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-    return PLK_OK;
-  };
+  PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_mont17), m17, sizeof m17));   // (per device: this one)
+  TwHost t{};
   int rc;
-  if ((rc = up(&g_tw.d_small_f, sf)) || (rc = up(&g_tw.d_small_i, si)) || (rc = up(&g_tw.d_lo_f, lf)) ||
-      (rc = up(&g_tw.d_hi_f, hf)) || (rc = up(&g_tw.d_lo_i, li)) || (rc = up(&g_tw.d_hi_i, hi_)))
+  if ((rc = up(&t.d_small_f, sf)) || (rc = up(&t.d_small_i, si)) || (rc = up(&t.d_lo_f, lf)) ||
+      (rc = up(&t.d_hi_f, hf)) || (rc = up(&t.d_lo_i, li)) || (rc = up(&t.d_hi_i, hi_))) {
+    free_tw(t);
+    free_tw(T29);
     return rc;
-  return plk_wave_init_coltabs();
+  }
+  T = t;   // (the column tables are built from the root tables of this device)
+  if ((rc = plk_wave_init_coltabs())) {
+    plk_wave_free_coltabs();
+    free_tw(T);   // d_small_f marks the device's tables complete: only with its column tables
+    free_tw(T29);
+    return rc;
+  }
+  return PLK_OK;
 }
 
+// every device's tables (the current device is restored)
 void plk_ntt_free_tables(void) {
-  (void)hipFree(g_tw.d_small_f); (void)hipFree(g_tw.d_small_i); (void)hipFree(g_tw.d_lo_f);
-  (void)hipFree(g_tw.d_hi_f); (void)hipFree(g_tw.d_lo_i); (void)hipFree(g_tw.d_hi_i);
-  (void)hipFree(g_tw29.d_small_f); (void)hipFree(g_tw29.d_small_i); (void)hipFree(g_tw29.d_lo_f);
-  (void)hipFree(g_tw29.d_hi_f); (void)hipFree(g_tw29.d_lo_i); (void)hipFree(g_tw29.d_hi_i);
-  g_tw29.d_small_f = g_tw29.d_small_i = g_tw29.d_lo_f = g_tw29.d_hi_f = g_tw29.d_lo_i = g_tw29.d_hi_i = nullptr;
-  g_tw = TwHost{};
-  plk_wave_free_coltabs();
+  const int prev = plk_cur_device();
+  for (int d = 0; d < PLK_MAX_DEVICES; d++) {
+    DevTw& t = g_tw[d];
+    if (!t.bb.d_small_f && !t.f29.d_small_f) continue;
+    (void)hipSetDevice(d);
+    free_tw(t.bb);
+    free_tw(t.f29);
+    plk_wave_free_coltabs();
+  }
+  (void)hipSetDevice(prev);
 }
 
 static int log2_ceil(uint64_t v) {

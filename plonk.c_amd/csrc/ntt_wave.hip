@@ -997,8 +997,9 @@ int wave_plan(int k, int TB, int* Ms) {
 #define PLK_NTT_COLT_MIN_K 13   // smallest transform using a column table (tuning: larger = lo * hi products)
 #endif
 constexpr int COLT_MIN_K = 13, COLT_MAX_K = 23;
-uint32_t* g_col[2][COLT_MAX_K + 1] = {};
-uint32_t* g_coli[2][COLT_MAX_K + 1] = {};   // the same times the product's final scale (ntt.hip's ninv)
+// per device (plk_cur_device: the calling thread's current device)
+uint32_t* g_col[PLK_MAX_DEVICES][2][COLT_MAX_K + 1] = {};
+uint32_t* g_coli[PLK_MAX_DEVICES][2][COLT_MAX_K + 1] = {};   // the same times the product's final scale (ntt.hip's ninv)
 
 WTw to_wtw(const PlkTwTables& t, bool inv) {
   return inv ? WTw{t.small_i, t.lo_i, t.hi_i, nullptr} : WTw{t.small_f, t.lo_f, t.hi_f, nullptr};
@@ -1008,14 +1009,15 @@ template <class F>
 WTw fwd_wtw(int k) {
   const bool f29 = F::ADIC == f29::TWO_ADICITY;
   WTw w = to_wtw(f29 ? plk_ntt_tables29() : plk_ntt_tables(), false);
-  w.col = (k >= PLK_NTT_COLT_MIN_K && k >= COLT_MIN_K && k <= COLT_MAX_K) ? g_col[f29 ? 1 : 0][k] : nullptr;
+  w.col = (k >= PLK_NTT_COLT_MIN_K && k >= COLT_MIN_K && k <= COLT_MAX_K) ? g_col[plk_cur_device()][f29 ? 1 : 0][k]
+                                                                          : nullptr;
   return w;
 }
 // the same for a product's last inverse pass: the scaled column table
 template <class F>
 WTw inv_wtw(int k) {
   WTw w = fwd_wtw<F>(k);
-  if (w.col) w.col = g_coli[F::ADIC == f29::TWO_ADICITY ? 1 : 0][k];
+  if (w.col) w.col = g_coli[plk_cur_device()][F::ADIC == f29::TWO_ADICITY ? 1 : 0][k];
   return w;
 }
 
@@ -1308,7 +1310,8 @@ int build_coltabs(int fi) {
     const uint32_t ninv = fi ? (uint32_t)((uint64_t)f29::hpow(1ull << k, f29::P - 2) * f29::R2 % f29::P)
                              : (uint32_t)((uint64_t)bb::hpow(1ull << k, bb::P - 2) * bb::R2 % bb::P);
     for (int s = 0; s < 2; s++) {
-      uint32_t*& t = s ? g_coli[fi][k] : g_col[fi][k];
+      const int dev = plk_cur_device();
+      uint32_t*& t = s ? g_coli[dev][fi][k] : g_col[dev][fi][k];
       if (t) continue;
       PLK_HIP(hipMalloc((void**)&t, 4ull << k));
       const WTw tw = to_wtw(fi ? plk_ntt_tables29() : plk_ntt_tables(), false);
@@ -1331,8 +1334,10 @@ int plk_wave_init_coltabs(void) {
   if (!rc) PLK_HIP(hipDeviceSynchronize());
   return rc;
 }
+// the current device's column tables
 void plk_wave_free_coltabs(void) {
-  for (auto* g : {&g_col, &g_coli})
+  const int dev = plk_cur_device();
+  for (auto* g : {&g_col[dev], &g_coli[dev]})
     for (auto& f : *g)
       for (auto& t : f) {
         (void)hipFree(t);

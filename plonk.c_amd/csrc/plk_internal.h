@@ -19,6 +19,7 @@ static_assert(offsetof(plk_msm_result_t, log) == 8 && offsetof(plk_msm_result_t,
 void plk_set_error(const char* fmt, ...);
 int plk_ctx_retain(void);    // a device prover is alive (capi.hip): plk_shutdown keeps the tables
 void plk_ctx_release(void);
+int plk_ctx_prepare_device(int dev);   // kernel tables on a further device (helper provers)
 int64_t plk_opt(int opt);    // current value of a PLK_OPT_* option (capi.hip)
 
 #define PLK_HIP(call)                                                                    \
@@ -32,6 +33,8 @@ int64_t plk_opt(int opt);    // current value of a PLK_OPT_* option (capi.hip)
 
 // shards.hip: in-process multi-device plk_msm_g1 (plk_init_devices); callers hold the library lock
 #define PLK_MAX_SHARDS 16
+#define PLK_MAX_DEVICES 64   // device ids with their own NTT tables (ntt.hip)
+int plk_cur_device(void);   // the calling thread's current HIP device (0 on error)
 // lanes: the entries all name the primary device and stand for host threads of the single-device
 // plk_msm_g1 (PLK_OPT_MSM_HOST_LANES), not a plk_init_devices list (plk_devices reports one device)
 int plk_shards_setup(const int* ids, int n, const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101,

@@ -25,6 +25,7 @@
 #include <initializer_list>
 #include <tuple>
 #include <utility>
+#include <string>
 #include <vector>
 
 #include "plk_device.h"
@@ -1170,6 +1171,20 @@ struct plk_prover {
     int k = 0, field = -1;
   } fix[13];
   uint32_t* fix_mem = nullptr;
+  // the device of this prover's memory and stream (a helper may live on another GPU)
+  int dev = 0;
+  // one proof over several GPUs from C (plk_prover_attach_helpers): helper provers on further
+  // entries of the plk_init_devices list compute round 3's t_2 / t_3 chains; their products land
+  // in rx[] on this device (hipMemcpyPeerAsync on the helper's stream, then its ev_done)
+  int nhelp = 0;
+  plk_prover* help[2] = {nullptr, nullptr};
+  int help_mask[2] = {0, 0};
+  uint8_t* rx_mem = nullptr;
+  uint8_t* rx[2] = {nullptr, nullptr};   // received t_2, t_3 (plk_prover_chain_bytes each)
+  hipEvent_t ev_in = nullptr;            // recorded on st before the helpers start: the inputs are there
+  // as a helper on another device: its copies of the 7 input polynomials it reads
+  uint8_t* hin = nullptr;
+  hipEvent_t ev_done = nullptr;          // (helper's device) its products have reached the proving device
 };
 
 namespace {
@@ -1395,11 +1410,16 @@ int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs, const Lc
   return PLK_OK;
 }
 
-}  // namespace
+// restores the calling thread's current device on scope exit
+struct DevGuard {
+  int prev;
+  DevGuard() : prev(plk_cur_device()) {}
+  ~DevGuard() { (void)hipSetDevice(prev); }
+};
 
-extern "C" {
-
-int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
+// plk_prover_create on device `dev` (the library's primary, or a helper's GPU whose tables
+// plk_ctx_prepare_device built); the caller's current device is restored
+int create_on(const plk_plonk_desc_t* d, int dev, plk_prover_t** out) {
   if (!d || !out) { plk_set_error("plk_prover_create: NULL argument"); return PLK_ERR_ARG; }
   *out = nullptr;
   if (d->n == 0 || !d->z_h || d->z_h_len == 0 || !d->srs_g1 || d->srs_len == 0) {
@@ -1408,7 +1428,18 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   }
   int rc = plk_ctx_retain();
   if (rc) return rc;
+  if (dev >= 0 && (rc = plk_ctx_prepare_device(dev))) {
+    plk_ctx_release();
+    return rc;
+  }
+  DevGuard dg;
+  if (dev >= 0 && hipSetDevice(dev) != hipSuccess) {
+    plk_ctx_release();
+    plk_set_error("plk_prover_create: hipSetDevice(%d) failed", dev);
+    return PLK_ERR_HIP;
+  }
   plk_prover* P = new plk_prover();
+  P->dev = plk_cur_device();
   P->n = d->n;
   P->srs_len = d->srs_len;
   // Z_H: trimmed as poly_z returns it; classify
@@ -1495,6 +1526,8 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   P->st = nullptr;
   hipError_t e = hipStreamCreateWithFlags(&P->st, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_in, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_done, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMemsetAsync(P->mem, 0, P->mem_bytes, P->st);
   if (e == hipSuccess) e = hipMemcpyAsync(P->d_srs, d->srs_g1, 3 * P->srs_len, hipMemcpyHostToDevice, P->st);
   if (e == hipSuccess) e = hipMemcpyAsync(P->d_zh, d->z_h, zl, hipMemcpyHostToDevice, P->st);
@@ -1530,13 +1563,26 @@ int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) {
   return PLK_OK;
 }
 
+void detach_helpers(plk_prover* P);
+
+}  // namespace
+
+extern "C" {
+
+int plk_prover_create(const plk_plonk_desc_t* d, plk_prover_t** out) { return create_on(d, -1, out); }
+
 void plk_prover_destroy(plk_prover_t* P) {
   if (!P) return;
+  detach_helpers(P);
+  DevGuard dg;
+  (void)hipSetDevice(P->dev);
   if (P->st) (void)hipStreamSynchronize(P->st);
   (void)hipFree(P->mem);
   if (P->h_res) (void)hipHostFree(P->h_res);
   (void)hipFree(P->fix_mem);
-  if (P->ev) (void)hipEventDestroy(P->ev);
+  (void)hipFree(P->hin);
+  for (hipEvent_t e : {P->ev, P->ev_in, P->ev_done})
+    if (e) (void)hipEventDestroy(e);
   if (P->st) (void)hipStreamDestroy(P->st);
   delete P;
   plk_ctx_release();
@@ -1556,7 +1602,7 @@ namespace {
 struct RoundsMode {
   int ext = 0;                          // chains (PLK_CHAIN_*) whose products come from t2 / t3
   const uint8_t *t2 = nullptr, *t3 = nullptr;
-  hipEvent_t ready = nullptr;           // the stream waits for it before reading t2 / t3
+  hipEvent_t ready[2] = {nullptr, nullptr};   // the stream waits for them before reading t2 / t3
   int only = 0;                         // helper: just these chains (into o2 / o3), then return
   uint8_t *o2 = nullptr, *o3 = nullptr;
 };
@@ -1717,7 +1763,8 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   }
   const uint8_t* const T2 = (md.ext & PLK_CHAIN_T2) ? md.t2 : P->T2;
   const uint8_t* const T3 = (md.ext & PLK_CHAIN_T3) ? md.t3 : P->T3;
-  if (md.ext && md.ready) PLK_HIP(hipStreamWaitEvent(P->st, md.ready, 0));   // their bytes have arrived
+  for (hipEvent_t e : md.ready)   // their bytes have arrived (the only wait of a split proof)
+    if (md.ext && e) PLK_HIP(hipStreamWaitEvent(P->st, e, 0));
   // t(x) = numerator / Z_H; t_lo / t_mid / t_hi = poly_slice(t_x, ...) with part n + 2
   // (src/plonk.h:494-519)
   const uint64_t part = n + 2;
@@ -1885,6 +1932,99 @@ int finish(plk_prover* P, int strict, int circuit, uint8_t proof[34]) {
   return PLK_OK;
 }
 
+// ---- one proof over several GPUs from C (plk_prover_attach_helpers)
+// the d_polys entries a helper's chains read: f_a f_b f_c s_sigma_1..3 acc_x (rounds(): prep_kernel
+// or its fallback; md.only returns before anything else is read)
+constexpr int HELPER_IN[7] = {0, 1, 2, 8, 9, 10, 11};
+
+size_t hin_stride(uint64_t n) { return (n + 16 + 255) & ~(size_t)255; }
+
+void detach_helpers(plk_prover* P) {
+  for (int h = 0; h < P->nhelp; h++) {
+    plk_prover_destroy(P->help[h]);
+    P->help[h] = nullptr;
+    P->help_mask[h] = 0;
+  }
+  P->nhelp = 0;
+  if (P->rx_mem) {
+    DevGuard dg;
+    (void)hipSetDevice(P->dev);
+    (void)hipStreamSynchronize(P->st);
+    (void)hipFree(P->rx_mem);
+  }
+  P->rx_mem = nullptr;
+  P->rx[0] = P->rx[1] = nullptr;
+}
+
+// Rounds 1-5 with the helpers' chains.  Ordering: P->st records ev_in after
+// everything already enqueued on it (a circuit's stage A; nothing for device-resident inputs);
+// each helper's stream waits for ev_in, copies the 7 inputs it reads to its own device when it
+// is another GPU (hipMemcpyPeerAsync), runs its chains, copies the products into P->rx on the
+// proving device (hipMemcpyPeerAsync on the helper's stream) and records ev_done; P's stream
+// runs everything else and waits for the ev_done events only before the numerator.
+int rounds_split(plk_prover* P, const uint8_t* const* pl, const uint8_t* const* hpl, const uint8_t chal[5],
+                 const uint8_t rnd[9], bool pre) {
+  DevGuard dg;
+  PLK_HIP(hipSetDevice(P->dev));
+  PLK_HIP(hipEventRecord(P->ev_in, P->st));
+  const Lens L = lens_for(P->n, P->zh_len);
+  const uint64_t clen[2] = {L.l2 + 16, L.l3 + 16};   // (the numerator reads whole dwords, masked)
+  RoundsMode md;
+  int rc = PLK_OK;
+  for (int h = 0; h < P->nhelp && !rc; h++) {
+    plk_prover* H = P->help[h];
+    if (hipSetDevice(H->dev) != hipSuccess || hipStreamWaitEvent(H->st, P->ev_in, 0) != hipSuccess) {
+      plk_set_error("split proof: helper %d (device %d) cannot wait for the inputs", h, H->dev);
+      rc = PLK_ERR_HIP;
+      break;
+    }
+    const uint8_t* hp[13];
+    for (int i = 0; i < 13; i++) hp[i] = hpl ? hpl[13 * (h + 1) + i] : pl[i];
+    if (!hpl && H->dev != P->dev) {   // the inputs it reads, from the proving device
+      const size_t st = hin_stride(P->n);
+      for (int q = 0; q < 7 && !rc; q++) {
+        uint8_t* dst = H->hin + q * st;
+        if (hipMemcpyPeerAsync(dst, H->dev, pl[HELPER_IN[q]], P->dev, P->n, H->st) != hipSuccess) {
+          plk_set_error("split proof: input copy to device %d failed", H->dev);
+          rc = PLK_ERR_HIP;
+        }
+        hp[HELPER_IN[q]] = dst;
+      }
+      if (rc) break;
+    }
+    RoundsMode hm;
+    hm.only = P->help_mask[h];
+    hm.o2 = H->T2;
+    hm.o3 = H->T3;
+    if ((rc = rounds(H, hp, chal, rnd, false, hm))) break;
+    for (int c = 0; c < 2 && !rc; c++) {
+      if (!(hm.only & (1 << c))) continue;
+      const uint8_t* src = c ? H->T3 : H->T2;
+      const hipError_t e = H->dev == P->dev
+                               ? hipMemcpyAsync(P->rx[c], src, clen[c], hipMemcpyDeviceToDevice, H->st)
+                               : hipMemcpyPeerAsync(P->rx[c], P->dev, src, H->dev, clen[c], H->st);
+      if (e != hipSuccess) {
+        plk_set_error("split proof: product copy from device %d failed: %s", H->dev, hipGetErrorString(e));
+        rc = PLK_ERR_HIP;
+      }
+    }
+    if (!rc && hipEventRecord(H->ev_done, H->st) != hipSuccess) rc = PLK_ERR_HIP;
+    md.ready[h] = H->ev_done;
+    md.ext |= hm.only;
+  }
+  if (rc) {
+    for (int h = 0; h < P->nhelp; h++) {
+      (void)hipSetDevice(P->help[h]->dev);
+      (void)hipStreamSynchronize(P->help[h]->st);
+    }
+    return rc;
+  }
+  PLK_HIP(hipSetDevice(P->dev));
+  md.t2 = P->rx[0];
+  md.t3 = P->rx[1];
+  return rounds(P, pl, chal, rnd, pre, md);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1894,7 +2034,94 @@ int plk_prover_rounds_dev(plk_prover_t* P, const uint8_t* const d_polys[13], con
   if (!P || !d_polys || !chal || !rand9) { plk_set_error("plk_prover_rounds_dev: NULL argument"); return PLK_ERR_ARG; }
   for (int i = 0; i < 13; i++)
     if (!d_polys[i]) { plk_set_error("plk_prover_rounds_dev: polynomial %d is NULL", i); return PLK_ERR_ARG; }
-  int rc = rounds(P, d_polys, chal, rand9, (flags & PLK_PROVE_PREPROCESSED) != 0);
+  const bool pre = (flags & PLK_PROVE_PREPROCESSED) != 0;
+  int rc = P->nhelp ? rounds_split(P, d_polys, nullptr, chal, rand9, pre) : rounds(P, d_polys, chal, rand9, pre);
+  if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
+  return finish(P, (flags & PLK_PROVE_STRICT) != 0, 0, proof);
+}
+
+int plk_prover_attach_helpers(plk_prover_t* P, int k) {
+  if (!P || k < 0 || k > 2) { plk_set_error("plk_prover_attach_helpers: prover and 0 <= k <= 2 required"); return PLK_ERR_ARG; }
+  if (P->dev != plk_cur_device()) {
+    plk_set_error("plk_prover_attach_helpers: call from the prover's device %d", P->dev);
+    return PLK_ERR_ARG;
+  }
+  detach_helpers(P);
+  if (!k) return PLK_OK;
+  int ids[PLK_MAX_SHARDS];
+  const int nd = plk_devices(ids, PLK_MAX_SHARDS);
+  if (nd < 1 + k) {
+    plk_set_error("plk_prover_attach_helpers: %d helper(s) need %d entries in the plk_init_devices list (it has %d)", k,
+                  1 + k, nd);
+    return PLK_ERR_ARG;
+  }
+  const Lens L = lens_for(P->n, P->zh_len);
+  // helpers need Z_H only (no SRS: they commit nothing): one identity point stands in
+  std::vector<uint8_t> zh(P->zh_len);
+  PLK_HIP(hipMemcpy(zh.data(), P->d_zh, P->zh_len, hipMemcpyDeviceToHost));
+  const uint8_t srs1[3] = {0, 0, 1};
+  plk_plonk_desc_t d{};
+  d.n = P->n;
+  d.z_h = zh.data();
+  d.z_h_len = zh.size();
+  d.srs_g1 = srs1;
+  d.srs_len = 1;
+  // chain_assignment (plonkhip/dist.py): one helper takes t_3 (the proving GPU keeps t_2 with its
+  // (a b) q_m sum group); two take t_2 and t_3
+  const int masks[2][2] = {{PLK_CHAIN_T3, 0}, {PLK_CHAIN_T2, PLK_CHAIN_T3}};
+  int rc = PLK_OK;
+  for (int h = 0; h < k && !rc; h++) {
+    plk_prover* H = nullptr;
+    if ((rc = create_on(&d, ids[1 + h], &H))) break;
+    P->help[P->nhelp] = H;
+    P->help_mask[P->nhelp++] = masks[k - 1][h];
+    if (H->dev != P->dev) {
+      DevGuard dg;
+      int can = 0;   // direct xGMI access both ways where the devices allow it (else staged copies)
+      if (hipDeviceCanAccessPeer(&can, H->dev, P->dev) == hipSuccess && can && hipSetDevice(H->dev) == hipSuccess)
+        (void)hipDeviceEnablePeerAccess(P->dev, 0);
+      if (hipDeviceCanAccessPeer(&can, P->dev, H->dev) == hipSuccess && can && hipSetDevice(P->dev) == hipSuccess)
+        (void)hipDeviceEnablePeerAccess(H->dev, 0);
+      (void)hipGetLastError();   // (already enabled is not an error here)
+      if (hipSetDevice(H->dev) != hipSuccess || hipMalloc((void**)&H->hin, 7 * hin_stride(P->n)) != hipSuccess) {
+        H->hin = nullptr;
+        plk_set_error("plk_prover_attach_helpers: input buffers on device %d", H->dev);
+        rc = PLK_ERR_NOMEM;
+      }
+    }
+  }
+  if (!rc) {
+    const size_t b2 = (L.l2 + 64 + 255) & ~(size_t)255, b3 = (L.l3 + 64 + 255) & ~(size_t)255;
+    if (hipMalloc((void**)&P->rx_mem, b2 + b3) != hipSuccess) {
+      P->rx_mem = nullptr;
+      plk_set_error("plk_prover_attach_helpers: receive buffers");
+      rc = PLK_ERR_NOMEM;
+    } else {
+      P->rx[0] = P->rx_mem;
+      P->rx[1] = P->rx_mem + b2;
+    }
+  }
+  if (rc) {
+    const std::string why = plk_last_error();
+    detach_helpers(P);
+    plk_set_error("%s", why.c_str());
+  }
+  return rc;
+}
+
+int plk_prover_helpers(const plk_prover_t* P) { return P ? P->nhelp : 0; }
+
+int plk_prover_rounds_multi_dev(plk_prover_t* P, const uint8_t* const* d_polys, int ndev, const uint8_t chal[5],
+                                const uint8_t rand9[9], int flags, uint8_t proof[34]) {
+  if (!P || !d_polys || !chal || !rand9) { plk_set_error("plk_prover_rounds_multi_dev: NULL argument"); return PLK_ERR_ARG; }
+  if (ndev != 1 + P->nhelp) {
+    plk_set_error("plk_prover_rounds_multi_dev: %d input sets for 1 + %d devices", ndev, P->nhelp);
+    return PLK_ERR_ARG;
+  }
+  for (int i = 0; i < 13 * ndev; i++)
+    if (!d_polys[i]) { plk_set_error("plk_prover_rounds_multi_dev: polynomial %d of set %d is NULL", i % 13, i / 13); return PLK_ERR_ARG; }
+  const bool pre = (flags & PLK_PROVE_PREPROCESSED) != 0;
+  int rc = P->nhelp ? rounds_split(P, d_polys, d_polys, chal, rand9, pre) : rounds(P, d_polys, chal, rand9, pre);
   if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
   return finish(P, (flags & PLK_PROVE_STRICT) != 0, 0, proof);
 }
@@ -1958,7 +2185,7 @@ int plk_prover_rounds_ext_dev(plk_prover_t* P, const uint8_t* const d_polys[13],
   md.t3 = d_t3;
   if (which && !(PLK_DIAG_DROP_HANDOFF & 2)) {   // everything enqueued on `ready` so far (the bytes'
     PLK_HIP(hipEventRecord(P->ev, (hipStream_t)ready));   // arrival; NULL: the null stream) before they are read
-    md.ready = P->ev;
+    md.ready[0] = P->ev;
   }
   rc = rounds(P, d_polys, chal, rand9, (flags & PLK_PROVE_PREPROCESSED) != 0, md);
   if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
@@ -2065,7 +2292,7 @@ int plk_prover_prove(plk_prover_t* P, const plk_circuit_t* c, const uint8_t chal
 
   const uint8_t* pl[13];
   for (int i = 0; i < 13; i++) pl[i] = P->d_polys[i];
-  int rc = rounds(P, pl, chal, rand9);
+  int rc = P->nhelp ? rounds_split(P, pl, nullptr, chal, rand9, false) : rounds(P, pl, chal, rand9);
   if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
   return finish(P, 1, 1, proof);
 }

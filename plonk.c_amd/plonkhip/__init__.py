@@ -77,6 +77,9 @@ SIGNATURES = {
     "plk_init_devices": (C.c_int, [C.POINTER(C.c_int), C.c_int]),
     "plk_devices": (C.c_int, [C.POINTER(C.c_int), C.c_int]),
     "plk_get_option": (C.c_int64, [C.c_int]),
+    "plk_prover_attach_helpers": (C.c_int, [_vp, C.c_int]),
+    "plk_prover_helpers": (C.c_int, [_vp]),
+    "plk_prover_rounds_multi_dev": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, _u8p, _u8p, C.c_int, _u8p]),
 }
 
 # PLK_OPT_* (include/plonkhip.h), by the name without the prefix
@@ -561,6 +564,30 @@ class Prover:
         _check("plk_prover_rounds_ext_dev", lib().plk_prover_rounds_ext_dev(
             self._h, args[0], args[1], args[2], flags, int(which), _ptr(t2) if t2 is not None else None,
             _ptr(t3) if t3 is not None else None, _stream(ready), out))
+        return bytes(out)
+
+    # ---- the same split from C over the plk_init_devices list (plk_prover_attach_helpers)
+    def attach_helpers(self, k):
+        """k helper provers on entries 1..k of the plk_init_devices list (0 detaches); from then on
+        rounds_dev / prove run split (the chains on the helpers, products peer-copied back)"""
+        _check("plk_prover_attach_helpers", lib().plk_prover_attach_helpers(self._h, int(k)))
+
+    def helpers(self):
+        return int(lib().plk_prover_helpers(self._h))
+
+    def rounds_multi_dev(self, poly_sets, chal, rand, strict=False, preprocessed=False):
+        """poly_sets: 1 + helpers() lists of 13 device tensors, set h on helper h's device"""
+        ch, rd = _u8(chal).reshape(-1), _u8(rand).reshape(-1)
+        if ch.size != 5 or rd.size != 9:
+            raise ValueError("rounds_multi_dev: chal must hold 5 values and rand 9")
+        flat = [p for ps in poly_sets for p in ps]
+        if any(len(ps) != 13 for ps in poly_sets):
+            raise ValueError("rounds_multi_dev: 13 polynomials per set")
+        arr = (_vp * len(flat))(*[_ptr(p) for p in flat])
+        out = (C.c_uint8 * 34)()
+        flags = (PLK_PROVE_STRICT if strict else 0) | (PLK_PROVE_PREPROCESSED if preprocessed else 0)
+        _check("plk_prover_rounds_multi_dev", lib().plk_prover_rounds_multi_dev(
+            self._h, arr, len(poly_sets), _p(ch), _p(rd), flags, out))
         return bytes(out)
 
     def preprocess(self, polys):

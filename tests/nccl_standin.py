@@ -13,6 +13,15 @@ with the same ordering hazards:
 
 A consumer that does not order itself behind the current stream at the right point reads bytes
 that are not there yet -- exactly what a missing ready= / done= ordering would do over RCCL.
+
+Two things keep a missing ordering from being hidden by timing:
+* before each helper's step the current stream spins (`delay` cycles): the helper's chains start
+  behind it (plk_prover_chains_dev makes its stream wait for `done` first), and so does a send
+  with no ordering -- which then copies while the chains run instead of after them;
+* HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default), in order per
+  queue: two streams that share one serialise in submission order and hide any race between
+  them.  The negative test (tests/test_split_streams_gpu.py) runs in a child process with 16
+  queues, more than the streams it creates, so every stream has its own.
 """
 import torch
 
@@ -76,6 +85,7 @@ def split_proof(hip, n, polys, chal, rnd, zh, pts, world, comm=None):
         stream = torch.cuda.current_stream()
         torch.cuda.synchronize()
         for r in range(1, world):
+            torch.cuda._sleep(comm.delay)       # (see the module docstring)
             split_proof_step(provers[r], dev, chal, rnd, bufs[r], r, world, stream, via_host=False, comm=comm)
         got = split_proof_step(provers[0], dev, chal, rnd, bufs[0], 0, world, stream, via_host=False, comm=comm)
         torch.cuda.synchronize()

@@ -85,7 +85,7 @@ def test_options_without_gpu():
     import plonkhip as h
     defaults = {"TINY_CALLS": 1, "PROVE_SYNC": 0, "POLY_BLOCK_L": 0, "POLY_BLOCK_S": 0, "NTT_F29": 1,
                 "NTT_SHARE": 1, "NTT_SHARED_FIX": 1, "NTT_T13_MIN_K": 21, "NTT_CENTER_BLOCKS": 0,
-                "MSM_HALF": 1, "MSM_SHARD_MIN": 1 << 16, "NTT_CENTER_SUM": 1}
+                "MSM_HALF": 1, "MSM_SHARD_MIN": 1 << 16, "NTT_CENTER_SUM": 1, "MSM_HOST_LANES": 4}
     for k, v in defaults.items():
         assert h.get_option(k) == v, k
     with h.options(NTT_SHARED_FIX=2, POLY_BLOCK_L=4096, POLY_BLOCK_S=513):
@@ -102,6 +102,21 @@ def test_options_without_gpu():
         if f.endswith((".hip", ".h")):
             envs |= set(re.findall(r'getenv\("(\w+)"\)', open(os.path.join(csrc, f)).read()))
     assert envs == {"PLK_DEVICE"}
+
+
+def test_split_prover_exports_without_gpu():
+    """plk_prover_attach_helpers / plk_prover_helpers / plk_prover_rounds_multi_dev (one proof over
+    the plk_init_devices list from C) refuse a NULL prover and bad counts before touching a device"""
+    import ctypes as C
+
+    import plonkhip as h
+    lib = h.lib()
+    assert lib.plk_prover_attach_helpers(None, 1) == h.PLK_ERR_ARG
+    assert lib.plk_prover_attach_helpers(None, 3) == h.PLK_ERR_ARG
+    assert lib.plk_prover_helpers(None) == 0
+    chal, rnd, out = (C.c_uint8 * 5)(), (C.c_uint8 * 9)(), (C.c_uint8 * 34)()
+    polys = (C.c_void_p * 13)()
+    assert lib.plk_prover_rounds_multi_dev(None, polys, 1, chal, rnd, 0, out) == h.PLK_ERR_ARG
 
 
 def _gcc(args, **kw):
