@@ -21,7 +21,10 @@ Two things keep a missing ordering from being hidden by timing:
 * HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default), in order per
   queue: two streams that share one serialise in submission order and hide any race between
   them.  The negative test (tests/test_split_streams_gpu.py) runs in a child process with 16
-  queues, more than the streams it creates, so every stream has its own.
+  queues, more than the streams it creates, so every stream has its own;
+* a stream's FIRST use waits for all work on the device (measured, tools/stream_probe.py: its
+  hardware queue is created then), which would order a first send behind the chains: the side
+  stream and every prover's stream are used once before the checked proof.
 """
 import torch
 
@@ -41,6 +44,11 @@ class NcclSemantics:
         self.side = torch.cuda.Stream()
         self.delay = delay
         self.wire = {}          # dst rank -> [(staged tensor, event after its copy)], in send order
+        # a stream's first use waits for the whole device (HIP creates its hardware queue then:
+        # tools/stream_probe.py), which would order the first send / receive behind everything
+        with torch.cuda.stream(self.side):
+            torch.zeros(1, device="cuda").add_(1)
+        torch.cuda.synchronize()
 
     def send(self, t, dst, group=None):
         ev = torch.cuda.Event()
@@ -83,6 +91,8 @@ def split_proof(hip, n, polys, chal, rnd, zh, pts, world, comm=None):
         cb = {c: provers[0].chain_bytes(c) for c in (hip.PLK_CHAIN_T2, hip.PLK_CHAIN_T3)}
         bufs = [{c: torch.zeros(b, dtype=torch.uint8, device="cuda") for c, b in cb.items()} for _ in range(world)]
         stream = torch.cuda.current_stream()
+        for p in provers:                      # every prover's stream used once (module docstring)
+            p.rounds_dev(dev, chal, rnd)
         torch.cuda.synchronize()
         for r in range(1, world):
             torch.cuda._sleep(comm.delay)       # (see the module docstring)
