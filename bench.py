@@ -317,6 +317,7 @@ def components(torch, hip, dev, st, want):
         out["prove_2^20_gates"] = prove_component(torch, hip, dev, 20)
         out["prove_2^20_gates_preprocessed"] = prove_component(torch, hip, dev, 20, preprocessed=True)
         out["prove_2^20_gates_split_pieces"] = prove_split_pieces(torch, hip, dev, 20)
+        out["prove_2^20_gates_c_split_rehearsal"] = prove_c_split_rehearsal(torch, hip, dev, 20)
     return out
 
 
@@ -691,6 +692,40 @@ def prove_split_pieces(torch, hip, dev, log2n, reps=5):
                    "same inputs, to completion; the multi-GPU time adds the chain products' transfer "
                    "(chain_bytes each) where it is not hidden behind rank 0's own work"}
     pr.close()
+    return out
+
+
+def prove_c_split_rehearsal(torch, hip, dev, log2n, reps=5):
+    """The split proof driven from C (plk_prover_attach_helpers over the plk_init_devices list) on
+    ONE GPU: lists repeating device 0 put the helper provers on their own streams of the same
+    device, so this times the code path and checks its bytes, not a speed-up (the helpers compete
+    with the proving prover for the same CUs).  Distinct GPUs: tools/devices_probe.py on
+    multi-GPU nodes (components.host_call_msm_2^22_devices.all_devices.prove_2^20_split_from_c)."""
+    n = 1 << log2n
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import gen
+    hpolys, chal, rnd, zh, pts = gen.prove_instance(n, 51, 2 * n + 8)
+    polys = [torch.from_numpy(p).to(dev) for p in hpolys]
+    pr = hip.Prover(n, zh, pts)
+    out = {"note": "one GPU: helpers on their own streams of device 0 (plk_init_devices [0,0] / [0,0,0]); "
+                   "a correctness rehearsal of the C-side split, the helpers share the proving GPU"}
+    try:
+        for k in (1, 2):
+            hip.init_devices([0] * (1 + k))
+            pr.attach_helpers(k)
+            pr.rounds_dev(polys, chal, rnd)
+            t = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                o = pr.rounds_dev(polys, chal, rnd)
+                t.append(time.perf_counter() - t0)
+            t.sort()
+            out["devices_%d" % (1 + k)] = {"median_ms": round(t[len(t) // 2] * 1e3, 3),
+                                           "matches_oracle": _prove_golden(n, o)}
+            pr.attach_helpers(0)
+    finally:
+        hip.init_devices([0])
+        pr.close()
     return out
 
 
