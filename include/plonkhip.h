@@ -82,7 +82,8 @@ enum {
   PLK_OPT_MSM_HOST_LANES = 17,   /* one device: plk_msm_g1 of >= MSM_SHARD_MIN points runs its SRS memcmp,
                                     staging and uploads on this many host threads (1: one); read by
                                     plk_init / plk_init_devices */
-  PLK_OPT_COUNT = 18
+  PLK_OPT_PROVE_DERIVE_T2A = 18, /* 1: round 3's A2 B2 from a_x b_x by an elementwise pass (0: its own product) */
+  PLK_OPT_COUNT = 19
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
 int64_t plk_get_option(int opt);              /* -1 for an unknown option */

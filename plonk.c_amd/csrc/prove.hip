@@ -297,6 +297,44 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a, const SlotFile f,
   }
 }
 
+// Round 3's A2 B2 = alpha (a + gamma + beta x)(b + gamma + beta k1 x) (src/plonk.h:409-434) without a
+// product of its own: distributing over GF(17),
+//   A2 B2 = alpha (ab + gamma (a + b) + beta k1 x a + beta x b + (gamma + beta x)(gamma + beta k1 x)),
+// an elementwise pass over a b (round 3's own a_x b_x product) and a, b with a shift of one --
+// the same bytes as the 2^(k+1)-point product it replaces (the derived form is exact mod 17).
+// 4 coefficients per thread; every pointer 4-byte aligned (prover-internal buffers).
+__global__ __launch_bounds__(256) void t2a_kernel(const uint8_t* __restrict__ ab, const uint8_t* __restrict__ a,
+                                                  const uint8_t* __restrict__ b, uint64_t la, uint64_t lab,
+                                                  const uint8_t* __restrict__ S, uint8_t* __restrict__ out) {
+  const uint32_t al = S[S_ALPHA], be = S[S_BETA], ga = S[S_GAMMA], bk1 = S[S_BK1];
+  const uint32_t K[3] = {ga * ga, ga * (bk1 + be), be * bk1};   // (gamma + beta x)(gamma + beta k1 x)
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < lab; i += stride) {
+    const uint32_t wab = load4(ab, lab, i);
+    uint32_t wa = 0, wb = 0, pa = 0, pb = 0;   // a[i..i+3], b[i..i+3], a[i-1], b[i-1]
+    if (i <= la) {                             // (a, b and their shifts vanish past index la)
+      wa = load4(a, la, i);
+      wb = load4(b, la, i);
+      if (i) {
+        pa = load4(a, la, i - 4) >> 24;
+        pb = load4(b, la, i - 4) >> 24;
+      }
+    }
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int sh = 8 * k;
+      const uint32_t ak = (wa >> sh) & 0xFFu, bk = (wb >> sh) & 0xFFu;
+      const uint32_t am = k ? (wa >> (sh - 8)) & 0xFFu : pa, bm = k ? (wb >> (sh - 8)) & 0xFFu : pb;
+      const uint64_t j = i + k;
+      // (hmod bound: 16 + 16 * 32 + 2 * 16 * 16 + 289 < 69632)
+      const uint32_t v = ((wab >> sh) & 0xFFu) + ga * (ak + bk) + bk1 * am + be * bm + (j < 3 ? K[j] : 0u);
+      o |= hmod(hmod(v) * al) << sh;
+    }
+    store4(out, lab, i, o);
+  }
+}
+
 // several independent lincombs in one launch (blockIdx.y = which), all 16-byte aligned
 constexpr int LCB_MAX = 8;
 struct LcBatch {
@@ -1717,8 +1755,11 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     // re-associated as (A2 B2)(C2 z): C2 z and C3 z(omega x) join this batch and the 4n products
     // come in one batch (associativity over GF(17); the centered F29 residues hold the 2n x 2n
     // products exactly)
+    // A2 B2 from a_x b_x when this call computes that product (t2a_kernel after this batch; a
+    // helper computing only the chains keeps the product)
+    const bool derive_t2a = (local & PLK_CHAIN_T2) && !md.only && plk_opt(PLK_OPT_PROVE_DERIVE_T2A);
     if (local & PLK_CHAIN_T2) {
-      g1.push_back({{P->A2, L.la, P->B2, L.la, P->T2a}, -1});
+      if (!derive_t2a) g1.push_back({{P->A2, L.la, P->B2, L.la, P->T2a}, -1});
       g1.push_back({{P->C2, L.la, cZ, L.lzx, P->T2b}, -1});
     }
     if (local & PLK_CHAIN_T3) {
@@ -1758,6 +1799,12 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
       std::vector<PlkPolyMulJob> jobs;
       for (const J& x : *g) jobs.push_back(x.j);
       if (!jobs.empty()) RC(plk_poly_mul_batch_launch(jobs.data(), (int)jobs.size(), P->work, P->work_bytes, P->st));
+      if (g == &g1 && derive_t2a) {   // (a_x b_x is complete on the stream here)
+        const uint64_t blocks = std::min<uint64_t>((L.lab + 1023) / 1024, 4096);
+        hipLaunchKernelGGL(t2a_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, P->AB, cA, cB,
+                           L.la, L.lab, dS, P->T2a);
+        PLK_HIP(hipGetLastError());
+      }
     }
     if (md.only) return PLK_OK;   // helper: the chains' products are enqueued
   }
