@@ -83,7 +83,8 @@ enum {
                                     staging and uploads on this many host threads (1: one); read by
                                     plk_init / plk_init_devices */
   PLK_OPT_PROVE_DERIVE_T2A = 18, /* 1: round 3's A2 B2 from a_x b_x by an elementwise pass (0: its own product) */
-  PLK_OPT_COUNT = 19
+  PLK_OPT_NTT_TABLE_SHARE = 19,  /* 1: a table pass runs several arrays of one tile per block (column words read once) */
+  PLK_OPT_COUNT = 20
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
 int64_t plk_get_option(int opt);              /* -1 for an unknown option */

@@ -606,12 +606,14 @@ __device__ __forceinline__ void load_pass_tw_pairs(uint32_t* Tsm, const uint32_t
 
 }  // namespace
 
-// Forward (DIF) pass over a batch's distinct arrays (blockIdx.y = array), u32 in place, or
-// the first pass reading bytes (zero padded, reduced mod 17, to Montgomery).
+// Forward (DIF) pass over a batch's distinct arrays, u32 in place, or the first pass reading
+// bytes (zero padded, reduced mod 17, to Montgomery).  Block (x, y) runs tile x of arrays
+// y apa .. y apa + apa - 1 (< na) one after another: the arrays' column factors at a tile are the
+// same words, so they are loaded once per block (and the stage twiddles too).
 // COLT: the column factors come from tw.col (one word per element, indexed like the data)
 // instead of lo * hi (two words and a multiply per element).
 template <int TB, int R, int M, bool FROM_U8, class F, bool COLT = false>
-__global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, WTw tw) {
+__global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, WTw tw, int na, int apa) {
   using G = Eng<TB, R, M, F>;
   static_assert(G::NT == wt_nt(TB), "tile block size");
   constexpr bool PW = F::ADIC == f29::TWO_ADICITY;   // {w, p - w} pairs (F29's lazy DIF)
@@ -619,36 +621,38 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
   __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
-  const WArr& ar = arrs.a[blockIdx.y];
-  uint32_t* d = ar.d;
-  const uint8_t* s8 = ar.s8;
-  const uint64_t ls = ar.ls;
 
   // uniform tile base pointers, 32-bit element offsets
   const uint64_t tb = G::tbase(p, tile);
-  uint32_t* dt = d + tb;
   const uint32_t* colt = COLT ? tw.col + tb : nullptr;
   const uint32_t b0 = G::template base_q<0>(tid, false);
   const uint32_t o0 = G::toff(p, b0);
-  uint32_t v[G::E];
-  const TileBuf bd(dt);
-  if constexpr (FROM_U8) {
-    // raw bytes now (0 past the operand: the buffer's range ends there), their values through
-    // an LDS table after the barrier
-    const uint32_t lim = ls > tb ? (uint32_t)(ls - tb < 0xFFFFFFFFull ? ls - tb : 0xFFFFFFFFull) : 0u;
-    const TileBuf bs(s8 + tb, lim);
+  // this thread's elements of array ai: raw bytes (0 past the operand: the buffer's range ends
+  // there; their values through an LDS table after the barrier) or words
+  auto load = [&](int ai, uint32_t (&v)[G::E]) {
+    const WArr& ar = arrs.a[ai];
+    if constexpr (FROM_U8) {
+      const uint64_t ls = ar.ls;
+      const uint32_t lim = ls > tb ? (uint32_t)(ls - tb < 0xFFFFFFFFull ? ls - tb : 0xFFFFFFFFull) : 0u;
+      const TileBuf bs(ar.s8 + tb, lim);
 #pragma unroll
-    for (int k = 0; k < G::E; k++) {
-      const uint32_t o = G::template toff_k<0, false>(p, o0, b0, k);
-      if ((PLK_NTT_DIAG & 8) && k > 0) { v[k] = (v[0] + k) & 0xFFu; continue; }
-      v[k] = bs.ldb(o);
-      if (!PLK_NTT_BYTE_LUT) v[k] = F::byte_val(v[k]);
+      for (int k = 0; k < G::E; k++) {
+        const uint32_t o = G::template toff_k<0, false>(p, o0, b0, k);
+        if ((PLK_NTT_DIAG & 8) && k > 0) { v[k] = (v[0] + k) & 0xFFu; continue; }
+        v[k] = bs.ldb(o);
+        if (!PLK_NTT_BYTE_LUT) v[k] = F::byte_val(v[k]);
+      }
+    } else {
+      const TileBuf bd(ar.d + tb);
+#pragma unroll
+      for (int k = 0; k < G::E; k++) v[k] = bd.ld(G::template toff_k<0, false>(p, o0, b0, k));
     }
-  } else {
-#pragma unroll
-    for (int k = 0; k < G::E; k++) v[k] = bd.ld(G::template toff_k<0, false>(p, o0, b0, k));
-  }
-  // column factor table words of the elements this thread stores (HIGH passes)
+  };
+  int ai = (int)blockIdx.y * apa;
+  uint32_t v[G::E];
+  load(ai, v);   // (the first array's loads go out before the tables')
+  // column factor table words of the elements this thread stores (HIGH passes): the same for
+  // every array of the block
   constexpr int LF = G::lbq(G::NR - 1, false);
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, false);
   const uint32_t of = G::toff(p, bf);
@@ -669,19 +673,26 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
   if (FROM_U8 && PLK_NTT_BYTE_LUT && tid < 256) lut[tid] = F::byte_val(tid);
   if constexpr (PW) load_pass_tw_pairs<M, G::NT>(Tsm, tw.small);
   else load_pass_tw<M, G::NT>(Tsm, tw.small);
-  __syncthreads();
-  if constexpr (FROM_U8 && PLK_NTT_BYTE_LUT) {
+  for (int q = 0;; q++) {
+    // (q = 0: the tables are in LDS; q > 0: every thread's reads of the previous array's last
+    // exchange are done before this one's first exchange writes)
+    __syncthreads();
+    if constexpr (FROM_U8 && PLK_NTT_BYTE_LUT) {
 #pragma unroll
-    for (int k = 0; k < G::E; k++) v[k] = lut[v[k]];
-  }
-  G::template pass<false, 1, PW, true>(v, tid, bufs, 0, Tsm);
+      for (int k = 0; k < G::E; k++) v[k] = lut[v[k]];
+    }
+    G::template pass<false, 1, PW, true>(v, tid, bufs, 0, Tsm);
+    const TileBuf bd(arrs.a[ai].d + tb);
 #pragma unroll
-  for (int k = 0; k < G::E; k++) {
-    uint32_t x = v[k];
-    if constexpr (G::HIGH && COLT) x = F::mul(x, cl[k]);
-    else if constexpr (G::HIGH) x = F::mul(x, F::colf(cl[k], ch[k]));
-    else x = F::canon(x);   // the lo = 0 pass is the last one of a standalone transform
-    bd.st(G::template toff_k<G::NR - 1, false>(p, of, bf, k), x);
+    for (int k = 0; k < G::E; k++) {
+      uint32_t x = v[k];
+      if constexpr (G::HIGH && COLT) x = F::mul(x, cl[k]);
+      else if constexpr (G::HIGH) x = F::mul(x, F::colf(cl[k], ch[k]));
+      else x = F::canon(x);   // the lo = 0 pass is the last one of a standalone transform
+      bd.st(G::template toff_k<G::NR - 1, false>(p, of, bf, k), x);
+    }
+    if (q + 1 >= apa || ai + 1 >= na) break;   // (uniform)
+    load(++ai, v);
   }
 }
 
@@ -724,120 +735,129 @@ __device__ __forceinline__ uint32_t wrap_fix(const WJob& jb, uint32_t wrapped, c
 // which also leaves Montgomery form), reduces mod 17 and writes bytes for idx < out_len.
 // COLT (final passes only): the column table is the inverse one, whose factors carry that scale
 // (the pass is linear), so the bytes come from the pass's outputs directly (F::out17s).
+// Block (x, y) runs tile x of jobs y jpb .. y jpb + jpb - 1 (< nj) one after another, loading the
+// column factors and stage twiddles once for all of them.
 template <int TB, int R, int M, bool TO_U8, class F, bool COLT = false>
-__global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, WTw tw, uint32_t ninv) {
+__global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, WTw tw, uint32_t ninv, int nj, int jpb) {
   using G = Eng<TB, R, M, F>;
   static_assert(G::NT == wt_nt(TB), "tile block size");
   __shared__ uint32_t Tsm[1 << M];
   __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
-  const WJob& jb = jobs.j[blockIdx.y];   // (sum-group members are not in the grid: no inverse of their own)
-  uint32_t* d = jb.C;
-  uint8_t* out8 = jb.out8;
-  const uint64_t out_len = jb.out_len;
-  const uint32_t* s1 = jb.S1;
-  const uint32_t* s2 = jb.S2;
 
   // uniform tile base pointers, 32-bit element offsets
   const uint64_t tb = G::tbase(p, tile);
-  uint32_t* dt = d + tb;
-  const uint32_t* s1t = s1 ? s1 + tb : nullptr;
-  const uint32_t* s2t = s2 ? s2 + tb : nullptr;
   const uint32_t* colt = COLT ? tw.col + tb : nullptr;
   const uint32_t b0 = G::template base_q<0>(tid, true);
   const uint32_t o0 = G::toff(p, b0);
   constexpr int L0 = G::lbq(0, true);
+  int ji = (int)blockIdx.y * jpb;
   uint32_t v[G::E];
-  uint32_t cl[G::HIGH ? G::E : 1], ch[G::HIGH && !COLT ? G::E : 1];
-  const TileBuf bd(dt);
+  auto load = [&](int j) {
+    const TileBuf bd(jobs.j[j].C + tb);
 #pragma unroll
-  for (int k = 0; k < G::E; k++) {
-    const uint32_t e = b0 + ((uint32_t)k << L0);
-    const uint32_t o = G::template toff_k<0, true>(p, o0, b0, k);
-    v[k] = bd.ld(o);
-    if (G::HIGH) {
+    for (int k = 0; k < G::E; k++) v[k] = bd.ld(G::template toff_k<0, true>(p, o0, b0, k));
+  };
+  load(ji);   // (the first job's loads go out before the tables')
+  uint32_t cl[G::HIGH ? G::E : 1], ch[G::HIGH && !COLT ? G::E : 1];
+  if (G::HIGH) {
+#pragma unroll
+    for (int k = 0; k < G::E; k++) {
       if constexpr (COLT) {
-        cl[k] = TileBuf(colt).ld(o);
+        cl[k] = TileBuf(colt).ld(G::template toff_k<0, true>(p, o0, b0, k));
       } else {
-        const uint32_t ex = G::col_exp(p, tile, e);   // roots of tw (inverse or forward)
+        const uint32_t ex = G::col_exp(p, tile, b0 + ((uint32_t)k << L0));   // roots of tw (inverse or forward)
         cl[k] = tw.lo[ex & 4095u];
         ch[k] = tw.hi[ex >> 12];
       }
     }
   }
-  if (s1) {   // a sum group's leader (uniform): its members' center outputs, all loads in flight
-    uint32_t a1[G::E], a2[G::E];
-#pragma unroll
-    for (int k = 0; k < G::E; k++) {
-      const uint32_t o = G::template toff_k<0, true>(p, o0, b0, k);
-      a1[k] = TileBuf(s1t).ld(o);
-      a2[k] = s2 ? TileBuf(s2t).ld(o) : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < G::E; k++) v[k] = F::sum(v[k], a1[k], a2[k]);
-  }
   load_pass_tw<M, G::NT>(Tsm, tw.small);
-  if (G::HIGH) {
-#pragma unroll
-    for (int k = 0; k < G::E; k++) {
-      if constexpr (COLT) v[k] = F::mul(v[k], cl[k]);
-      else v[k] = F::mul(v[k], F::colf(cl[k], ch[k]));
-    }
-  }
-  __syncthreads();
-  G::template pass<true>(v, tid, bufs, 0, Tsm);
   constexpr int LF = G::lbq(G::NR - 1, true);
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, true);
   const uint32_t of = G::toff(p, bf);
-  uint32_t wrapped = 0;   // elements of this thread that hold c[j] + c[N + j] (j < ntop)
-  uint32_t last = 0;      // 1 + the largest index this thread left a non-zero byte at
   const uint32_t N = 1u << p.k;   // (k <= 27: every index fits 32 bits)
-  const uint32_t lim = out_len < N ? (uint32_t)out_len : N;
-  const uint32_t ntop = (uint32_t)jb.ntop;   // (read once: the byte stores below may alias the job table)
-  if constexpr (!TO_U8) {
+  for (int q = 0;; q++) {
+    const WJob& jb = jobs.j[ji];   // (sum-group members are not in the grid: no inverse of their own)
+    uint8_t* out8 = jb.out8;
+    const uint64_t out_len = jb.out_len;
+    const uint32_t* s1 = jb.S1;
+    const uint32_t* s2 = jb.S2;
+    if (s1) {   // a sum group's leader (uniform): its members' center outputs, all loads in flight
+      const uint32_t* s1t = s1 + tb;
+      const uint32_t* s2t = s2 ? s2 + tb : nullptr;
+      uint32_t a1[G::E], a2[G::E];
 #pragma unroll
-    for (int k = 0; k < G::E; k++)   // (the standalone inverse's last pass; poly_mul's 3-pass middle one)
-      bd.st(G::template toff_k<G::NR - 1, true>(p, of, bf, k), F::canon(v[k]));
-  } else {
-    // poly_mul runs its inverse with the FORWARD roots (no inverse table in LDS): that yields
-    // N c[-idx mod N], so the coefficient lands at the negated position.  Every byte is computed
-    // before the first store (the stores then issue back to back).
-    // (the buffer's range is the output length: bytes at or past it are dropped by the store)
-    const TileBuf bo(out8, lim);
-    uint32_t jj[G::E], rr[G::E];
+      for (int k = 0; k < G::E; k++) {
+        const uint32_t o = G::template toff_k<0, true>(p, o0, b0, k);
+        a1[k] = TileBuf(s1t).ld(o);
+        a2[k] = s2 ? TileBuf(s2t).ld(o) : 0u;
+      }
 #pragma unroll
-    for (int k = 0; k < G::E; k++) {
-      jj[k] = (N - ((uint32_t)tb + G::template toff_k<G::NR - 1, true>(p, of, bf, k))) & (N - 1);
-      rr[k] = COLT ? F::out17s(v[k]) : F::out17(v[k], ninv);
+      for (int k = 0; k < G::E; k++) v[k] = F::sum(v[k], a1[k], a2[k]);
     }
+    if (G::HIGH) {
 #pragma unroll
-    for (int k = 0; k < G::E; k++) bo.stb(jj[k], rr[k]);
-    // the wrapped positions and the trimmed length only when the job has them (uniform: the
-    // prover's batched products want neither, and the bookkeeping was ~7 VALU per element)
-    if (ntop) {   // (j < ntop <= 16 implies j < lim)
-#pragma unroll
-      for (int k = 0; k < G::E; k++) wrapped |= jj[k] < ntop ? 1u << k : 0u;
+      for (int k = 0; k < G::E; k++) {
+        if constexpr (COLT) v[k] = F::mul(v[k], cl[k]);
+        else v[k] = F::mul(v[k], F::colf(cl[k], ch[k]));
+      }
     }
-    if (jb.nz) {
+    // (q = 0: the stage twiddles are in LDS; q > 0: the previous job's last exchange reads are done)
+    __syncthreads();
+    G::template pass<true>(v, tid, bufs, 0, Tsm);
+    uint32_t wrapped = 0;   // elements of this thread that hold c[j] + c[N + j] (j < ntop)
+    uint32_t last = 0;      // 1 + the largest index this thread left a non-zero byte at
+    const uint32_t lim = out_len < N ? (uint32_t)out_len : N;
+    const uint32_t ntop = (uint32_t)jb.ntop;   // (read once: the byte stores below may alias the job table)
+    if constexpr (!TO_U8) {
+      const TileBuf bd(jb.C + tb);
 #pragma unroll
-      for (int k = 0; k < G::E; k++) last = max(last, (jj[k] < lim && jj[k] >= ntop && rr[k]) ? jj[k] + 1u : 0u);
-    }
-    if (wrapped) last = max(last, wrap_fix<G>(jb, wrapped, p, tile, bf, LF, 1ull << p.k, rr));
-  }
-
-  // Trimmed length (src/poly.h:20-38).  The top coefficient of a single product is
-  // a[la-1] b[lb-1] mod 17 (one term, wrapped or not); when it is non-zero -- operands with
-  // non-zero leading bytes, the usual case -- the length is la + lb - 1 and one store says so.
-  // Otherwise every tile takes its block's maximum into the word (zeroed by the center kernel).
-  if (TO_U8 && jb.nz) {
-    const bool top = jb.ngroup == 0 && (jb.a8[jb.la - 1] % 17u) * (jb.b8[jb.lb - 1] % 17u) % 17u != 0u;
-    if (top) {
-      if (blockIdx.x == 0 && tid == 0) *jb.nz = (uint32_t)(out_len + (uint64_t)jb.ntop);
+      for (int k = 0; k < G::E; k++)   // (the standalone inverse's last pass; poly_mul's 3-pass middle one)
+        bd.st(G::template toff_k<G::NR - 1, true>(p, of, bf, k), F::canon(v[k]));
     } else {
-      last = plk_block_max(last);
-      if (tid == 0 && last) atomicMax(jb.nz, last);
+      // poly_mul runs its inverse with the FORWARD roots (no inverse table in LDS): that yields
+      // N c[-idx mod N], so the coefficient lands at the negated position.  Every byte is computed
+      // before the first store (the stores then issue back to back).
+      // (the buffer's range is the output length: bytes at or past it are dropped by the store)
+      const TileBuf bo(out8, lim);
+      uint32_t jj[G::E], rr[G::E];
+#pragma unroll
+      for (int k = 0; k < G::E; k++) {
+        jj[k] = (N - ((uint32_t)tb + G::template toff_k<G::NR - 1, true>(p, of, bf, k))) & (N - 1);
+        rr[k] = COLT ? F::out17s(v[k]) : F::out17(v[k], ninv);
+      }
+#pragma unroll
+      for (int k = 0; k < G::E; k++) bo.stb(jj[k], rr[k]);
+      // the wrapped positions and the trimmed length only when the job has them (uniform: the
+      // prover's batched products want neither, and the bookkeeping was ~7 VALU per element)
+      if (ntop) {   // (j < ntop <= 16 implies j < lim)
+#pragma unroll
+        for (int k = 0; k < G::E; k++) wrapped |= jj[k] < ntop ? 1u << k : 0u;
+      }
+      if (jb.nz) {
+#pragma unroll
+        for (int k = 0; k < G::E; k++) last = max(last, (jj[k] < lim && jj[k] >= ntop && rr[k]) ? jj[k] + 1u : 0u);
+      }
+      if (wrapped) last = max(last, wrap_fix<G>(jb, wrapped, p, tile, bf, LF, 1ull << p.k, rr));
     }
+
+    // Trimmed length (src/poly.h:20-38).  The top coefficient of a single product is
+    // a[la-1] b[lb-1] mod 17 (one term, wrapped or not); when it is non-zero -- operands with
+    // non-zero leading bytes, the usual case -- the length is la + lb - 1 and one store says so.
+    // Otherwise every tile takes its block's maximum into the word (zeroed by the center kernel).
+    if (TO_U8 && jb.nz) {
+      const bool top = jb.ngroup == 0 && (jb.a8[jb.la - 1] % 17u) * (jb.b8[jb.lb - 1] % 17u) % 17u != 0u;
+      if (top) {
+        if (blockIdx.x == 0 && tid == 0) *jb.nz = (uint32_t)(out_len + (uint64_t)jb.ntop);
+      } else {
+        last = plk_block_max(last);
+        if (tid == 0 && last) atomicMax(jb.nz, last);
+      }
+    }
+    if (q + 1 >= jpb || ji + 1 >= nj) break;   // (uniform)
+    load(++ji);
   }
 }
 
@@ -1024,17 +1044,43 @@ WTw inv_wtw(int k) {
 // the table path applies to the pass whose bits reach the top (lo + M = k): a plan's first
 // forward and last inverse pass; byte-input forward / byte-output inverse or single-array
 // forward passes are the only ones instantiated with it
+// Arrays (jobs) per block of a table pass: several arrays of one tile share its column-table words
+// (read once per block instead of once per array: the 2^22 table is 16 MiB); chosen so that the
+// launch's rounds of resident blocks (2 per CU) times the arrays per block stay at their minimum
+// (one array per block: ceil(tiles n / resident)), the largest such count.
+// PLK_OPT_NTT_TABLE_SHARE = 0: one array per block.
+int per_block(uint32_t tiles, int n) {
+  if (!plk_opt(PLK_OPT_NTT_TABLE_SHARE) || n <= 1) return 1;
+  static std::atomic<int> cus{0};
+  int c = cus.load(std::memory_order_relaxed);
+  if (!c) {
+    int dev = 0;
+    c = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    if (c <= 0) c = 256;
+    cus.store(c, std::memory_order_relaxed);
+  }
+  const uint64_t res = 2ull * (uint64_t)c;   // resident 1024-thread blocks: 2 per CU
+  auto cost = [&](int J) { return ((tiles * (uint64_t)((n + J - 1) / J) + res - 1) / res) * (uint64_t)J; };
+  int best = 1;
+  for (int J = 2; J <= n; J++)
+    if (cost(J) <= cost(best)) best = J;
+  return best;
+}
+
 template <int TB, int M, bool U8, class F>
 void launch_fwd(WPass p, const WArrs& arrs, int na, WTw tw, hipStream_t st) {
   constexpr int R = wt_r(TB);
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB);
   if constexpr (M < TB) {
     if (tw.col && p.lo + M == p.k) {
-      hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, F, true>), dim3(tiles, na), dim3(wt_nt(TB)), 0, st, p, arrs, tw);
+      const int J = per_block(tiles, na);
+      hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, F, true>), dim3(tiles, (na + J - 1) / J), dim3(wt_nt(TB)), 0, st, p,
+                         arrs, tw, na, J);
       return;
     }
   }
-  hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, F>), dim3(tiles, na), dim3(wt_nt(TB)), 0, st, p, arrs, tw);
+  hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, F>), dim3(tiles, na), dim3(wt_nt(TB)), 0, st, p, arrs, tw, na, 1);
 }
 template <int TB, int M, bool U8, class F>
 void launch_inv(WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipStream_t st) {
@@ -1042,12 +1088,13 @@ void launch_inv(WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipSt
   const uint32_t tiles = (uint32_t)((1ull << p.k) >> TB);
   if constexpr (M < TB && U8) {
     if (tw.col && p.lo + M == p.k) {
-      hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8, F, true>), dim3(tiles, nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw,
-                         ninv);
+      const int J = per_block(tiles, nj);
+      hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8, F, true>), dim3(tiles, (nj + J - 1) / J), dim3(wt_nt(TB)), 0, st, p,
+                         jobs, tw, ninv, nj, J);
       return;
     }
   }
-  hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8, F>), dim3(tiles, nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw, ninv);
+  hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8, F>), dim3(tiles, nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw, ninv, nj, 1);
 }
 
 // pass widths: 1..8 for both tile sizes, 9..10 for 2^13 tiles, M = TB for the lo = 0 pass
