@@ -84,9 +84,15 @@ enum {
                                     plk_init / plk_init_devices */
   PLK_OPT_PROVE_DERIVE_T2A = 18, /* 1: round 3's A2 B2 from a_x b_x by an elementwise pass (0: its own product) */
   PLK_OPT_NTT_TABLE_SHARE = 19,  /* 1: a table pass runs several arrays of one tile per block (column words read once) */
-  PLK_OPT_COUNT = 20
+  PLK_OPT_NTT_LAUNCH_LOG = 20,   /* diagnostics: 1 records the NTT passes' launch plans (plk_ntt_launch_log) */
+  PLK_OPT_COUNT = 21
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
+/* Diagnostics for the offline roofline tools: with PLK_OPT_NTT_LAUNCH_LOG = 1 every NTT pass launch
+ * is recorded as 7 ints {kind (0 forward, 1 inverse, 2 center, 3 shared lo = 0 pass), tile bits,
+ * pass bits, log2 size, arrays / products, arrays per block, center pass units}; this copies up to
+ * cap records into out (7 ints each), clears the log and returns the count. */
+int plk_ntt_launch_log(int32_t *out, int cap);
 int64_t plk_get_option(int opt);              /* -1 for an unknown option */
 
 /* ---- host-buffer entry points (what the drop-in headers call) ------------------------ */

@@ -465,6 +465,7 @@ const OptDef kOpt[PLK_OPT_COUNT] = {
     {4, 1, PLK_MAX_SHARDS, false},             // MSM_HOST_LANES (read at plk_init / plk_init_devices)
     {1, 0, 1, false},                          // PROVE_DERIVE_T2A
     {1, 0, 1, false},                          // NTT_TABLE_SHARE
+    {0, 0, 1, false},                          // NTT_LAUNCH_LOG
 };
 struct Opts {
   std::atomic<int64_t> v[PLK_OPT_COUNT];

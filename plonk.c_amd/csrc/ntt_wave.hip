@@ -32,6 +32,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
+#include <vector>
 
 #ifndef PLK_NTT_DIAG
 #define PLK_NTT_DIAG 0        // tuning builds only: bit 0 skips the butterflies, bit 1 the LDS exchanges,
@@ -1044,6 +1046,22 @@ WTw inv_wtw(int k) {
 // the table path applies to the pass whose bits reach the top (lo + M = k): a plan's first
 // forward and last inverse pass; byte-input forward / byte-output inverse or single-array
 // forward passes are the only ones instantiated with it
+// Diagnostics (PLK_OPT_NTT_LAUNCH_LOG = 1): the launch plans of the tile engine's passes, in launch
+// order, for the offline roofline tools (tools/ntt_roofline.py, tools/ntt_pmc_summary.py --plan):
+// a profiler records a launch's grid, not how many arrays its blocks walk (per_block below) or
+// how many pass units the persistent center kernel runs.  kind: 0 forward pass, 1 inverse pass,
+// 2 center (n = products, units = lo = 0 passes run per tile), 3 shared-operand lo = 0 pass.
+struct LaunchRec {
+  int32_t kind, tb, m, k, n, per_block, units;
+};
+std::mutex g_log_mu;
+std::vector<LaunchRec> g_log;
+void log_launch(int kind, int tb, int m, int k, int n, int per_block, int units) {
+  if (!plk_opt(PLK_OPT_NTT_LAUNCH_LOG)) return;
+  std::lock_guard<std::mutex> lk(g_log_mu);
+  if (g_log.size() < 65536) g_log.push_back(LaunchRec{kind, tb, m, k, n, per_block, units});
+}
+
 // Arrays (jobs) per block of a table pass: several arrays of one tile share its column-table words
 // (read once per block instead of once per array: the 2^22 table is 16 MiB); chosen so that the
 // launch's rounds of resident blocks (2 per CU) times the arrays per block stay at their minimum
@@ -1075,11 +1093,13 @@ void launch_fwd(WPass p, const WArrs& arrs, int na, WTw tw, hipStream_t st) {
   if constexpr (M < TB) {
     if (tw.col && p.lo + M == p.k) {
       const int J = per_block(tiles, na);
+      log_launch(0, TB, M, p.k, na, J, 0);
       hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, F, true>), dim3(tiles, (na + J - 1) / J), dim3(wt_nt(TB)), 0, st, p,
                          arrs, tw, na, J);
       return;
     }
   }
+  log_launch(0, TB, M, p.k, na, 1, 0);
   hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, F>), dim3(tiles, na), dim3(wt_nt(TB)), 0, st, p, arrs, tw, na, 1);
 }
 template <int TB, int M, bool U8, class F>
@@ -1089,11 +1109,13 @@ void launch_inv(WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipSt
   if constexpr (M < TB && U8) {
     if (tw.col && p.lo + M == p.k) {
       const int J = per_block(tiles, nj);
+      log_launch(1, TB, M, p.k, nj, J, 0);
       hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8, F, true>), dim3(tiles, (nj + J - 1) / J), dim3(wt_nt(TB)), 0, st, p,
                          jobs, tw, ninv, nj, J);
       return;
     }
   }
+  log_launch(1, TB, M, p.k, nj, 1, 0);
   hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8, F>), dim3(tiles, nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw, ninv, nj, 1);
 }
 
@@ -1268,6 +1290,7 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
       }
     }
     if (ns) {
+      log_launch(3, TB, TB, k, ns, 1, ns);
       hipLaunchKernelGGL((wt_fixfwd_kernel<TB, wt_rc(TB), F>), dim3(tiles, ns), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, sh,
                          twf);
       PLK_HIP(hipGetLastError());
@@ -1280,6 +1303,9 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
   bool grp = false;
   for (int j = 0; j < nj; j++) grp |= cj.j[j].ncm > 0;
   if (grid) {
+    int units = 0;
+    for (int j = 0; j < nj; j++) units += center_units(cj, j);
+    log_launch(2, TB, TB, k, nj, 1, units);
     if (grp)
       hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F, true>), dim3(grid), dim3(wt_ntc(TB)), 0, st, WPass{k, 0},
                          cj, twf, sc);
@@ -1430,4 +1456,16 @@ int plk_wave_ntt_launch(uint32_t* d, int k, int batch, int inverse, int field, h
     if (rc) return rc;
   }
   return PLK_OK;
+}
+
+extern "C" int plk_ntt_launch_log(int32_t* out, int cap) {
+  std::lock_guard<std::mutex> lk(g_log_mu);
+  const int n = (int)std::min<size_t>(g_log.size(), cap > 0 ? (size_t)cap : 0);
+  for (int i = 0; i < n && out; i++) {
+    const LaunchRec& r = g_log[i];
+    const int32_t v[7] = {r.kind, r.tb, r.m, r.k, r.n, r.per_block, r.units};
+    for (int f = 0; f < 7; f++) out[7 * i + f] = v[f];
+  }
+  g_log.clear();
+  return n;
 }

@@ -291,8 +291,16 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a, const SlotFile f,
       oZ1 |= hmod((vz + c0 * 16u) * al2) << sh;
     }
     store4(a.cA, a.la, i, oA); store4(a.cB, a.la, i, oB); store4(a.cC, a.la, i, oC);
-    store4(a.A2, a.la, i, oA2); store4(a.B2, a.la, i, oB2); store4(a.C2, a.la, i, oC2);
-    store4(a.A3, a.la, i, oA3); store4(a.B3, a.la, i, oB3); store4(a.C3, a.la, i, oC3);
+    // (NULL: not needed by this call -- A2 B2 derived from a_x b_x by t2a_kernel, or a chain whose
+    // product comes from another GPU; uniform branches)
+    if (a.A2) {
+      store4(a.A2, a.la, i, oA2);
+      store4(a.B2, a.la, i, oB2);
+    }
+    if (a.C2) store4(a.C2, a.la, i, oC2);
+    if (a.A3) {
+      store4(a.A3, a.la, i, oA3); store4(a.B3, a.la, i, oB3); store4(a.C3, a.la, i, oC3);
+    }
     store4(a.cZ, a.lzx, i, oZ); store4(a.ZW, a.lzx, i, oZW); store4(a.Z1, a.lzx, i, oZ1);
   }
 }
@@ -1694,9 +1702,18 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   int rc;
 #define RC(x) do { if ((rc = (x))) return rc; } while (0)
   // ---- rounds 1-2 (a_x b_x c_x z_x) and round 3's linear factors, src/plonk.h:280-489
+  // Chains: 1 = t_2's (A2 B2, C2 z -> T2), 2 = t_3's (A3 B3, C3 z(omega x) -> T3).  `local`: the
+  // chains this call computes itself; a helper call computes only md.only.
+  const int local = md.only ? md.only : (PLK_CHAIN_T2 | PLK_CHAIN_T3) & ~md.ext;
+  // A2 B2 from a_x b_x when this call computes that product (t2a_kernel after round 3's first
+  // batch; a helper computing only the chains keeps the product)
+  const bool derive_t2a = (local & PLK_CHAIN_T2) && !md.only && plk_opt(PLK_OPT_PROVE_DERIVE_T2A);
   if (prep) {
+    uint8_t* const a2 = (local & PLK_CHAIN_T2) && !derive_t2a ? P->A2 : nullptr;
+    uint8_t* const c2 = (local & PLK_CHAIN_T2) ? P->C2 : nullptr;
+    uint8_t* const a3 = (local & PLK_CHAIN_T3) ? P->A3 : nullptr;
     const PrepArgs pa{P->d_zh, FA, FB, FC, ACC, S1, S2, S3, L.lz, n, L.la, L.lzx,
-                      cA, cB, cC, cZ, P->A2, P->B2, P->C2, P->A3, P->B3, P->C3, P->ZW, P->Z1};
+                      cA, cB, cC, cZ, a2, P->B2, c2, a3, P->B3, P->C3, P->ZW, P->Z1};
     const uint64_t blocks = std::min<uint64_t>((L.lzx + 1023) / 1024, 4096);
     hipLaunchKernelGGL(prep_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, pa, sf,
                        P->d_S, P->d_stat, (int)ST_GATE);
@@ -1726,9 +1743,6 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
         make_lc({{cZ, L.lzx}}, {S_ONE}, S_NEG1, -1, S_ALPHA2, -1, P->Z1, L.lz1)}));  // alpha^2 (z - 1)
   }
   {
-    // Chains: 1 = t_2's (A2 B2, C2 z -> T2), 2 = t_3's (A3 B3, C3 z(omega x) -> T3).  `local`: the
-    // chains this call computes itself; a helper call computes only md.only.
-    const int local = md.only ? md.only : (PLK_CHAIN_T2 | PLK_CHAIN_T3) & ~md.ext;
     // a_x q_l + b_x q_r + c_x q_o as ONE sum group (one inverse transform) when the sum fits
     // F29's centered range: 3 * 64 n <= (p - 1) / 2 (n <= 1,223,338)
     const int lin = plk_poly_mul_summable(L.la, n) && (uint64_t)3 * L.la * 128 < f29::P ? 1 : 0;
@@ -1755,9 +1769,6 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     // re-associated as (A2 B2)(C2 z): C2 z and C3 z(omega x) join this batch and the 4n products
     // come in one batch (associativity over GF(17); the centered F29 residues hold the 2n x 2n
     // products exactly)
-    // A2 B2 from a_x b_x when this call computes that product (t2a_kernel after this batch; a
-    // helper computing only the chains keeps the product)
-    const bool derive_t2a = (local & PLK_CHAIN_T2) && !md.only && plk_opt(PLK_OPT_PROVE_DERIVE_T2A);
     if (local & PLK_CHAIN_T2) {
       if (!derive_t2a) g1.push_back({{P->A2, L.la, P->B2, L.la, P->T2a}, -1});
       g1.push_back({{P->C2, L.la, cZ, L.lzx, P->T2b}, -1});

@@ -80,6 +80,7 @@ SIGNATURES = {
     "plk_prover_attach_helpers": (C.c_int, [_vp, C.c_int]),
     "plk_prover_helpers": (C.c_int, [_vp]),
     "plk_prover_rounds_multi_dev": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, _u8p, _u8p, C.c_int, _u8p]),
+    "plk_ntt_launch_log": (C.c_int, [C.POINTER(C.c_int32), C.c_int]),
 }
 
 # PLK_OPT_* (include/plonkhip.h), by the name without the prefix
@@ -87,7 +88,7 @@ OPTIONS = {"TINY_CALLS": 1, "PROVE_SYNC": 2, "POLY_BLOCK_L": 3, "POLY_BLOCK_S": 
            "NTT_SHARED_FIX": 7, "NTT_T13_MIN_K": 8, "NTT_CENTER_BLOCKS": 9, "MSM_THREADS": 10,
            "MSM_MAX_BLOCKS": 11, "MSM_GROUPS": 12, "MSM_COPIES": 13, "MSM_HALF": 14, "MSM_SHARD_MIN": 15,
            "NTT_CENTER_SUM": 16, "MSM_HOST_LANES": 17,
-           "PROVE_DERIVE_T2A": 18, "NTT_TABLE_SHARE": 19}
+           "PROVE_DERIVE_T2A": 18, "NTT_TABLE_SHARE": 19, "NTT_LAUNCH_LOG": 20}
 
 PLK_PROVE_STRICT = 1
 PLK_PROVE_PREPROCESSED = 2
@@ -174,6 +175,14 @@ def devices():
     arr = (C.c_int * 16)()
     n = int(lib().plk_devices(arr, 16))
     return [arr[i] for i in range(min(n, 16))]
+
+
+def ntt_launch_log(cap=4096):
+    """plk_ntt_launch_log: the recorded NTT pass launches (PLK_OPT_NTT_LAUNCH_LOG = 1) as dicts, log cleared"""
+    buf = (C.c_int32 * (7 * cap))()
+    n = int(lib().plk_ntt_launch_log(buf, cap))
+    keys = ("kind", "tb", "m", "k", "n", "per_block", "units")
+    return [dict(zip(keys, buf[7 * i:7 * i + 7])) for i in range(n)]
 
 
 def _opt_id(name):

@@ -14,7 +14,7 @@ cp $P/msm_pmc_latest.json profiles/msm_pmc_latest.json
 cp "$P/prove_2^20_breakdown.txt" "profiles/${R}_prove_2^20_breakdown.txt"
 [ -f "$P/prove_2^20_preprocessed_breakdown.txt" ] && cp "$P/prove_2^20_preprocessed_breakdown.txt" "profiles/${R}_prove_2^20_preprocessed_breakdown.txt"
 cp $P/ntt_bench.json profiles/${R}_ntt_bench.json
-for f in bfly_peak.json prove_ntt_roofline.json prove_ntt_roofline.txt ntt_roofline.json ntt_roofline.txt; do
+for f in bfly_peak.json prove_ntt_roofline.json prove_ntt_roofline.txt ntt_roofline.json ntt_roofline.txt prove_plan.json; do
   [ -f $P/$f ] && cp $P/$f profiles/${R}_$f
 done
 tail -1 $P/gpu_tests.log > profiles/${R}_gpu_tests.txt

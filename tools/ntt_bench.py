@@ -14,6 +14,9 @@ from bench import event_avg_ms  # noqa: E402
 
 hip.tune_from_env()   # PLK_TUNE="NAME=value,..." (plk_set_option), tuning runs only
 hip.init(0)
+PLAN = sys.argv[sys.argv.index("--plan") + 1] if "--plan" in sys.argv else None
+if PLAN:   # every NTT pass launch of this run, in order (tools/ntt_roofline.py --plan)
+    hip.set_option("NTT_LAUNCH_LOG", 1)
 dev = torch.device("cuda", 0)
 st = torch.cuda.current_stream()
 out = {}
@@ -51,3 +54,6 @@ for la, lb in (((1 << 19, 1 << 19),) if quick else
     avg, med = event_avg_ms(torch, st, lambda i: hip.poly_mul_dev(a, la, b, lb, o, nz, work, st), 20)
     out["poly_mul_%dx%d_us" % (la, lb)] = round(avg * 1e3, 2)
 print(json.dumps(out))
+if PLAN:
+    with open(PLAN, "w") as f:
+        json.dump({"launches": hip.ntt_launch_log(1 << 16)}, f)

@@ -11,6 +11,7 @@ traffic (FETCH_SIZE x 2 per the gfx950 calibration + WRITE_SIZE, KiB -> bytes) a
 kernel's algorithmic bytes (8 B per element per pass: u32 read + write; byte-input / byte-output
 passes 5 B), and VALU instructions per butterfly.  The SQ counters come from a subset of the
 shader engines and are scaled by launched waves / SQ_WAVES.""" 
+import json
 import re
 import sqlite3
 import sys
@@ -55,7 +56,19 @@ def tile_bits(name):
     return (int(m.group(1)), int(m.group(2)), int(m.group(3)) if m.group(3) else None) if m else (None, None, None)
 
 
+def load_plan():
+    """--plan plan.json (tools/prove_plan.py): arrays per (kind, TB, M, tiles) of the proof's table
+    passes -- their grid y counts array GROUPS since round 4 (several arrays per block)"""
+    if "--plan" not in sys.argv:
+        return {}
+    with open(sys.argv[sys.argv.index("--plan") + 1]) as f:
+        launches = json.load(f)["launches"]
+    return {("fwd" if r["kind"] == 0 else "inv", r["tb"], r["m"], (1 << r["k"]) >> r["tb"]): r["n"]
+            for r in launches if r["kind"] in (0, 1)}
+
+
 def main():
+    plan = load_plan()
     dbs = [load(p) for p in sys.argv[1:5]]
     keys = set()
     for a, _ in dbs:
@@ -86,9 +99,11 @@ def main():
         bfly = None
         alg = None
         if TB and M is not None and not center and "fixfwd" not in name:
-            bfly = blocks * gy * (1 << (TB - 1)) * M
+            kind = "fwd" if "wt_fwd" in name else "inv"
+            arrays = plan.get((kind, TB, M, blocks), gy)   # (blocks of the x dimension = tiles)
+            bfly = blocks * arrays * (1 << (TB - 1)) * M
             u8 = name.replace(" ", "").split(",")[3] == "true"
-            alg = blocks * gy * (1 << TB) * (5 if u8 else 8)
+            alg = blocks * arrays * (1 << TB) * (5 if u8 else 8)
         valu = cs.get("SQ_INSTS_VALU", 0) * scale if scale else None
         vt = valu * CYC_PER_VALU / SIMDS / CLK * 1e6 if valu else None
         ldsc = cs.get("SQ_LDS_BANK_CONFLICT", 0) / cs["SQ_LDS_IDX_ACTIVE"] if cs.get("SQ_LDS_IDX_ACTIVE") else None

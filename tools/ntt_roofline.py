@@ -3,7 +3,7 @@
 butterfly peak (tools/bfly_peak.hip: the engine's own butterfly formulas in registers, no memory,
 full occupancy -- the integer-VALU roof of this arithmetic on this chip).
 
-    python tools/ntt_roofline.py <run_results.db> <bfly_peak.json> [--prove | --all] [--json out]
+    python tools/ntt_roofline.py <run_results.db> <bfly_peak.json> [--prove [--plan plan.json] | --all] [--json out]
 
 --prove: the kernels of the LAST prove call of the trace (tools/prove_bench.py; calls end with
 trim_pack_kernel); --all (default): every wt_* dispatch, aggregated per (kernel, grid).
@@ -16,7 +16,13 @@ Butterflies counted (the algorithmic work, radix-2 count):
       inverse per item); the items are the next inverse pass's blocks (same batch).  An estimate:
       fixed operands' skipped passes are counted, merged sum-group members' forward passes are
       not (the prover's 2^21 batch: 24 counted per tile for 22 run; 2^22: 6 for 8)
-Peak: F29 / BabyBear DIF for forward passes, DIT for inverse, (2 DIF + 1 DIT) / 3 for the center."""
+Peak: F29 / BabyBear DIF for forward passes, DIT for inverse, (2 DIF + 1 DIT) / 3 for the center.
+
+--plan (tools/prove_plan.py, round 4): the proof's launch plan from the library
+(plk_ntt_launch_log), matched to the pass kernels of the last proof in launch order.  Table passes
+now walk several arrays per block (grid y = array groups, not arrays), and the plan gives the
+exact counts: arrays x tiles x 2^(TB-1) x M for a pass, tiles x pass units x 2^(TB-1) x TB for the
+center (the lo = 0 passes it actually runs, fixed operands' skipped passes excluded)."""
 import json
 import re
 import sqlite3
@@ -55,12 +61,28 @@ def main():
     if "--prove" in sys.argv:
         idx = [i for i, r in enumerate(rows) if "trim_pack" in r[0]]
         rows = rows[idx[-2] + 1:idx[-1] + 1]
+    # (--all --plan: the plan of the whole traced run, every pass launch in order)
+    plan = None
+    if "--plan" in sys.argv:
+        with open(sys.argv[sys.argv.index("--plan") + 1]) as f:
+            plan = [r for r in json.load(f)["launches"] if r["kind"] in (0, 1, 2)]
     disp = []
+    pi = 0
     for i, (name, gx, gy, wx, dur, _) in enumerate(rows):
         p = parse(name)
         if not p:
             continue
         kind, tb, mm, field = p
+        if plan is not None:
+            r = plan[pi]
+            pi += 1
+            want = {"fwd": 0, "inv": 1, "center": 2}[kind]
+            if r["kind"] != want or r["tb"] != tb or r["m"] != mm:
+                raise SystemExit("plan mismatch at %s: %r" % (name, r))
+            tiles = (1 << r["k"]) >> tb
+            bfly = tiles * ((r["units"] * tb) if kind == "center" else (r["n"] * mm)) * (1 << (tb - 1))
+            disp.append((name.replace("(anonymous namespace)::", "").split("(")[0], gx, gy, kind, field, bfly, dur / 1e3))
+            continue
         if kind == "center":
             nxt = next((r for r in rows[i + 1:] if parse(r[0]) and parse(r[0])[0] == "inv"), None)
             if nxt is None:

@@ -23,9 +23,10 @@ python3 tools/prove_breakdown.py $O/prove/run_results.db > $O/prove_2^20_breakdo
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prove_pre -o run -- python3 tools/prove_bench.py --pre 20 > $O/prove_pre.json 2>&1 || exit 1
 python3 tools/prove_breakdown.py $O/prove_pre/run_results.db > $O/prove_2^20_preprocessed_breakdown.txt || exit 1
 timeout -k 10 60 ./tools/bfly_peak > $O/bfly_peak.json || exit 1
-python3 tools/ntt_roofline.py $O/prove/run_results.db $O/bfly_peak.json --prove --json $O/prove_ntt_roofline.json > $O/prove_ntt_roofline.txt || exit 1
+timeout -k 10 120 python3 tools/prove_plan.py 20 > $O/prove_plan.json 2>/dev/null || exit 1
+python3 tools/ntt_roofline.py $O/prove/run_results.db $O/bfly_peak.json --prove --plan $O/prove_plan.json --json $O/prove_ntt_roofline.json > $O/prove_ntt_roofline.txt || exit 1
 timeout -k 10 200 python tools/ntt_bench.py > $O/ntt_bench.json 2>/dev/null || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace -d $O/ntt -o run -- python3 tools/ntt_bench.py > /dev/null 2>&1 || exit 1
-python3 tools/ntt_roofline.py $O/ntt/run_results.db $O/bfly_peak.json --json $O/ntt_roofline.json > $O/ntt_roofline.txt || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace -d $O/ntt -o run -- python3 tools/ntt_bench.py --plan $O/ntt_plan.json > /dev/null 2>&1 || exit 1
+python3 tools/ntt_roofline.py $O/ntt/run_results.db $O/bfly_peak.json --plan $O/ntt_plan.json --json $O/ntt_roofline.json > $O/ntt_roofline.txt || exit 1
 rm -rf $O/trace $O/pmc $O/prove $O/prove_pre $O/ntt
 echo "round profile $TAG done"
