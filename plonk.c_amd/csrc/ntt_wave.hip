@@ -71,6 +71,7 @@ constexpr int wt_r(int TB) { return TB == 13 ? PLK_NTT_R13 : PLK_NTT_R12; }
 constexpr int wt_nt(int TB) { return 1 << (TB - wt_r(TB)); }
 constexpr int WT_MAX_HI12 = 8;                 // widest high-bit pass with 2^12 tiles
 constexpr int WT_MAX_HI13 = 10;                // ... with 2^13 tiles
+constexpr uint32_t M17_LUT = 1040;             // mod-17 table of the byte outputs (F::out17_idx < 1035)
 
 __device__ __forceinline__ int wphys(int e) { return e + (e >> 5); }
 
@@ -86,6 +87,15 @@ struct TileBuf {
   __device__ __forceinline__ uint32_t ld(uint32_t off) const { return __builtin_amdgcn_raw_buffer_load_b32(r, off << 2, 0, 0); }
   __device__ __forceinline__ void st(uint32_t off, uint32_t v) const {
     __builtin_amdgcn_raw_buffer_store_b32(v, r, off << 2, 0, 0);
+  }
+  // the same with a UNIFORM part of the word offset in the instruction's SGPR offset (no VGPR and
+  // no address VALU per register index).  Only for accesses that do not rely on the range check
+  // (the words of a tile: the resource's range is unbounded there).
+  __device__ __forceinline__ uint32_t ld(uint32_t off, uint32_t uoff) const {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off << 2, uoff << 2, 0);
+  }
+  __device__ __forceinline__ void st(uint32_t off, uint32_t uoff, uint32_t v) const {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, off << 2, uoff << 2, 0);
   }
   __device__ __forceinline__ uint32_t ldb(uint32_t off) const { return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0); }
   __device__ __forceinline__ void stb(uint32_t off, uint32_t v) const {
@@ -182,6 +192,9 @@ struct FBB {
   __device__ static __forceinline__ uint32_t out17(uint32_t v, uint32_t ninv) { return bb::mmul(v, ninv) % 17u; }
   // the same when the scale is already applied (the inverse column table holds it)
   __device__ static __forceinline__ uint32_t out17s(uint32_t v) { return v % 17u; }
+  // an index < M17_LUT whose entry of the mod-17 table is out17s(v): 2^8 = 1 (mod 17), so a word is
+  // congruent to the sum of its bytes (one v_dot4_u32_u8)
+  __device__ static __forceinline__ uint32_t out17_idx(uint32_t v) { return __builtin_amdgcn_udot4(v, 0x01010101u, 0u, false); }
   __device__ static __forceinline__ uint32_t scale(uint32_t c, uint32_t ninv) { return bb::mmul(c, ninv); }
   __device__ static __forceinline__ uint32_t canon(uint32_t v) { return v; }   // always reduced
 };
@@ -270,6 +283,14 @@ struct F29 {
     const uint32_t y = red4(v);
     const uint32_t j = __umulhi(y + (f29::P - 1) / 2, 2454267022u) >> 28;   // ceil(2^60 / p)
     return (y + 5u * j) % 17u;
+  }
+  // the same as an index into a mod-17 table (< M17_LUT): y is congruent to the sum of its bytes
+  // (2^8 = 1 mod 17), so the centered value is congruent to bytesum(y) + 5 j <= 4 * 255 + 5 * 3
+  // (one v_dot4_u32_u8 and a v_mad_u32_u24 instead of the % 17: 3 VALU fewer per output byte)
+  __device__ static __forceinline__ uint32_t out17_idx(uint32_t v) {
+    const uint32_t y = red4(v);
+    const uint32_t j = __umulhi(y + (f29::P - 1) / 2, 2454267022u) >> 28;
+    return __builtin_amdgcn_udot4(y, 0x01010101u, 5u * j, false);
   }
   __device__ static __forceinline__ uint32_t scale(uint32_t c, uint32_t ninv) { return f29::red1(f29::mmul(c, ninv)); }
 };
@@ -565,6 +586,26 @@ struct Eng {
     else return toff(p, b + ((uint32_t)k << LB));
   }
 
+  // toff_k as (per-lane o0, UNIFORM per-k part) when the register index only moves row bits --
+  // every column-mapped round and the lo = 0 pass: word access k of the thread = o0 + kpart(k)
+  template <int Q, bool INV>
+  static constexpr bool ksplit() { return M == TB || lbq(Q, INV) + R <= M; }
+  template <int Q, bool INV>
+  __device__ static __forceinline__ uint32_t kpart(const WPass& p, int k) {
+    return ((uint32_t)k << lbq(Q, INV)) << (M == TB ? 0 : p.lo);
+  }
+  // a tile's word k of round Q's mapping through a TileBuf: the split form where it applies
+  template <int Q, bool INV>
+  __device__ static __forceinline__ uint32_t ldk(const TileBuf& t, const WPass& p, uint32_t o0, uint32_t b, int k) {
+    if constexpr (ksplit<Q, INV>()) return t.ld(o0, kpart<Q, INV>(p, k));
+    else return t.ld(toff_k<Q, INV>(p, o0, b, k));
+  }
+  template <int Q, bool INV>
+  __device__ static __forceinline__ void stk(const TileBuf& t, const WPass& p, uint32_t o0, uint32_t b, int k, uint32_t v) {
+    if constexpr (ksplit<Q, INV>()) t.st(o0, kpart<Q, INV>(p, k), v);
+    else t.st(toff_k<Q, INV>(p, o0, b, k), v);
+  }
+
   // column factor exponent (in w_{2^27} units) for element e of a high-bit pass
   __device__ static __forceinline__ uint32_t col_exp(const WPass& p, uint32_t tile, uint32_t e) {
     constexpr int cb = TB - M;
@@ -615,7 +656,7 @@ __device__ __forceinline__ void load_pass_tw_pairs(uint32_t* Tsm, const uint32_t
 // COLT: the column factors come from tw.col (one word per element, indexed like the data)
 // instead of lo * hi (two words and a multiply per element).
 template <int TB, int R, int M, bool FROM_U8, class F, bool COLT = false>
-__global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, WTw tw, int na, int apa) {
+__global__ __launch_bounds__(wt_nt(TB), 8) void wt_fwd_kernel(WPass p, WArrs arrs, WTw tw, int na, int apa) {
   using G = Eng<TB, R, M, F>;
   static_assert(G::NT == wt_nt(TB), "tile block size");
   constexpr bool PW = F::ADIC == f29::TWO_ADICITY;   // {w, p - w} pairs (F29's lazy DIF)
@@ -647,7 +688,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
     } else {
       const TileBuf bd(ar.d + tb);
 #pragma unroll
-      for (int k = 0; k < G::E; k++) v[k] = bd.ld(G::template toff_k<0, false>(p, o0, b0, k));
+      for (int k = 0; k < G::E; k++) v[k] = G::template ldk<0, false>(bd, p, o0, b0, k);
     }
   };
   int ai = (int)blockIdx.y * apa;
@@ -663,7 +704,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
       if constexpr (COLT) {
-        cl[k] = (PLK_NTT_DIAG & 16) ? 0x12345u + k : TileBuf(colt).ld(G::template toff_k<G::NR - 1, false>(p, of, bf, k));
+        cl[k] = (PLK_NTT_DIAG & 16) ? 0x12345u + k : G::template ldk<G::NR - 1, false>(TileBuf(colt), p, of, bf, k);
       } else {
         const uint32_t ex = G::col_exp(p, tile, bf + ((uint32_t)k << LF));
         cl[k] = tw.lo[ex & 4095u];
@@ -691,7 +732,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
       if constexpr (G::HIGH && COLT) x = F::mul(x, cl[k]);
       else if constexpr (G::HIGH) x = F::mul(x, F::colf(cl[k], ch[k]));
       else x = F::canon(x);   // the lo = 0 pass is the last one of a standalone transform
-      bd.st(G::template toff_k<G::NR - 1, false>(p, of, bf, k), x);
+      G::template stk<G::NR - 1, false>(bd, p, of, bf, k, x);
     }
     if (q + 1 >= apa || ai + 1 >= na) break;   // (uniform)
     load(++ai, v);
@@ -701,36 +742,29 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_fwd_kernel(WPass p, WArrs arrs, 
 
 // Wrapped products (la + lb - 1 = N + ntop): the last inverse pass wrote c[j] + c[N + j] mod 17
 // at j < ntop.  c[N + j] (sum group: of the group's sum) has only the terms a[i] b[N + j - i]
-// with i > N + j - lb (ntop - j <= 16 of them): computed from the bytes by the few threads
-// that hold such j, after the pass's stores (a rare path outside the unrolled store loop).
-// Returns 1 + the largest index it left a non-zero byte at (0: none).
-// (rr: the bytes this thread's pass stored, c[j] + c[N + j] mod 17 at the wrapped positions)
-template <class G>
-__device__ __forceinline__ uint32_t wrap_fix(const WJob& jb, uint32_t wrapped, const WPass& p, uint32_t tile,
-                                          uint32_t bf, int LF, uint64_t N, const uint32_t* rr) {
-  uint32_t last = 0;
-  // the pass's own byte stores at these positions complete before they are overwritten here
-  __builtin_amdgcn_s_waitcnt(0);
-  for (int k = 0; k < G::E; k++) {
-    if (!(wrapped >> k & 1)) continue;
-    const uint64_t idx = G::index(p, tile, bf + ((uint32_t)k << LF));
-    const uint64_t j = (N - idx) & (N - 1);
-    uint32_t s = 0;
-    for (int g = 0; g <= jb.ngroup; g++) {
-      const uint8_t* a = g ? jb.ga8[g - 1] : jb.a8;
-      const uint8_t* b = g ? jb.gb8[g - 1] : jb.b8;
-      const uint64_t la = g ? jb.gla[g - 1] : jb.la, lb = g ? jb.glb[g - 1] : jb.lb;
-      if (la + lb - 1 <= N + j) continue;   // (a shorter member: no term reaches c[N + j])
-      for (uint64_t i = N + j + 1 - lb; i < la; i++) s += (a[i] % 17u) * (b[N + j - i] % 17u);
-    }
-    s %= 17u;
-    const uint32_t lo = (rr[k] + 17u - s) % 17u;
-    jb.out8[j] = (uint8_t)lo;
-    jb.out8[N + j] = (uint8_t)s;
-    if (lo) last = max(last, (uint32_t)j + 1u);
-    if (s) last = max(last, (uint32_t)(N + j) + 1u);
+// with i > N + j - lb (ntop - j <= 16 of them): computed from the bytes after the pass, by this
+// small launch (round 4: inlined into the pass kernel, its loops held registers in the hot path).
+// Block = job (jobs without a wrapped top return at once), thread j < ntop = position j; a job
+// with a trimmed-length word takes the positions' maximum into it (the pass left them out).
+__global__ __launch_bounds__(64) void wrap_fix_kernel(WJobs jobs, uint64_t N) {
+  const WJob& jb = jobs.j[blockIdx.x];
+  const uint32_t ntop = (uint32_t)jb.ntop, j = threadIdx.x;
+  if (j >= ntop) return;
+  uint32_t s = 0;
+  for (int g = 0; g <= jb.ngroup; g++) {
+    const uint8_t* a = g ? jb.ga8[g - 1] : jb.a8;
+    const uint8_t* b = g ? jb.gb8[g - 1] : jb.b8;
+    const uint64_t la = g ? jb.gla[g - 1] : jb.la, lb = g ? jb.glb[g - 1] : jb.lb;
+    if (la + lb - 1 <= N + j) continue;   // (a shorter member: no term reaches c[N + j])
+    for (uint64_t i = N + j + 1 - lb; i < la; i++) s += (a[i] % 17u) * (b[N + j - i] % 17u);
   }
-  return last;
+  s %= 17u;
+  const uint32_t lo = (jb.out8[j] + 17u - s) % 17u;
+  jb.out8[j] = (uint8_t)lo;
+  jb.out8[N + j] = (uint8_t)s;
+  uint32_t last = lo ? j + 1u : 0u;
+  if (s) last = (uint32_t)(N + j) + 1u;
+  if (jb.nz && last) atomicMax(jb.nz, last);
 }
 
 // Inverse (DIT) pass, u32 in place (the job's C); the final pass (TO_U8) scales by N^-1 (normal form,
@@ -740,7 +774,7 @@ __device__ __forceinline__ uint32_t wrap_fix(const WJob& jb, uint32_t wrapped, c
 // Block (x, y) runs tile x of jobs y jpb .. y jpb + jpb - 1 (< nj) one after another, loading the
 // column factors and stage twiddles once for all of them.
 template <int TB, int R, int M, bool TO_U8, class F, bool COLT = false>
-__global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, WTw tw, uint32_t ninv, int nj, int jpb) {
+__global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs jobs, WTw tw, uint32_t ninv, int nj, int jpb) {
   using G = Eng<TB, R, M, F>;
   static_assert(G::NT == wt_nt(TB), "tile block size");
   __shared__ uint32_t Tsm[1 << M];
@@ -759,7 +793,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
   auto load = [&](int j) {
     const TileBuf bd(jobs.j[j].C + tb);
 #pragma unroll
-    for (int k = 0; k < G::E; k++) v[k] = bd.ld(G::template toff_k<0, true>(p, o0, b0, k));
+    for (int k = 0; k < G::E; k++) v[k] = G::template ldk<0, true>(bd, p, o0, b0, k);
   };
   load(ji);   // (the first job's loads go out before the tables')
   uint32_t cl[G::HIGH ? G::E : 1], ch[G::HIGH && !COLT ? G::E : 1];
@@ -767,7 +801,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
       if constexpr (COLT) {
-        cl[k] = TileBuf(colt).ld(G::template toff_k<0, true>(p, o0, b0, k));
+        cl[k] = G::template ldk<0, true>(TileBuf(colt), p, o0, b0, k);
       } else {
         const uint32_t ex = G::col_exp(p, tile, b0 + ((uint32_t)k << L0));   // roots of tw (inverse or forward)
         cl[k] = tw.lo[ex & 4095u];
@@ -776,6 +810,11 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
     }
   }
   load_pass_tw<M, G::NT>(Tsm, tw.small);
+  // (COLT byte outputs) x mod 17 for x < M17_LUT, read at F::out17_idx
+  __shared__ uint8_t m17[TO_U8 && COLT ? M17_LUT : 1];
+  if constexpr (TO_U8 && COLT) {
+    for (uint32_t i = tid; i < M17_LUT; i += G::NT) m17[i] = (uint8_t)(i % 17u);
+  }
   constexpr int LF = G::lbq(G::NR - 1, true);
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, true);
   const uint32_t of = G::toff(p, bf);
@@ -792,9 +831,8 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
       uint32_t a1[G::E], a2[G::E];
 #pragma unroll
       for (int k = 0; k < G::E; k++) {
-        const uint32_t o = G::template toff_k<0, true>(p, o0, b0, k);
-        a1[k] = TileBuf(s1t).ld(o);
-        a2[k] = s2 ? TileBuf(s2t).ld(o) : 0u;
+        a1[k] = G::template ldk<0, true>(TileBuf(s1t), p, o0, b0, k);
+        a2[k] = s2 ? G::template ldk<0, true>(TileBuf(s2t), p, o0, b0, k) : 0u;
       }
 #pragma unroll
       for (int k = 0; k < G::E; k++) v[k] = F::sum(v[k], a1[k], a2[k]);
@@ -809,7 +847,6 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
     // (q = 0: the stage twiddles are in LDS; q > 0: the previous job's last exchange reads are done)
     __syncthreads();
     G::template pass<true>(v, tid, bufs, 0, Tsm);
-    uint32_t wrapped = 0;   // elements of this thread that hold c[j] + c[N + j] (j < ntop)
     uint32_t last = 0;      // 1 + the largest index this thread left a non-zero byte at
     const uint32_t lim = out_len < N ? (uint32_t)out_len : N;
     const uint32_t ntop = (uint32_t)jb.ntop;   // (read once: the byte stores below may alias the job table)
@@ -817,7 +854,7 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
       const TileBuf bd(jb.C + tb);
 #pragma unroll
       for (int k = 0; k < G::E; k++)   // (the standalone inverse's last pass; poly_mul's 3-pass middle one)
-        bd.st(G::template toff_k<G::NR - 1, true>(p, of, bf, k), F::canon(v[k]));
+        G::template stk<G::NR - 1, true>(bd, p, of, bf, k, F::canon(v[k]));
     } else {
       // poly_mul runs its inverse with the FORWARD roots (no inverse table in LDS): that yields
       // N c[-idx mod N], so the coefficient lands at the negated position.  Every byte is computed
@@ -828,21 +865,16 @@ __global__ __launch_bounds__(wt_nt(TB)) void wt_inv_kernel(WPass p, WJobs jobs, 
 #pragma unroll
       for (int k = 0; k < G::E; k++) {
         jj[k] = (N - ((uint32_t)tb + G::template toff_k<G::NR - 1, true>(p, of, bf, k))) & (N - 1);
-        rr[k] = COLT ? F::out17s(v[k]) : F::out17(v[k], ninv);
+        rr[k] = COLT ? (uint32_t)m17[F::out17_idx(v[k])] : F::out17(v[k], ninv);
       }
 #pragma unroll
       for (int k = 0; k < G::E; k++) bo.stb(jj[k], rr[k]);
-      // the wrapped positions and the trimmed length only when the job has them (uniform: the
-      // prover's batched products want neither, and the bookkeeping was ~7 VALU per element)
-      if (ntop) {   // (j < ntop <= 16 implies j < lim)
-#pragma unroll
-        for (int k = 0; k < G::E; k++) wrapped |= jj[k] < ntop ? 1u << k : 0u;
-      }
+      // the trimmed length only when the job has one (uniform: the prover's batched products do
+      // not; the wrapped positions j < ntop are fixed, and counted, by wrap_fix_kernel)
       if (jb.nz) {
 #pragma unroll
         for (int k = 0; k < G::E; k++) last = max(last, (jj[k] < lim && jj[k] >= ntop && rr[k]) ? jj[k] + 1u : 0u);
       }
-      if (wrapped) last = max(last, wrap_fix<G>(jb, wrapped, p, tile, bf, LF, 1ull << p.k, rr));
     }
 
     // Trimmed length (src/poly.h:20-38).  The top coefficient of a single product is
@@ -1328,6 +1360,12 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
     rc = i == 0 ? inv_m<TB, true, F>(Ms[i], p, jj, ni, twi, ninv, st)
                 : inv_m<TB, false, F>(Ms[i], p, jj, ni, twf, 0u, st);
     if (rc) return rc;
+  }
+  bool wrapped = false;
+  for (int j = 0; j < ni; j++) wrapped |= ic.j[j].ntop > 0;
+  if (wrapped) {   // (after the last inverse pass's byte stores, on the same stream)
+    hipLaunchKernelGGL(wrap_fix_kernel, dim3(ni), dim3(64), 0, st, ic, 1ull << k);
+    PLK_HIP(hipGetLastError());
   }
   return PLK_OK;
 }
