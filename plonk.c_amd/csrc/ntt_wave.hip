@@ -815,7 +815,6 @@ __global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs job
   if constexpr (TO_U8 && COLT) {
     for (uint32_t i = tid; i < M17_LUT; i += G::NT) m17[i] = (uint8_t)(i % 17u);
   }
-  constexpr int LF = G::lbq(G::NR - 1, true);
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, true);
   const uint32_t of = G::toff(p, bf);
   const uint32_t N = 1u << p.k;   // (k <= 27: every index fits 32 bits)
