@@ -942,8 +942,8 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
       const TileBuf b_a(P.A + tb), b_b(P.B + tb);
 #pragma unroll
       for (int k = 0; k < G::E; k++) {
-        va[k] = b_a.ld(b0 + ((uint32_t)k << L0));
-        vb[k] = b_b.ld(b0 + ((uint32_t)k << L0));
+        va[k] = b_a.ld(b0, (uint32_t)k << L0);   // (the per-register part in the SGPR offset)
+        vb[k] = b_b.ld(b0, (uint32_t)k << L0);
       }
       if (q == 0) __syncthreads();   // (the previous item's last exchange read)
       // (afix / bfix: the operand's transform is finished -- plk_wave_pretransform / wt_fixfwd_kernel
@@ -961,16 +961,16 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
       for (int k = 0; k < G::E; k++) va[k] = F::pmul(va[k], vb[k]);
       if (GRP && q) {
 #pragma unroll
-        for (int k = 0; k < G::E; k++) va[k] = F::add2(va[k], b_c.ld(b0 + ((uint32_t)k << L0)));
+        for (int k = 0; k < G::E; k++) va[k] = F::add2(va[k], b_c.ld(b0, (uint32_t)k << L0));
       }
       if (!GRP || q == J.ncm) break;
 #pragma unroll
-      for (int k = 0; k < G::E; k++) b_c.st(b0 + ((uint32_t)k << L0), va[k]);
+      for (int k = 0; k < G::E; k++) b_c.st(b0, (uint32_t)k << L0, va[k]);
       __builtin_amdgcn_s_waitcnt(0);   // (the parked words are this thread's own: stored before reloaded)
     }
     G::template pass<true, PLK_NTT_CENTER_SWZ>(va, tid, bufs, xc, Tf);
 #pragma unroll
-    for (int k = 0; k < G::E; k++) b_c.st(bf + ((uint32_t)k << LF), va[k]);
+    for (int k = 0; k < G::E; k++) b_c.st(bf, (uint32_t)k << LF, va[k]);
   }
 }
 
@@ -991,12 +991,12 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_fi
   uint32_t v[G::E];
   const TileBuf bt(d + ((uint64_t)tile << TB));   // (the lo = 0 pass: consecutive words)
 #pragma unroll
-  for (int k = 0; k < G::E; k++) v[k] = bt.ld(b0 + ((uint32_t)k << L0));
+  for (int k = 0; k < G::E; k++) v[k] = bt.ld(b0, (uint32_t)k << L0);
   load_pass_tw<TB, G::NT>(Tlds, twf.small);
   __syncthreads();
   G::template pass<false, false>(v, tid, bufs, G::XCH, Tlds);
 #pragma unroll
-  for (int k = 0; k < G::E; k++) bt.st(b0 + ((uint32_t)k << L0), v[k]);
+  for (int k = 0; k < G::E; k++) bt.st(b0, (uint32_t)k << L0, v[k]);
 }
 
 // Column-factor table of a 2-pass plan (lo = TB, M = k - TB): entry i = the high pass's factor
