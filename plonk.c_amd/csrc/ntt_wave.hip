@@ -656,7 +656,8 @@ __device__ __forceinline__ void load_pass_tw_pairs(uint32_t* Tsm, const uint32_t
 // COLT: the column factors come from tw.col (one word per element, indexed like the data)
 // instead of lo * hi (two words and a multiply per element).
 template <int TB, int R, int M, bool FROM_U8, class F, bool COLT = false>
-__global__ __launch_bounds__(wt_nt(TB), 8) void wt_fwd_kernel(WPass p, WArrs arrs, WTw tw, int na, int apa) {
+__global__ __launch_bounds__(wt_nt(TB), TB == 13 && M == TB ? 4 : 8) void wt_fwd_kernel(WPass p, WArrs arrs, WTw tw, int na,
+                                                                                       int apa) {
   using G = Eng<TB, R, M, F>;
   static_assert(G::NT == wt_nt(TB), "tile block size");
   constexpr bool PW = F::ADIC == f29::TWO_ADICITY;   // {w, p - w} pairs (F29's lazy DIF)
