@@ -747,20 +747,47 @@ __global__ __launch_bounds__(wt_nt(TB), TB == 13 && M == TB ? 4 : 8) void wt_fwd
 // small launch (round 4: inlined into the pass kernel, its loops held registers in the hot path).
 // Block = job (jobs without a wrapped top return at once), thread j < ntop = position j; a job
 // with a trimmed-length word takes the positions' maximum into it (the pass left them out).
+// Every term a[i] b[N + j - i] of c[N + j] (j < ntop <= 16) has i in the top 16 bytes of a and
+// N + j - i in the top 16 of b (la + lb - 1 - N <= 16, also for a group's shorter members): the
+// block stages those bytes in LDS with ONE load each, then thread j sums from LDS -- one memory
+// round trip for the whole fix (a loop of dependent byte loads per term took ~5 us per launch).
 __global__ __launch_bounds__(64) void wrap_fix_kernel(WJobs jobs, uint64_t N) {
   const WJob& jb = jobs.j[blockIdx.x];
-  const uint32_t ntop = (uint32_t)jb.ntop, j = threadIdx.x;
+  const uint32_t ntop = (uint32_t)jb.ntop;
+  if (!ntop) return;   // (uniform: a job without a wrapped top)
+  __shared__ uint32_t A[3][16], B[3][16];   // [member][q] = byte la - 16 + q (0 below index 0)
+  const uint32_t t = threadIdx.x;
+  if (t < 48) {
+    const int g = (int)(t >> 4), q = (int)(t & 15);
+    uint32_t va = 0, vb = 0;
+    if (g <= jb.ngroup) {
+      const uint8_t* a = g ? jb.ga8[g - 1] : jb.a8;
+      const uint8_t* b = g ? jb.gb8[g - 1] : jb.b8;
+      const uint64_t la = g ? jb.gla[g - 1] : jb.la, lb = g ? jb.glb[g - 1] : jb.lb;
+      if (la + (uint64_t)q >= 16) va = a[la - 16 + q] % 17u;
+      if (lb + (uint64_t)q >= 16) vb = b[lb - 16 + q] % 17u;
+    }
+    A[g][q] = va;
+    B[g][q] = vb;
+  }
+  const uint32_t j = t;
+  const uint32_t cur = j < ntop ? jb.out8[j] : 0u;   // (c[j] + c[N + j] mod 17, the pass's byte)
+  __syncthreads();
   if (j >= ntop) return;
   uint32_t s = 0;
   for (int g = 0; g <= jb.ngroup; g++) {
-    const uint8_t* a = g ? jb.ga8[g - 1] : jb.a8;
-    const uint8_t* b = g ? jb.gb8[g - 1] : jb.b8;
     const uint64_t la = g ? jb.gla[g - 1] : jb.la, lb = g ? jb.glb[g - 1] : jb.lb;
     if (la + lb - 1 <= N + j) continue;   // (a shorter member: no term reaches c[N + j])
-    for (uint64_t i = N + j + 1 - lb; i < la; i++) s += (a[i] % 17u) * (b[N + j - i] % 17u);
+    // i in [N + j + 1 - lb, la): q = i - la + 16, b index N + j - i = lb - 16 + (16 + N + j + lb... )
+    const int d = (int)(la + lb - 1 - N - j);   // terms: i = la - d .. la - 1 (d <= 16)
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      // i = la - d + u: a at q = 16 - d + u, b index N + j - i = lb - 1 - u: q = 15 - u
+      if (u < d) s += A[g][16 - d + u] * B[g][15 - u];
+    }
   }
   s %= 17u;
-  const uint32_t lo = (jb.out8[j] + 17u - s) % 17u;
+  const uint32_t lo = (cur + 17u - s) % 17u;
   jb.out8[j] = (uint8_t)lo;
   jb.out8[N + j] = (uint8_t)s;
   uint32_t last = lo ? j + 1u : 0u;
