@@ -61,6 +61,9 @@ namespace {
 #ifndef PLK_NTT_CENTER_SWZ
 #define PLK_NTT_CENTER_SWZ 0   // center exchanges: 0 padded (2, swizzled only where the padding conflicts, spills)
 #endif
+#ifndef PLK_NTT_WRAP_INLINE
+#define PLK_NTT_WRAP_INLINE 0  // 1: wrapped tops fixed at the end of the last inverse pass (no wrap_fix_kernel launch)
+#endif
 #ifndef PLK_NTT_CW13
 #define PLK_NTT_CW13 8         // min waves per SIMD (launch bound): 8 = two 1024-thread blocks per CU
 #endif
@@ -920,6 +923,57 @@ __global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs job
     if (q + 1 >= jpb || ji + 1 >= nj) break;   // (uniform)
     load(++ji);
   }
+#if PLK_NTT_WRAP_INLINE
+  // Wrapped tops (wrap_fix_kernel's work, done by the block whose tile holds the position, after
+  // its jobs: no launch of its own).  Position j < ntop is element (N - j) mod N.
+  if constexpr (TO_U8) {
+    const int j0 = (int)blockIdx.y * jpb;
+    bool any = false;
+    for (int q = j0; q <= ji; q++) any |= jobs.j[q].ntop > 0;
+    if (any) {
+      __builtin_amdgcn_s_waitcnt(0);   // this thread's byte stores complete ...
+      __syncthreads();                 // ... and every other thread's
+      for (int q = j0; q <= ji; q++) {
+        const WJob& jb = jobs.j[q];
+        const uint32_t ntop = (uint32_t)jb.ntop, j = tid;
+        if (j >= ntop) continue;
+        const uint32_t idx = (N - j) & (N - 1);
+        uint32_t tl;   // the tile of element idx (Eng::index inverted)
+        if (M == TB) {
+          tl = idx >> TB;
+        } else {
+          constexpr int cb = TB - M;
+          const int sh = p.lo - cb;
+          tl = ((idx >> (p.lo + M)) << sh) | ((idx & ((1u << p.lo) - 1)) >> cb);
+        }
+        if (tl != tile) continue;
+        uint32_t sum = 0;
+        for (int g = 0; g <= jb.ngroup; g++) {
+          const uint8_t* a = g ? jb.ga8[g - 1] : jb.a8;
+          const uint8_t* b = g ? jb.gb8[g - 1] : jb.b8;
+          const uint64_t la = g ? jb.gla[g - 1] : jb.la, lb = g ? jb.glb[g - 1] : jb.lb;
+          if (la + lb - 1 <= (uint64_t)N + j) continue;
+          const int d = (int)(la + lb - 1 - N - j);   // terms i = la - d + u, b index lb - 1 - u
+          uint32_t av[16], bv[16];
+#pragma unroll
+          for (int u = 0; u < 16; u++) {
+            av[u] = u < d ? a[la - d + u] : 0u;
+            bv[u] = u < d ? b[lb - 1 - u] : 0u;
+          }
+#pragma unroll
+          for (int u = 0; u < 16; u++) sum += (av[u] % 17u) * (bv[u] % 17u);
+        }
+        const uint32_t sv = sum % 17u;
+        const uint32_t lo = (jb.out8[j] + 17u - sv) % 17u;
+        jb.out8[j] = (uint8_t)lo;
+        jb.out8[N + j] = (uint8_t)sv;
+        uint32_t lst = lo ? j + 1u : 0u;
+        if (sv) lst = N + j + 1u;
+        if (jb.nz && lst) atomicMax(jb.nz, lst);
+      }
+    }
+  }
+#endif
 }
 
 // Center of poly_mul: last forward pass (lo = 0) of a and b, pointwise product (plus a merged
@@ -1390,7 +1444,7 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
   }
   bool wrapped = false;
   for (int j = 0; j < ni; j++) wrapped |= ic.j[j].ntop > 0;
-  if (wrapped) {   // (after the last inverse pass's byte stores, on the same stream)
+  if (wrapped && !PLK_NTT_WRAP_INLINE) {   // (after the last inverse pass's byte stores, on the same stream)
     hipLaunchKernelGGL(wrap_fix_kernel, dim3(ni), dim3(64), 0, st, ic, 1ull << k);
     PLK_HIP(hipGetLastError());
   }
