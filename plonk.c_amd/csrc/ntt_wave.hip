@@ -62,7 +62,7 @@ namespace {
 #define PLK_NTT_CENTER_SWZ 0   // center exchanges: 0 padded (2, swizzled only where the padding conflicts, spills)
 #endif
 #ifndef PLK_NTT_WRAP_INLINE
-#define PLK_NTT_WRAP_INLINE 0  // 1: wrapped tops fixed at the end of the last inverse pass (no wrap_fix_kernel launch)
+#define PLK_NTT_WRAP_INLINE 1  // wrapped tops fixed at the end of the last inverse pass (0: wrap_fix_kernel launches)
 #endif
 #ifndef PLK_NTT_CW13
 #define PLK_NTT_CW13 8         // min waves per SIMD (launch bound): 8 = two 1024-thread blocks per CU
