@@ -67,6 +67,25 @@ namespace {
 #ifndef PLK_NTT_CW13
 #define PLK_NTT_CW13 8         // min waves per SIMD (launch bound): 8 = two 1024-thread blocks per CU
 #endif
+#ifndef PLK_NTT_CENTER_PF
+#define PLK_NTT_CENTER_PF 0    // center: the next item's A loaded during the current item's inverse rounds
+#endif
+// Round-4 latency-hiding variants, per-kernel times from one box (tools/ab_kernels.sh, prover 2^20,
+// forward M = 8 / forward M = 9 / inverse M = 8 passes, us): all off 46.9 / 39.4 / 30.9;
+// PREFETCH + XCH_REMAT 45.2 / 38.6 / 31.7 (the inverse passes' prefetch: +0.8, so off there);
+// U8_KRSRC alone 50.5 / 43.3 / 30.5 (slower); PREFETCH alone spilled (41.8 us inverse).
+#ifndef PLK_NTT_PREFETCH
+#define PLK_NTT_PREFETCH 1     // forward pass kernels load array i+1 before array i's butterflies
+#endif
+#ifndef PLK_NTT_PREFETCH_INV
+#define PLK_NTT_PREFETCH_INV 0 // ... and the inverse ones job i+1 before job i's
+#endif
+#ifndef PLK_NTT_XCH_REMAT
+#define PLK_NTT_XCH_REMAT 1    // swizzled exchange addresses recomputed per pass, not held across the array loop
+#endif
+#ifndef PLK_NTT_U8_KRSRC
+#define PLK_NTT_U8_KRSRC 0     // byte loads: one buffer resource per register index (one offset VGPR)
+#endif
 constexpr int wt_rc(int TB) { return TB == 13 ? PLK_NTT_RC13 : PLK_NTT_R12; }
 constexpr int wt_ntc(int TB) { return 1 << (TB - wt_rc(TB)); }
 // register bits per thread for a tile size; the block has 2^(TB-R) threads
@@ -507,7 +526,13 @@ struct Eng {
       // moves bits < 5 and the bits >= 5 of k << lb are disjoint from base's, so the word is
       // (xw ^ lo_k) + hi_k: one XOR with a constant (none when lo_k = 0) and the rest in the
       // ds_write / ds_read offset, on byte addresses (no per-element shift)
-      const uint32_t xw4 = (bf ^ swz_h<Q, INV>(bf)) << 2, xr4 = (bt ^ swz_h<Q, INV>(bt)) << 2;
+      uint32_t xw4 = (bf ^ swz_h<Q, INV>(bf)) << 2, xr4 = (bt ^ swz_h<Q, INV>(bt)) << 2;
+      if (PLK_NTT_XCH_REMAT) {
+        // opaque here: the per-register addresses (xw4 ^ lo) are formed at each use -- one XOR
+        // each -- instead of ~7 registers per base live across a kernel's whole array loop
+        asm volatile("" : "+v"(xw4));
+        asm volatile("" : "+v"(xr4));
+      }
       char* bb = reinterpret_cast<char*>(buf);
 #pragma unroll
       for (int k = 0; k < E; k++) {
@@ -681,6 +706,18 @@ __global__ __launch_bounds__(wt_nt(TB), TB == 13 && M == TB ? 4 : 8) void wt_fwd
     if constexpr (FROM_U8) {
       const uint64_t ls = ar.ls;
       const uint32_t lim = ls > tb ? (uint32_t)(ls - tb < 0xFFFFFFFFull ? ls - tb : 0xFFFFFFFFull) : 0u;
+      if constexpr (PLK_NTT_U8_KRSRC && !(PLK_NTT_DIAG & 8) && G::template ksplit<0, false>()) {
+        // register index k reads byte o0 + kpart(k): its own resource based at kpart(k) with the
+        // range shortened by as much, so one offset VGPR serves all E loads and the range check
+        // still zero-pads past the operand
+#pragma unroll
+        for (int k = 0; k < G::E; k++) {
+          const uint32_t kp = G::template kpart<0, false>(p, k);
+          v[k] = TileBuf(ar.s8 + tb + kp, lim > kp ? lim - kp : 0u).ldb(o0);
+          if (!PLK_NTT_BYTE_LUT) v[k] = F::byte_val(v[k]);
+        }
+        return;
+      }
       const TileBuf bs(ar.s8 + tb, lim);
 #pragma unroll
       for (int k = 0; k < G::E; k++) {
@@ -728,6 +765,11 @@ __global__ __launch_bounds__(wt_nt(TB), TB == 13 && M == TB ? 4 : 8) void wt_fwd
 #pragma unroll
       for (int k = 0; k < G::E; k++) v[k] = lut[v[k]];
     }
+    const bool more = q + 1 < apa && ai + 1 < na;   // (uniform)
+    // the next array's loads go out before this one's rounds, so their latency hides behind the
+    // butterflies (the barriers wait for LDS only: the loads stay in flight across them)
+    uint32_t nv[G::E];
+    if (PLK_NTT_PREFETCH && more) load(ai + 1, nv);
     G::template pass<false, 1, PW, true>(v, tid, bufs, 0, Tsm);
     const TileBuf bd(arrs.a[ai].d + tb);
 #pragma unroll
@@ -738,8 +780,14 @@ __global__ __launch_bounds__(wt_nt(TB), TB == 13 && M == TB ? 4 : 8) void wt_fwd
       else x = F::canon(x);   // the lo = 0 pass is the last one of a standalone transform
       G::template stk<G::NR - 1, false>(bd, p, of, bf, k, x);
     }
-    if (q + 1 >= apa || ai + 1 >= na) break;   // (uniform)
-    load(++ai, v);
+    if (!more) break;
+    ++ai;
+    if constexpr (PLK_NTT_PREFETCH) {
+#pragma unroll
+      for (int k = 0; k < G::E; k++) v[k] = nv[k];
+    } else {
+      load(ai, v);
+    }
   }
 }
 
@@ -808,6 +856,9 @@ template <int TB, int R, int M, bool TO_U8, class F, bool COLT = false>
 __global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs jobs, WTw tw, uint32_t ninv, int nj, int jpb) {
   using G = Eng<TB, R, M, F>;
   static_assert(G::NT == wt_nt(TB), "tile block size");
+  // prefetch where the registers allow it: the wide byte-output passes have none to spare (their
+  // spill reloads would wait for the prefetched loads anyway)
+  constexpr bool PF = PLK_NTT_PREFETCH_INV && !(TO_U8 && (M > 8 || M < 4));
   __shared__ uint32_t Tsm[1 << M];
   __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
   const uint32_t tid = threadIdx.x;
@@ -821,12 +872,12 @@ __global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs job
   constexpr int L0 = G::lbq(0, true);
   int ji = (int)blockIdx.y * jpb;
   uint32_t v[G::E];
-  auto load = [&](int j) {
+  auto load = [&](int j, uint32_t (&x)[G::E]) {
     const TileBuf bd(jobs.j[j].C + tb);
 #pragma unroll
-    for (int k = 0; k < G::E; k++) v[k] = G::template ldk<0, true>(bd, p, o0, b0, k);
+    for (int k = 0; k < G::E; k++) x[k] = G::template ldk<0, true>(bd, p, o0, b0, k);
   };
-  load(ji);   // (the first job's loads go out before the tables')
+  load(ji, v);   // (the first job's loads go out before the tables')
   uint32_t cl[G::HIGH ? G::E : 1], ch[G::HIGH && !COLT ? G::E : 1];
   if (G::HIGH) {
 #pragma unroll
@@ -874,6 +925,10 @@ __global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs job
         else v[k] = F::mul(v[k], F::colf(cl[k], ch[k]));
       }
     }
+    const bool more = q + 1 < jpb && ji + 1 < nj;   // (uniform)
+    // the next job's loads before this one's rounds (wt_fwd_kernel)
+    uint32_t nv[G::E];
+    if (PF && more) load(ji + 1, nv);
     // (q = 0: the stage twiddles are in LDS; q > 0: the previous job's last exchange reads are done)
     __syncthreads();
     G::template pass<true>(v, tid, bufs, 0, Tsm);
@@ -920,8 +975,14 @@ __global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs job
         if (tid == 0 && last) atomicMax(jb.nz, last);
       }
     }
-    if (q + 1 >= jpb || ji + 1 >= nj) break;   // (uniform)
-    load(++ji);
+    if (!more) break;
+    ++ji;
+    if constexpr (PF) {
+#pragma unroll
+      for (int k = 0; k < G::E; k++) v[k] = nv[k];
+    } else {
+      load(ji, v);
+    }
   }
 #if PLK_NTT_WRAP_INLINE
   // Wrapped tops (wrap_fix_kernel's work, done by the block whose tile holds the position, after
@@ -1006,6 +1067,14 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
   // the twiddle table first (a "first item" flag inside the loop had the compiler hoist the
   // table's addresses out of the loop and spill them)
   load_pass_tw<TB, G::NT>(Tlds, twf.small);
+  // the item after `it` in this block's stride that has a job (items of padding slots skipped)
+  auto next_item = [&](uint32_t it) {
+    for (it += gridDim.x; it < items && sc.job[it / tiles] < 0; it += gridDim.x) {
+    }
+    return it;
+  };
+  uint32_t pa[G::E];   // (PLK_NTT_CENTER_PF) the next item's A words, loaded during this item's inverse rounds
+  bool have = false;   // (uniform) pa holds this item's A
   for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
     const uint32_t slot = it / tiles, tile = it - slot * tiles;
     const int job = sc.job[slot];
@@ -1022,9 +1091,11 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
     for (int q = 0;; q++) {
       const WJob& P = jobs.j[q ? J.cm[q - 1] : job];
       const TileBuf b_a(P.A + tb), b_b(P.B + tb);
+      // (a block's first item loads its A here; later ones found it prefetched)
+      const bool pre = PLK_NTT_CENTER_PF && q == 0 && have;
 #pragma unroll
       for (int k = 0; k < G::E; k++) {
-        va[k] = b_a.ld(b0, (uint32_t)k << L0);   // (the per-register part in the SGPR offset)
+        va[k] = pre ? pa[k] : b_a.ld(b0, (uint32_t)k << L0);   // (the per-register part in the SGPR offset)
         vb[k] = b_b.ld(b0, (uint32_t)k << L0);
       }
       if (q == 0) __syncthreads();   // (the previous item's last exchange read)
@@ -1049,6 +1120,18 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
 #pragma unroll
       for (int k = 0; k < G::E; k++) b_c.st(b0, (uint32_t)k << L0, va[k]);
       __builtin_amdgcn_s_waitcnt(0);   // (the parked words are this thread's own: stored before reloaded)
+    }
+    if (PLK_NTT_CENTER_PF) {
+      // the next item's A goes out before this one's inverse rounds (no job writes an array
+      // another job reads, and the same job's next item is another tile)
+      const uint32_t nit = next_item(it);
+      have = nit < items;
+      if (have) {
+        const uint32_t ns = nit / tiles;
+        const TileBuf b_n(jobs.j[sc.job[ns]].A + ((uint64_t)(nit - ns * tiles) << TB));
+#pragma unroll
+        for (int k = 0; k < G::E; k++) pa[k] = b_n.ld(b0, (uint32_t)k << L0);
+      }
     }
     G::template pass<true, PLK_NTT_CENTER_SWZ>(va, tid, bufs, xc, Tf);
 #pragma unroll
