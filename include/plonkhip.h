@@ -85,7 +85,9 @@ enum {
   PLK_OPT_PROVE_DERIVE_T2A = 18, /* 1: round 3's A2 B2 from a_x b_x by an elementwise pass (0: its own product) */
   PLK_OPT_NTT_TABLE_SHARE = 19,  /* 1: a table pass runs several arrays of one tile per block (column words read once) */
   PLK_OPT_NTT_LAUNCH_LOG = 20,   /* diagnostics: 1 records the NTT passes' launch plans (plk_ntt_launch_log) */
-  PLK_OPT_COUNT = 21
+  PLK_OPT_PROVE_FUSE_DIV = 21,   /* 1: round 5's numerators and their divisions by x - z, x - z omega in one
+                                    launch (single-pass suffix scan); 0: numerators, then the apply launch */
+  PLK_OPT_COUNT = 22
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
 /* Diagnostics for the offline roofline tools: with PLK_OPT_NTT_LAUNCH_LOG = 1 every NTT pass launch

@@ -901,6 +901,140 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(LinDivs L, const
   }
 }
 
+// Round 5 in ONE launch (PLK_OPT_PROVE_FUSE_DIV): each block forms its 4096-coefficient chunk
+// of the numerator in registers (lincomb_scan_kernel's loads), publishes the chunk's aggregate
+// as one 64-bit word {epoch, sum}, then reduces the aggregates of every later chunk and finishes
+// its quotient bytes as lin_scan_apply_kernel does -- the numerator is never stored or re-read.
+// Chunks are taken in REVERSE block order: a block waits only for chunks owned by blocks that
+// were dispatched before it (running or done), so the waits cannot deadlock whatever the
+// residency.  A wait that still sees a stale word after ~2^22 polls gives up and marks the
+// division's remainder word with SCAN_TIMEOUT (reported as an internal error, never a proof).
+constexpr uint32_t SCAN_TIMEOUT = 1u << 30;
+__global__ __launch_bounds__(SCAN_T) void lincomb_divide_kernel(LcBatch b, LinDivs L, const uint8_t* __restrict__ S,
+                                                               unsigned long long* __restrict__ fw0, uint32_t fw_stride,
+                                                               uint32_t epoch) {
+  const int d = blockIdx.y;
+  const LcArgs& a = b.a[d];
+  const LinDiv& D = L.d[d];
+  const int c = (int)(gridDim.x - 1 - blockIdx.x);   // this block's chunk
+  if (c >= D.nb) return;
+  unsigned long long* fw = fw0 + (uint64_t)d * fw_stride;
+  // (the scalars are uniform: read into SGPRs, so the power tables below cost no VGPRs)
+  uint32_t cf[LC_MAX];
+#pragma unroll
+  for (int t = 0; t < LC_MAX; t++) cf[t] = __builtin_amdgcn_readfirstlane(t < a.nt ? S[a.slot[t]] : 0u);
+  const uint32_t sc = __builtin_amdgcn_readfirstlane(S[a.scale]);
+  const uint32_t c0 = __builtin_amdgcn_readfirstlane(a.c0 >= 0 ? S[a.c0] : 0u);
+  const uint32_t c1 = __builtin_amdgcn_readfirstlane(a.c1 >= 0 ? S[a.c1] : 0u);
+  const uint64_t base = (uint64_t)c * SCAN_B + (uint64_t)threadIdx.x * SCAN_E;
+  const uint64_t nl = a.out_len;
+  uint32_t acc[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) acc[k] = 0;
+  if (base == 0) { acc[0] = c0; acc[1] = c1; }
+#pragma unroll
+  for (int t = 0; t < LC_MAX; t++) {
+    if (t < a.nt) {   // uniform
+      uint32_t w[4];
+      load16_masked(a.p[t], a.len[t], base, w);
+#pragma unroll
+      for (int k = 0; k < 16; k++) acc[k] += cf[t] * ((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+    }
+  }
+  const uint32_t av = __builtin_amdgcn_readfirstlane(S[D.aslot]);
+  uint32_t pw[16];
+  pw[0] = 1;
+#pragma unroll
+  for (int j = 1; j < 16; j++) pw[j] = pw[j - 1] * av % HFP;
+  // the chunk's numerator coefficients num[base + k] (0 past nl), packed, and the thread's part of
+  // the chunk aggregate sum_{i > 0} num[i] a^i ((base + k) mod 16 = k)
+  uint32_t nb8[4] = {0, 0, 0, 0}, agg = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint32_t v = base + k < nl ? hmod(hmod(acc[k]) * sc) : 0u;   // (acc <= 16 x 16 x 255 + 32)
+    nb8[k >> 2] |= v << (8 * (k & 3));
+    if (base + k > 0) agg += v * pw[k];
+  }
+  // publish the chunk aggregate
+  const uint32_t t = scan_block_sum(agg % HFP) % HFP;
+  if (threadIdx.x == 0)
+    __hip_atomic_store(fw + c, ((unsigned long long)epoch << 32) | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the aggregates of every later chunk (each word carries its own payload: no fence needed)
+  uint32_t carry = 0;
+  bool late = false;
+  for (int cb = c + 1 + (int)threadIdx.x; cb < D.nb; cb += SCAN_T) {
+    unsigned long long v = __hip_atomic_load(fw + cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t it = 0; (uint32_t)(v >> 32) != epoch; it++) {
+      if (it == (1u << 22)) { late = true; break; }
+      __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(fw + cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    carry += (uint32_t)v % HFP;
+  }
+  if (late) atomicOr(D.flag, SCAN_TIMEOUT);
+  // from here lin_scan_apply_kernel's work on the packed coefficients
+  uint32_t ipw[16];
+  ipw[0] = 1;
+  const uint32_t ai = hinv(av);
+#pragma unroll
+  for (int j = 1; j < 16; j++) ipw[j] = ipw[j - 1] * ai % HFP;
+  uint32_t w[SCAN_E], tot = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_E; k++) {
+    w[k] = base + k > 0 ? hmod(((nb8[k >> 2] >> (8 * (k & 3))) & 0xFFu) * pw[k]) : 0u;
+    tot += w[k];
+  }
+  // a = 0: q[j] = num[j + 1], which for the thread's last coefficient is the next thread's first
+  // (lane shuffle / LDS across waves) or, for the block's last thread, the next chunk's first
+  // coefficient (recomputed from the terms: nt byte loads, that thread only)
+  __shared__ uint32_t first[SCAN_T / 64 + 1];
+  const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+  uint32_t nxt = __shfl_down(nb8[0] & 0xFFu, 1, 64);
+  if (av == 0) {   // (uniform)
+    if (lane == 0) first[wv] = nb8[0] & 0xFFu;
+    if (threadIdx.x == SCAN_T - 1) {
+      const uint64_t i = base + 16;
+      uint32_t s = 0;
+      for (int u = 0; u < a.nt; u++) s += i < a.len[u] ? cf[u] * a.p[u][i] : 0u;
+      first[SCAN_T / 64] = i < nl ? hmod(hmod(s) * sc) : 0u;
+    }
+  }
+  // suffix sums: lanes, waves, then the later chunks' carry -- one barrier
+  const uint32_t suf = wave_suffix(tot);
+  const uint32_t cw = wave_sum(carry % HFP);
+  __shared__ uint32_t ws[2][SCAN_T / 64];
+  if (lane == 0) {
+    ws[0][wv] = suf;
+    ws[1][wv] = cw;
+  }
+  __syncthreads();
+  if (av == 0 && lane == 63) nxt = first[wv + 1];
+  uint32_t run = suf - tot;
+#pragma unroll
+  for (int u = 0; u < SCAN_T / 64; u++) run += (u > wv ? ws[0][u] : 0u) + ws[1][u];
+  const uint64_t ql = nl - 1;
+  uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = SCAN_E - 1; k >= 0; k--) {
+    const uint64_t j = base + k;   // run = sum_{i > j} w_i
+    if (j < ql) {
+      const uint32_t nx = k == 15 ? nxt : (nb8[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu;
+      const uint32_t v = av == 0 ? nx : run % HFP * ipw[(k + 1) & 15] % HFP;
+      o[k >> 2] |= v << (8 * (k & 3));
+      if (j == 0 && ((nb8[0] & 0xFFu) + av * v) % HFP) atomicOr(D.flag, 1u);
+    }
+    run += w[k];
+  }
+  uint8_t* q = D.q;
+  if (D.vec && base + 16 <= ql) {
+    *reinterpret_cast<uint4*>(q + base) = make_uint4(o[0], o[1], o[2], o[3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      if (base + k < ql) q[base + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
+  }
+}
+
 // (c) any other divisor: the reference's long division in one workgroup (only reached for
 // tiny non-subgroup H, e.g. n = 3).
 __global__ __launch_bounds__(256) void divide_general_kernel(const uint8_t* __restrict__ num, uint64_t nl,
@@ -1191,6 +1325,9 @@ struct plk_prover {
   int t2_sum = 0;                  // round 3: (a b) q_m + t_2 computed as one sum (in T2)
   uint64_t rem_blocks = 0;
   uint32_t* d_bsum = nullptr;      // scan block sums
+  unsigned long long* d_scanw = nullptr;   // lincomb_divide_kernel's chunk words {epoch, sum}
+  uint32_t scanw_stride = 0;       // words per division
+  uint32_t scan_epoch = 0;         // launches of lincomb_divide_kernel so far (0: none)
   PlkMsmResult* d_res = nullptr;   // 9 MSM records
   uint8_t* arena = nullptr;        // [9][cstride] committed polynomials
   size_t cstride = 0, cmax = 0;
@@ -1447,6 +1584,13 @@ int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs, const Lc
     nbmax = std::max(nbmax, nb);
   }
   if (!nd) return PLK_OK;
+  if (lcs && plk_opt(PLK_OPT_PROVE_FUSE_DIV) && (uint32_t)nbmax <= P->scanw_stride) {
+    if (++P->scan_epoch == 0) ++P->scan_epoch;   // (words hold 0 after create: never a live epoch)
+    hipLaunchKernelGGL(lincomb_divide_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, *lcs, L, P->d_S,
+                       P->d_scanw, P->scanw_stride, P->scan_epoch);
+    PLK_HIP(hipGetLastError());
+    return PLK_OK;
+  }
   if (lcs) hipLaunchKernelGGL(lincomb_scan_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, *lcs, L, P->d_S);
   else hipLaunchKernelGGL(lin_scan_sums_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, L, P->d_S);
   PLK_HIP(hipGetLastError());
@@ -1531,6 +1675,7 @@ int create_on(const plk_plonk_desc_t* d, int dev, plk_prover_t** out) {
                o_stat = B.take(4 * NSTAT), o_tick = B.take(4 * TICK_STRIDE * (EV_MAX + 1)),
                o_rem = B.take(P->zh_len / 1024 + 64),
                o_bsum = B.take(4 * ((L.lw + SCAN_B - 1) / SCAN_B + 2) + 4 * ((L.lzz + SCAN_B) / SCAN_B + 2)),
+               o_scanw = B.take(8 * 2 * ((std::max(L.lw, L.lzz) + SCAN_B) / SCAN_B + 2)),
                o_res = B.take(9 * sizeof(PlkMsmResult)),
                o_arena = B.take(9 * P->cstride);
   size_t o_polys[13];
@@ -1563,6 +1708,8 @@ int create_on(const plk_plonk_desc_t* d, int dev, plk_prover_t** out) {
   uint8_t* m = P->mem;
   P->d_srs = m + o_srs; P->d_zh = m + o_zh; P->d_h3 = m + o_h3; P->d_hinv = m + o_hinv; P->d_S = m + o_S;
   P->d_stat = (uint32_t*)(m + o_stat); P->d_tick = (uint32_t*)(m + o_tick); P->d_rem = m + o_rem; P->d_bsum = (uint32_t*)(m + o_bsum);
+  P->d_scanw = (unsigned long long*)(m + o_scanw);
+  P->scanw_stride = (uint32_t)((std::max(L.lw, L.lzz) + SCAN_B) / SCAN_B + 2);
   P->d_res = (PlkMsmResult*)(m + o_res); P->arena = m + o_arena;
   for (int i = 0; i < 13; i++) P->d_polys[i] = m + o_polys[i];
   P->d_cir = m + o_cir; P->d_vals = m + o_vals; P->d_outs = (uint8_t**)(m + o_outs);
@@ -1952,6 +2099,10 @@ int check_status(const plk_prover* P, const uint32_t* st, int strict, int circui
   if (st[ST_TXLEN] <= 2 * part) { plk_set_error("Invalid slice indices in poly_slice"); return PLK_ERR_RANGE; }
   for (int i = 4; i < 7; i++)
     if (st[ST_LEN0 + i] > P->srs_len) { plk_set_error("SRS length is less than polynomial length"); return PLK_ERR_RANGE; }
+  if ((st[ST_REM_W1] | st[ST_REM_W2]) & SCAN_TIMEOUT) {   // (lincomb_divide_kernel: a wait gave up)
+    plk_set_error("internal: round-5 division scan timed out waiting for a chunk aggregate");
+    return PLK_ERR_HIP;
+  }
   if (strict && st[ST_REM_W1]) { plk_set_error("assertion poly_is_zero(&rem1) failed"); return PLK_ERR_ARG; }
   if (strict && st[ST_REM_W2]) { plk_set_error("assertion poly_is_zero(&rem2) failed"); return PLK_ERR_ARG; }
   for (int i = 7; i < 9; i++)
