@@ -87,7 +87,9 @@ enum {
   PLK_OPT_NTT_LAUNCH_LOG = 20,   /* diagnostics: 1 records the NTT passes' launch plans (plk_ntt_launch_log) */
   PLK_OPT_PROVE_FUSE_DIV = 21,   /* 1: round 5's numerators and their divisions by x - z, x - z omega in one
                                     launch (single-pass suffix scan); 0: numerators, then the apply launch */
-  PLK_OPT_COUNT = 22
+  PLK_OPT_PROVE_SRS_LOGS = 22,   /* 1: the prover's commitments read its SRS in log form (1 B per point,
+                                    converted once at plk_prover_create); 0: the G1 form (3 B) */
+  PLK_OPT_COUNT = 23
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
 /* Diagnostics for the offline roofline tools: with PLK_OPT_NTT_LAUNCH_LOG = 1 every NTT pass launch

@@ -467,6 +467,7 @@ const OptDef kOpt[PLK_OPT_COUNT] = {
     {1, 0, 1, false},                          // NTT_TABLE_SHARE
     {0, 0, 1, false},                          // NTT_LAUNCH_LOG
     {0, 0, 1, false},                          // PROVE_FUSE_DIV (measured slower)
+    {1, 0, 1, false},                          // PROVE_SRS_LOGS
 };
 struct Opts {
   std::atomic<int64_t> v[PLK_OPT_COUNT];

@@ -29,6 +29,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 // Diagnostic builds only (tools/msm_lab.hip): bit 0 replaces the LDS table by arithmetic,
 // bit 1 replaces the ticketed atomics by a plain store.  Always 0 in libplonkhip.
 #ifndef PLK_MSM_DIAG
@@ -199,6 +201,58 @@ __device__ __forceinline__ uint32_t half_sum(const Half& h, const uint32_t* tab,
   return __builtin_amdgcn_udot4(hi, h.s.y, __builtin_amdgcn_udot4(lo, h.s.x, 0u, false), false);   // <= 8*101*255
 }
 
+// Finish of one block of an MSM launch (msm_dlog_kernel / msm_log_kernel): the block's log sum
+// and irregular flag go to record res with the ticketed atomics described below.
+template <int NT>
+__device__ __forceinline__ void msm_finish(uint32_t acc, bool bad, PlkMsmResult* res, uint32_t* wsum, uint32_t* wbad,
+                                           const uint32_t* etab) {
+  const uint32_t wave = threadIdx.x / PLK_WAVE;
+  const uint32_t s = plk_wave_sum(acc);
+  const uint64_t anybad = __ballot(bad);
+  if ((threadIdx.x & (PLK_WAVE - 1)) == 0) {
+    wsum[wave] = s;
+    wbad[wave] = anybad != 0;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  uint32_t bs = 0, bb_ = 0;
+#pragma unroll
+  for (int k = 0; k < NT / PLK_WAVE; k++) {
+    bs += wsum[k];
+    bb_ |= wbad[k];
+  }
+  if (PLK_MSM_DIAG & 2) {
+    res->pad[blockIdx.x % 11] = bs + bb_;
+    return;
+  }
+  const uint32_t X = gridDim.x;
+  unsigned long long add =
+      (unsigned long long)(bs % PLK_GROUP_ORDER) | (1ull << 32) | ((unsigned long long)(bb_ != 0) << 48);
+  {
+    const uint32_t lin = blockIdx.y * X + blockIdx.x;
+    const uint32_t sh = lin % PLK_MSM_SHARDS;
+    // blocks of this MSM in shard sh: x in [0, X) with (y X + x) = sh (mod 8)
+    const uint32_t r = (sh + PLK_MSM_SHARDS - (blockIdx.y * X) % PLK_MSM_SHARDS) % PLK_MSM_SHARDS;
+    const uint32_t in_shard = r < X ? (X - r + PLK_MSM_SHARDS - 1) / PLK_MSM_SHARDS : 0u;
+    unsigned long long* word = reinterpret_cast<unsigned long long*>(&res->shard[sh][0]);
+    const unsigned long long old = atomicAdd(word, add);
+    if (((old >> 32) & 0xFFFFull) != in_shard - 1) return;
+    const unsigned long long tot = old + add;
+    atomicExch(word, 0ull);
+    add = (unsigned long long)((uint32_t)(tot & 0xFFFFFFFFull) % PLK_GROUP_ORDER) | (1ull << 32) |
+          ((unsigned long long)((tot >> 48) != 0) << 48);
+  }
+  const uint32_t arrivals = X < PLK_MSM_SHARDS ? X : PLK_MSM_SHARDS;   // shards with blocks
+  const unsigned long long old = atomicAdd(&res->top, add);
+  if (((old >> 32) & 0xFFFFull) != arrivals - 1) return;
+  const unsigned long long tot = old + add;
+  const uint32_t lg = (uint32_t)(tot & 0xFFFFFFFFull) % PLK_GROUP_ORDER;
+  res->log = lg;
+  res->irregular = (uint32_t)(tot >> 48);
+  *reinterpret_cast<uint32_t*>(res->g1) = etab[lg];
+  atomicExch(&res->top, 0ull);
+}
+
 }  // namespace
 
 // One launch = a batch of gridDim.y MSMs of n points each (points/scalars of MSM b at
@@ -334,52 +388,60 @@ __global__ __launch_bounds__(NT) void msm_dlog_kernel(const uint8_t* pts_base, u
     }
   }
   acc %= PLK_GROUP_ORDER;
+  msm_finish<NT>(acc, bad, res, wsum, wbad, etab);
+}
 
-  const uint32_t wave = threadIdx.x / PLK_WAVE;
-  const uint32_t s = plk_wave_sum(acc);
-  const uint64_t anybad = __ballot(bad);
-  if ((threadIdx.x & (PLK_WAVE - 1)) == 0) {
-    wsum[wave] = s;
-    wbad[wave] = anybad != 0;
-  }
+// ---------------------------------------------------------------------------------------
+// A FIXED SRS in log form.  The prover commits 9 polynomials against one SRS per proof
+// (src/plonk.h:299-301, 379, 522-524, 620-621): it converts the SRS once (srs_log_kernel: LOG(P_i)
+// as one byte, the same table lookup as above; any non-canonical encoding raises the flag and
+// the caller keeps the G1 form), after which each commitment reads 1 B of log + 1 B of scalar
+// per point instead of 3 + 1, and multiplies with v_dot4_u32_u8 (4 points per instruction).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void srs_log_kernel(const uint8_t* __restrict__ pts, uint64_t n,
+                                                      uint8_t* __restrict__ logs, uint32_t* __restrict__ irregular) {
+  __shared__ uint32_t tab[TAB_ENTRIES];
+  for (uint32_t i = threadIdx.x; i < TAB_ENTRIES; i += blockDim.x) tab[i] = c_ytab[i];
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  uint32_t bs = 0, bb_ = 0;
-#pragma unroll
-  for (int k = 0; k < NT / PLK_WAVE; k++) {
-    bs += wsum[k];
-    bb_ |= wbad[k];
+  bool bad = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t k = encode(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
+    const uint32_t d = tab[(k >> 16) & 0x1FFu] - k;
+    bad |= d >= 256u;
+    logs[i] = (uint8_t)d;
   }
-  if (PLK_MSM_DIAG & 2) {
-    res->pad[blockIdx.x % 11] = bs + bb_;
-    return;
+  if (__ballot(bad) && (threadIdx.x & (PLK_WAVE - 1)) == 0) atomicOr(irregular, 1u);
+}
+
+// MSM b of the launch (b = blockIdx.y): logs at logs + b lstride, scalars at sc + b sstride, n
+// points; 16-byte aligned bases (the caller checks).  Every thread takes 16-point groups with the
+// grid's stride; the finish is msm_dlog_kernel's (msm_finish).
+template <int NT>
+__global__ __launch_bounds__(NT) void msm_log_kernel(const uint8_t* logs_base, uint64_t lstride, const uint8_t* sc_base,
+                                                     uint64_t sstride, uint64_t n, PlkMsmResult* res_base) {
+  __shared__ uint32_t etab[PLK_GROUP_ORDER];
+  __shared__ uint32_t wsum[NT / PLK_WAVE];
+  __shared__ uint32_t wbad[NT / PLK_WAVE];
+  const uint8_t* lg = logs_base + (uint64_t)blockIdx.y * lstride;
+  const uint8_t* sc = sc_base + (uint64_t)blockIdx.y * sstride;
+  if (threadIdx.x < PLK_GROUP_ORDER) etab[threadIdx.x] = reinterpret_cast<const uint32_t*>(c_exp)[threadIdx.x];
+  const uint64_t stride = (uint64_t)gridDim.x * NT;
+  const uint64_t ngroups = n >> 4;
+  const uint4* l4 = reinterpret_cast<const uint4*>(lg);
+  const uint4* s4 = reinterpret_cast<const uint4*>(sc);
+  uint32_t acc = 0;
+  for (uint64_t g = (uint64_t)blockIdx.x * NT + threadIdx.x; g < ngroups; g += stride) {
+    const uint4 a = l4[g], b = s4[g];
+    uint32_t t = __builtin_amdgcn_udot4(a.x, b.x, 0u, false);   // 16 x 101 x 255 < 2^19
+    t = __builtin_amdgcn_udot4(a.y, b.y, t, false);
+    t = __builtin_amdgcn_udot4(a.z, b.z, t, false);
+    t = __builtin_amdgcn_udot4(a.w, b.w, t, false);
+    acc += t % PLK_GROUP_ORDER;
   }
-  const uint32_t X = gridDim.x;
-  unsigned long long add =
-      (unsigned long long)(bs % PLK_GROUP_ORDER) | (1ull << 32) | ((unsigned long long)(bb_ != 0) << 48);
-  {
-    const uint32_t lin = blockIdx.y * X + blockIdx.x;
-    const uint32_t sh = lin % PLK_MSM_SHARDS;
-    // blocks of this MSM in shard sh: x in [0, X) with (y X + x) = sh (mod 8)
-    const uint32_t r = (sh + PLK_MSM_SHARDS - (blockIdx.y * X) % PLK_MSM_SHARDS) % PLK_MSM_SHARDS;
-    const uint32_t in_shard = r < X ? (X - r + PLK_MSM_SHARDS - 1) / PLK_MSM_SHARDS : 0u;
-    unsigned long long* word = reinterpret_cast<unsigned long long*>(&res->shard[sh][0]);
-    const unsigned long long old = atomicAdd(word, add);
-    if (((old >> 32) & 0xFFFFull) != in_shard - 1) return;
-    const unsigned long long tot = old + add;
-    atomicExch(word, 0ull);
-    add = (unsigned long long)((uint32_t)(tot & 0xFFFFFFFFull) % PLK_GROUP_ORDER) | (1ull << 32) |
-          ((unsigned long long)((tot >> 48) != 0) << 48);
-  }
-  const uint32_t arrivals = X < PLK_MSM_SHARDS ? X : PLK_MSM_SHARDS;   // shards with blocks
-  const unsigned long long old = atomicAdd(&res->top, add);
-  if (((old >> 32) & 0xFFFFull) != arrivals - 1) return;
-  const unsigned long long tot = old + add;
-  const uint32_t lg = (uint32_t)(tot & 0xFFFFFFFFull) % PLK_GROUP_ORDER;
-  res->log = lg;
-  res->irregular = (uint32_t)(tot >> 48);
-  *reinterpret_cast<uint32_t*>(res->g1) = etab[lg];
-  atomicExch(&res->top, 0ull);
+  const uint64_t base = ngroups << 4;   // the n mod 16 tail: the first block
+  if (blockIdx.x == 0 && base + threadIdx.x < n) acc += (uint32_t)lg[base + threadIdx.x] * sc[base + threadIdx.x];
+  acc %= PLK_GROUP_ORDER;
+  msm_finish<NT>(acc, false, res_base + blockIdx.y, wsum, wbad, etab);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1052,6 +1114,39 @@ int plk_msm_finalize_launch(const uint32_t* d_logs, int batch, int stride, uint8
 
 int plk_msm_combine_launch(const uint32_t* d_logs, int count, uint8_t* d_out, hipStream_t st) {
   hipLaunchKernelGGL(msm_combine_kernel, dim3(1), dim3(64), 0, st, d_logs, count, d_out);
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
+int plk_srs_log_launch(const uint8_t* d_pts, uint64_t n, uint8_t* d_logs, uint32_t* d_irregular, hipStream_t st) {
+  if (!n) return PLK_OK;
+  const uint64_t b = std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(srs_log_kernel, dim3((unsigned)b), dim3(256), 0, st, d_pts, n, d_logs, d_irregular);
+  PLK_HIP(hipGetLastError());
+  return PLK_OK;
+}
+
+// batch MSMs over log-form points (plk_srs_log_launch); bases and strides 16-byte aligned.
+// Blocks per MSM: PLK_OPT_MSM_MAX_BLOCKS (default 2048: one resident round of 256-thread blocks)
+// shared by the batch, at most one 16-point group per thread.
+int plk_msm_log_batch_launch(const uint8_t* d_logs, uint64_t lstride, const uint8_t* d_sc, uint64_t sstride, uint64_t n,
+                             int batch, PlkMsmResult* d_res, hipStream_t st) {
+  if (batch <= 0) return PLK_OK;
+  if (batch > 65535) {
+    plk_set_error("plk_msm batch %d too large", batch);
+    return PLK_ERR_RANGE;
+  }
+  if ((uintptr_t)d_logs % 16 || (uintptr_t)d_sc % 16 || (batch > 1 && (lstride % 16 || sstride % 16))) {
+    plk_set_error("plk_msm_log_batch_launch: unaligned operands");
+    return PLK_ERR_ARG;
+  }
+  const uint64_t groups = n >> 4;
+  const int64_t env_blocks = plk_opt(PLK_OPT_MSM_MAX_BLOCKS);
+  uint64_t b = std::max<uint64_t>(1, (env_blocks > 0 ? (uint64_t)env_blocks : 2048) / (uint64_t)batch);
+  b = std::min<uint64_t>(b, std::max<uint64_t>(1, (groups + 255) / 256));
+  b = std::min<uint64_t>(b, 8ull * 65535ull);   // the finish's per-shard ticket field is 16 bits
+  hipLaunchKernelGGL(msm_log_kernel<256>, dim3((unsigned)b, batch), dim3(256), 0, st, d_logs, lstride, d_sc, sstride, n,
+                     d_res);
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }

@@ -52,6 +52,11 @@ void plk_msm_geometry(uint64_t n, int batch, int* threads, int* blocks, int* gro
 int plk_msm_batch_launch(const uint8_t* d_pts, uint64_t pstride, const uint8_t* d_sc, uint64_t sstride, uint64_t n,
                          int batch, PlkMsmResult* d_res, hipStream_t st);
 int plk_msm_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsmResult* d_res, hipStream_t st);
+// a fixed SRS in log form (1 byte per point; *d_irregular |= 1 if any encoding is not canonical,
+// and the logs are then unusable) and batch MSMs over it
+int plk_srs_log_launch(const uint8_t* d_pts, uint64_t n, uint8_t* d_logs, uint32_t* d_irregular, hipStream_t st);
+int plk_msm_log_batch_launch(const uint8_t* d_logs, uint64_t lstride, const uint8_t* d_sc, uint64_t sstride, uint64_t n,
+                             int batch, PlkMsmResult* d_res, hipStream_t st);
 int plk_msm_serial_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsmResult* d_res,
                           hipStream_t st);
 int plk_msm_finalize_launch(const uint32_t* d_logs, int batch, int stride, uint8_t* d_out, hipStream_t st);

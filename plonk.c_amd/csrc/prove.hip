@@ -1141,13 +1141,16 @@ __global__ void scalars_init_kernel(SlotFile f, uint8_t* __restrict__ S, uint32_
 // the MSM (which runs over the committed length and does not need them): wave w < ntrim finds
 // buffer w's last non-zero byte from the top, 1 KB per step (16 bytes per lane, the highest
 // non-zero lane by ballot); the remaining waves OR the remainder-vote bytes (TRIM_ANY).
+#ifndef PLK_DIAG_PACK_ONLY
+#define PLK_DIAG_PACK_ONLY 0   // timing builds only: 1 skips the trimmed-length scans (wrong status words)
+#endif
 constexpr int PACK_T = 1024;
 static_assert(NSTAT <= 64 && 34 <= 64, "trim_pack_kernel: wave 0 writes the status words, the last wave the proof");
 __global__ __launch_bounds__(PACK_T) void trim_pack_kernel(TrimArgs a, int nt, const PlkMsmResult* __restrict__ res,
                                                            const uint8_t* __restrict__ S, uint32_t* __restrict__ stat,
                                                            uint8_t* __restrict__ host, uint32_t seq) {
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
-  const int ntrim = nt > 0 && (a.dst[nt - 1] & TRIM_ANY) ? nt - 1 : nt;   // the vote buffer comes last
+  const int ntrim = PLK_DIAG_PACK_ONLY ? 0 : nt > 0 && (a.dst[nt - 1] & TRIM_ANY) ? nt - 1 : nt;   // the vote buffer comes last
   // the proof bytes do not depend on the trimmed lengths: the last waves load and send them to
   // the host first, so their round trips overlap the scans below
   if (wv == PACK_T / 64 - 1) {
@@ -1329,6 +1332,8 @@ struct plk_prover {
   uint32_t scanw_stride = 0;       // words per division
   uint32_t scan_epoch = 0;         // launches of lincomb_divide_kernel so far (0: none)
   PlkMsmResult* d_res = nullptr;   // 9 MSM records
+  uint8_t* d_srs_log = nullptr;    // the SRS in log form (srs_log_kernel), valid when !srs_irregular
+  uint32_t* d_srs_flag = nullptr;  // srs_log_kernel's irregular flag
   uint8_t* arena = nullptr;        // [9][cstride] committed polynomials
   size_t cstride = 0, cmax = 0;
   uint8_t* d_polys[13] = {};       // stage-A outputs (circuit path)
@@ -1677,6 +1682,7 @@ int create_on(const plk_plonk_desc_t* d, int dev, plk_prover_t** out) {
                o_bsum = B.take(4 * ((L.lw + SCAN_B - 1) / SCAN_B + 2) + 4 * ((L.lzz + SCAN_B) / SCAN_B + 2)),
                o_scanw = B.take(8 * 2 * ((std::max(L.lw, L.lzz) + SCAN_B) / SCAN_B + 2)),
                o_res = B.take(9 * sizeof(PlkMsmResult)),
+               o_srslog = B.take(P->srs_len + 16 + 16),
                o_arena = B.take(9 * P->cstride);
   size_t o_polys[13];
   for (int i = 0; i < 13; i++) o_polys[i] = B.take(n + 16);
@@ -1711,6 +1717,8 @@ int create_on(const plk_plonk_desc_t* d, int dev, plk_prover_t** out) {
   P->d_scanw = (unsigned long long*)(m + o_scanw);
   P->scanw_stride = (uint32_t)((std::max(L.lw, L.lzz) + SCAN_B) / SCAN_B + 2);
   P->d_res = (PlkMsmResult*)(m + o_res); P->arena = m + o_arena;
+  P->d_srs_log = m + o_srslog;
+  P->d_srs_flag = (uint32_t*)(m + o_srslog + ((P->srs_len + 16 + 15) & ~(size_t)15));
   for (int i = 0; i < 13; i++) P->d_polys[i] = m + o_polys[i];
   P->d_cir = m + o_cir; P->d_vals = m + o_vals; P->d_outs = (uint8_t**)(m + o_outs);
   for (size_t i = 0; i < sizeof(iv) / sizeof(iv[0]); i++) *iv[i].p = m + o_iv[i];
@@ -1736,21 +1744,15 @@ int create_on(const plk_plonk_desc_t* d, int dev, plk_prover_t** out) {
     plk_prover_destroy(P);
     return PLK_ERR_HIP;
   }
-  {  // SRS encodings: one probe MSM decides whether every point is canonical (fast path)
-    uint8_t* d_ones = nullptr;
-    if (hipMalloc((void**)&d_ones, P->srs_len + 16) != hipSuccess) { plk_prover_destroy(P); plk_set_error("hipMalloc"); return PLK_ERR_NOMEM; }
-    (void)hipMemsetAsync(d_ones, 1, P->srs_len, P->st);
-    (void)hipMemsetAsync(P->d_res, 0, sizeof(PlkMsmResult), P->st);
-    rc = plk_msm_launch(P->d_srs, d_ones, P->srs_len, P->d_res, P->st);
-    PlkMsmResult h{};
-    if (!rc && hipMemcpyAsync(&h, P->d_res, sizeof h, hipMemcpyDeviceToHost, P->st) == hipSuccess &&
-        hipStreamSynchronize(P->st) == hipSuccess) {
-      P->srs_irregular = h.irregular != 0;
-    } else if (!rc) {
+  {  // the SRS in log form, once (the commitments' MSMs read 1 B per point); any non-canonical
+     // encoding keeps the G1 form and the exact serial folds
+    uint32_t flag = 0;
+    rc = plk_srs_log_launch(P->d_srs, P->srs_len, P->d_srs_log, P->d_srs_flag, P->st);
+    if (!rc && (hipMemcpyAsync(&flag, P->d_srs_flag, 4, hipMemcpyDeviceToHost, P->st) != hipSuccess ||
+                hipStreamSynchronize(P->st) != hipSuccess))
       rc = PLK_ERR_HIP;
-    }
-    (void)hipFree(d_ones);
     if (rc) { plk_prover_destroy(P); return rc; }
+    P->srs_irregular = flag != 0;
   }
   *out = P;
   return PLK_OK;
@@ -2073,7 +2075,9 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   // ---- the 9 commitments: one batched MSM over the arena (srs_eval_at_s, src/srs.h:53-68)
   const uint64_t nm = std::min<uint64_t>(P->cmax, P->srs_len);
   // (the 9 result records are zeroed at plk_prover_create and every launch leaves them re-armed)
-  if (!P->srs_irregular) {
+  if (!P->srs_irregular && plk_opt(PLK_OPT_PROVE_SRS_LOGS)) {
+    RC(plk_msm_log_batch_launch(P->d_srs_log, 0, P->arena, P->cstride, nm, 9, P->d_res, P->st));
+  } else if (!P->srs_irregular) {
     RC(plk_msm_batch_launch(P->d_srs, 0, P->arena, P->cstride, nm, 9, P->d_res, P->st));
   } else {
     for (int i = 0; i < 9; i++) RC(plk_msm_serial_launch(P->d_srs, P->arena + i * P->cstride, nm, P->d_res + i, P->st));

@@ -86,6 +86,20 @@ def test_round5_divisions_vs_oracle(hip, oracle, n, seed, z):
                 assert pr.rounds_dev(dev, chal, rnd, strict=False).hex() == want.hex(), fuse
 
 
+@pytest.mark.parametrize("n,seed", [(37, 71), (4096, 72), (20000, 73)])
+def test_commitments_srs_log_form(hip, oracle, n, seed):
+    """The 9 commitments from the SRS in log form (PROVE_SRS_LOGS = 1: srs_log_kernel once at
+    create, msm_log_kernel per proof; committed lengths n + 2 .. n + 3, so 16-point groups plus
+    a ragged tail) and from the G1 form give the oracle's proof."""
+    polys, chal, rnd, zh, pts = _synthetic(n, seed, 2 * n + 8)
+    want = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes()).rounds(polys, chal, rnd, strict=False)
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    for logs in (1, 0, 1):
+        with hip.options(PROVE_SRS_LOGS=logs):
+            assert pr.rounds_dev(dev, chal, rnd, strict=False).hex() == want.hex(), logs
+
+
 @pytest.mark.parametrize("n,seed", [(8, 1), (37, 2), (256, 3), (1000, 4), (3000, 5), (2100, 6), (5000, 7)])
 def test_rounds_shape_vs_oracle(hip, oracle, n, seed):
     """(n = 2100 and 5000: t_2 (4n + 6 coefficients) and (a b) q_m (3n + 2) need different
