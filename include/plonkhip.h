@@ -89,7 +89,9 @@ enum {
                                     launch (single-pass suffix scan); 0: numerators, then the apply launch */
   PLK_OPT_PROVE_SRS_LOGS = 22,   /* 1: the prover's commitments read its SRS in log form (1 B per point,
                                     converted once at plk_prover_create); 0: the G1 form (3 B) */
-  PLK_OPT_COUNT = 23
+  PLK_OPT_PROVE_PACK_FUSE = 23,  /* 1 (with PROVE_SRS_LOGS): commitments, trimmed lengths and the proof packing
+                                    in one launch (commit_pack_kernel); 0: the MSM, then trim_pack_kernel */
+  PLK_OPT_COUNT = 24
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
 /* Diagnostics for the offline roofline tools: with PLK_OPT_NTT_LAUNCH_LOG = 1 every NTT pass launch

@@ -26,6 +26,7 @@
 // the exact serial fold on the device (msm_serial_fold_kernel) -- bit-exact either way.
 #include "plk_device.h"
 #include "plk_internal.h"
+#include "plk_msm_finish.h"
 
 #include <stdlib.h>
 
@@ -41,6 +42,7 @@ __constant__ uint32_t c_ytab[512];             // E[idx], see above
 __constant__ __attribute__((aligned(16))) uint8_t c_exp[PLK_GROUP_ORDER * 4];  // EXP[k] = {x, y, inf, 0}
 __constant__ uint8_t c_inv101[PLK_GF_P];       // a^-1 mod 101 (0 -> 0), for the raw fold
 __constant__ uint32_t c_inv101w[PLK_GF_P];     // the same as words (scalar loads in the uniform fold)
+__device__ uint32_t g_exp_words[PLK_GROUP_ORDER];   // c_exp as words in global memory (plk_msm_exp_words_dev)
 
 namespace {
 
@@ -199,58 +201,6 @@ __device__ __forceinline__ uint32_t half_sum(const Half& h, const uint32_t* tab,
   const uint32_t hi = __builtin_amdgcn_perm(__builtin_amdgcn_perm(d7, d6, 0x0C0C0400u),
                                             __builtin_amdgcn_perm(d5, d4, 0x0C0C0400u), 0x05040100u);
   return __builtin_amdgcn_udot4(hi, h.s.y, __builtin_amdgcn_udot4(lo, h.s.x, 0u, false), false);   // <= 8*101*255
-}
-
-// Finish of one block of an MSM launch (msm_dlog_kernel / msm_log_kernel): the block's log sum
-// and irregular flag go to record res with the ticketed atomics described below.
-template <int NT>
-__device__ __forceinline__ void msm_finish(uint32_t acc, bool bad, PlkMsmResult* res, uint32_t* wsum, uint32_t* wbad,
-                                           const uint32_t* etab) {
-  const uint32_t wave = threadIdx.x / PLK_WAVE;
-  const uint32_t s = plk_wave_sum(acc);
-  const uint64_t anybad = __ballot(bad);
-  if ((threadIdx.x & (PLK_WAVE - 1)) == 0) {
-    wsum[wave] = s;
-    wbad[wave] = anybad != 0;
-  }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  uint32_t bs = 0, bb_ = 0;
-#pragma unroll
-  for (int k = 0; k < NT / PLK_WAVE; k++) {
-    bs += wsum[k];
-    bb_ |= wbad[k];
-  }
-  if (PLK_MSM_DIAG & 2) {
-    res->pad[blockIdx.x % 11] = bs + bb_;
-    return;
-  }
-  const uint32_t X = gridDim.x;
-  unsigned long long add =
-      (unsigned long long)(bs % PLK_GROUP_ORDER) | (1ull << 32) | ((unsigned long long)(bb_ != 0) << 48);
-  {
-    const uint32_t lin = blockIdx.y * X + blockIdx.x;
-    const uint32_t sh = lin % PLK_MSM_SHARDS;
-    // blocks of this MSM in shard sh: x in [0, X) with (y X + x) = sh (mod 8)
-    const uint32_t r = (sh + PLK_MSM_SHARDS - (blockIdx.y * X) % PLK_MSM_SHARDS) % PLK_MSM_SHARDS;
-    const uint32_t in_shard = r < X ? (X - r + PLK_MSM_SHARDS - 1) / PLK_MSM_SHARDS : 0u;
-    unsigned long long* word = reinterpret_cast<unsigned long long*>(&res->shard[sh][0]);
-    const unsigned long long old = atomicAdd(word, add);
-    if (((old >> 32) & 0xFFFFull) != in_shard - 1) return;
-    const unsigned long long tot = old + add;
-    atomicExch(word, 0ull);
-    add = (unsigned long long)((uint32_t)(tot & 0xFFFFFFFFull) % PLK_GROUP_ORDER) | (1ull << 32) |
-          ((unsigned long long)((tot >> 48) != 0) << 48);
-  }
-  const uint32_t arrivals = X < PLK_MSM_SHARDS ? X : PLK_MSM_SHARDS;   // shards with blocks
-  const unsigned long long old = atomicAdd(&res->top, add);
-  if (((old >> 32) & 0xFFFFull) != arrivals - 1) return;
-  const unsigned long long tot = old + add;
-  const uint32_t lg = (uint32_t)(tot & 0xFFFFFFFFull) % PLK_GROUP_ORDER;
-  res->log = lg;
-  res->irregular = (uint32_t)(tot >> 48);
-  *reinterpret_cast<uint32_t*>(res->g1) = etab[lg];
-  atomicExch(&res->top, 0ull);
 }
 
 }  // namespace
@@ -955,7 +905,13 @@ int plk_msm_upload_tables(const uint32_t* ytab, const uint8_t* exp4, const uint8
   uint32_t w[PLK_GF_P];
   for (int i = 0; i < PLK_GF_P; i++) w[i] = inv101[i];
   PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_inv101w), w, sizeof w));
+  PLK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_exp_words), exp4, PLK_GROUP_ORDER * 4));
   return PLK_OK;
+}
+
+const uint32_t* plk_msm_exp_words_dev() {   // (the current device's copy)
+  void* p = nullptr;
+  return hipGetSymbolAddress(&p, HIP_SYMBOL(g_exp_words)) == hipSuccess ? (const uint32_t*)p : nullptr;
 }
 
 // Launch geometry.  Big MSMs use 512-thread blocks (two 64 KB tables per CU, 16 waves);

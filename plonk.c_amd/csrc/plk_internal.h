@@ -54,6 +54,8 @@ int plk_msm_batch_launch(const uint8_t* d_pts, uint64_t pstride, const uint8_t* 
 int plk_msm_launch(const uint8_t* d_pts, const uint8_t* d_sc, uint64_t n, PlkMsmResult* d_res, hipStream_t st);
 // a fixed SRS in log form (1 byte per point; *d_irregular |= 1 if any encoding is not canonical,
 // and the logs are then unusable) and batch MSMs over it
+// EXP words {x, y, inf, 0} of the group (uploaded with the MSM tables) on the current device
+const uint32_t* plk_msm_exp_words_dev();
 int plk_srs_log_launch(const uint8_t* d_pts, uint64_t n, uint8_t* d_logs, uint32_t* d_irregular, hipStream_t st);
 int plk_msm_log_batch_launch(const uint8_t* d_logs, uint64_t lstride, const uint8_t* d_sc, uint64_t sstride, uint64_t n,
                              int batch, PlkMsmResult* d_res, hipStream_t st);

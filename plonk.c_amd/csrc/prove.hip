@@ -30,6 +30,7 @@
 
 #include "plk_device.h"
 #include "plk_internal.h"
+#include "plk_msm_finish.h"
 
 // Diagnostic builds only (plonk.c_amd/Makefile `diag`): 1 drops plk_prover_chains_dev's ordering of
 // `done` behind the chains, 2 drops plk_prover_rounds_ext_dev's wait for `ready` -- the hand-off
@@ -1206,6 +1207,85 @@ __global__ __launch_bounds__(PACK_T) void trim_pack_kernel(TrimArgs a, int nt, c
   if (t == 0) __hip_atomic_store((uint32_t*)(host + 60), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The 9 commitments, the trimmed lengths and the packing in ONE launch (the prover's SRS in log
+// form, PLK_OPT_PROVE_PACK_FUSE): rows y < 9 of the grid are msm_log_kernel's MSMs over the
+// arena; row 9 scans the trimmed-length buffers (block x < nt: buffer x, 4 KB per step from the
+// top; the vote buffer's block ORs its bytes) while the MSM rows stream.  Every finished record
+// and every trim block then arrives on `done`; the last arrival (one thread) packs the proof and
+// the status words into the mapped host buffer and writes the completion word, as
+// trim_pack_kernel does -- its launch and its scan latency leave the proof's tail.
+constexpr int CP_T = 256;
+__global__ __launch_bounds__(CP_T) void commit_pack_kernel(const uint8_t* __restrict__ logs, const uint8_t* arena,
+                                                           uint64_t cstride, uint64_t n, PlkMsmResult* res,
+                                                           const uint32_t* __restrict__ exp_words, TrimArgs a, int nt,
+                                                           const uint8_t* __restrict__ S, uint32_t* stat,
+                                                           uint8_t* __restrict__ host, uint32_t seq, uint32_t* done) {
+  __shared__ uint32_t etab[PLK_GROUP_ORDER];
+  __shared__ uint32_t wsum[CP_T / PLK_WAVE];
+  __shared__ uint32_t wbad[CP_T / PLK_WAVE];
+  bool arrive = false;
+  if (blockIdx.y < 9) {
+    const uint8_t* sc = arena + (uint64_t)blockIdx.y * cstride;
+    if (threadIdx.x < PLK_GROUP_ORDER) etab[threadIdx.x] = exp_words[threadIdx.x];
+    const uint64_t stride = (uint64_t)gridDim.x * CP_T;
+    const uint64_t ngroups = n >> 4;
+    const uint4* l4 = reinterpret_cast<const uint4*>(logs);
+    const uint4* s4 = reinterpret_cast<const uint4*>(sc);
+    uint32_t acc = 0;
+    for (uint64_t g = (uint64_t)blockIdx.x * CP_T + threadIdx.x; g < ngroups; g += stride) {
+      const uint4 l = l4[g], s = s4[g];
+      uint32_t t = __builtin_amdgcn_udot4(l.x, s.x, 0u, false);   // 16 x 101 x 255 < 2^19
+      t = __builtin_amdgcn_udot4(l.y, s.y, t, false);
+      t = __builtin_amdgcn_udot4(l.z, s.z, t, false);
+      t = __builtin_amdgcn_udot4(l.w, s.w, t, false);
+      acc += t % PLK_GROUP_ORDER;
+    }
+    const uint64_t base = ngroups << 4;
+    if (blockIdx.x == 0 && base + threadIdx.x < n) acc += (uint32_t)logs[base + threadIdx.x] * sc[base + threadIdx.x];
+    arrive = msm_finish<CP_T>(acc % PLK_GROUP_ORDER, false, res + blockIdx.y, wsum, wbad, etab);
+  } else {
+    const int x = (int)blockIdx.x;
+    if (x >= nt) return;   // (uniform)
+    const uint8_t* p = a.p[x];
+    const uint64_t len = a.len[x];
+    const int d = a.dst[x];
+    if (d & TRIM_ANY) {   // the remainder votes: any non-zero byte
+      uint32_t any = 0;
+      for (uint64_t i = threadIdx.x; i < len; i += CP_T) any |= p[i];
+      any = __syncthreads_or(any != 0);
+      if (threadIdx.x == 0 && any) stat[d & ~TRIM_ANY] = 1u;
+    } else {               // index + 1 of the last non-zero byte, at least 1 (src/poly.h:20-24)
+      uint32_t found = 0;
+      for (uint64_t hi = len; hi > 0;) {
+        const uint64_t lo = hi > 16 * CP_T ? hi - 16 * CP_T : 0;
+#pragma unroll
+        for (int k = 15; k >= 0; k--) {   // thread t: bytes hi - 16 (t + 1) .. hi - 16 t - 1
+          const int64_t i = (int64_t)hi - 16 * ((int64_t)threadIdx.x + 1) + k;
+          const bool nz = i >= (int64_t)lo && p[i < (int64_t)lo ? lo : i] != 0;
+          found = (!found && nz) ? (uint32_t)(i + 1) : found;
+        }
+        found = plk_block_max(found);
+        if (found) break;   // (uniform: the block's maximum)
+        hi = lo;
+      }
+      if (threadIdx.x == 0) stat[d] = found ? found : 1u;
+    }
+    arrive = threadIdx.x == 0;
+  }
+  if (!arrive) return;
+  // this record's point / this trim's word is written: release it, then arrive
+  __threadfence();
+  if (atomicAdd(done, 1u) != 9u + (uint32_t)nt - 1u) return;
+  __threadfence();   // (acquire: every other arrival's writes are visible)
+  *done = 0;         // re-armed for the next proof
+  const int ev[7] = {S_AZ, S_BZ, S_CZ, S_S1Z, S_S2Z, S_RZ, S_ZWZ};
+  for (int i = 0; i < 27; i++) host[i] = res[i / 3].g1[i % 3];
+  for (int i = 0; i < 7; i++) host[27 + i] = S[ev[i]];
+  for (int i = 0; i < NSTAT; i++) ((uint32_t*)(host + 64))[i] = __hip_atomic_load(stat + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __threadfence_system();
+  __hip_atomic_store((uint32_t*)(host + 60), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ------------------------------------------------------------------ stage A (circuit)
 // constraints_satisfy (src/constraints.h:145-171) and copy_constraints_to_roots
 // (src/plonk.h:141-160): one thread per gate.
@@ -1333,7 +1413,9 @@ struct plk_prover {
   uint32_t scan_epoch = 0;         // launches of lincomb_divide_kernel so far (0: none)
   PlkMsmResult* d_res = nullptr;   // 9 MSM records
   uint8_t* d_srs_log = nullptr;    // the SRS in log form (srs_log_kernel), valid when !srs_irregular
+  const uint32_t* exp_words = nullptr;   // the group's EXP words on this prover's device
   uint32_t* d_srs_flag = nullptr;  // srs_log_kernel's irregular flag
+  uint32_t* d_done = nullptr;      // commit_pack_kernel's arrival word (re-armed by its last arrival)
   uint8_t* arena = nullptr;        // [9][cstride] committed polynomials
   size_t cstride = 0, cmax = 0;
   uint8_t* d_polys[13] = {};       // stage-A outputs (circuit path)
@@ -1682,7 +1764,7 @@ int create_on(const plk_plonk_desc_t* d, int dev, plk_prover_t** out) {
                o_bsum = B.take(4 * ((L.lw + SCAN_B - 1) / SCAN_B + 2) + 4 * ((L.lzz + SCAN_B) / SCAN_B + 2)),
                o_scanw = B.take(8 * 2 * ((std::max(L.lw, L.lzz) + SCAN_B) / SCAN_B + 2)),
                o_res = B.take(9 * sizeof(PlkMsmResult)),
-               o_srslog = B.take(P->srs_len + 16 + 16),
+               o_srslog = B.take(P->srs_len + 16), o_words = B.take(64),
                o_arena = B.take(9 * P->cstride);
   size_t o_polys[13];
   for (int i = 0; i < 13; i++) o_polys[i] = B.take(n + 16);
@@ -1718,7 +1800,8 @@ int create_on(const plk_plonk_desc_t* d, int dev, plk_prover_t** out) {
   P->scanw_stride = (uint32_t)((std::max(L.lw, L.lzz) + SCAN_B) / SCAN_B + 2);
   P->d_res = (PlkMsmResult*)(m + o_res); P->arena = m + o_arena;
   P->d_srs_log = m + o_srslog;
-  P->d_srs_flag = (uint32_t*)(m + o_srslog + ((P->srs_len + 16 + 15) & ~(size_t)15));
+  P->d_srs_flag = (uint32_t*)(m + o_words);
+  P->d_done = (uint32_t*)(m + o_words + 4);
   for (int i = 0; i < 13; i++) P->d_polys[i] = m + o_polys[i];
   P->d_cir = m + o_cir; P->d_vals = m + o_vals; P->d_outs = (uint8_t**)(m + o_outs);
   for (size_t i = 0; i < sizeof(iv) / sizeof(iv[0]); i++) *iv[i].p = m + o_iv[i];
@@ -1747,7 +1830,8 @@ int create_on(const plk_plonk_desc_t* d, int dev, plk_prover_t** out) {
   {  // the SRS in log form, once (the commitments' MSMs read 1 B per point); any non-canonical
      // encoding keeps the G1 form and the exact serial folds
     uint32_t flag = 0;
-    rc = plk_srs_log_launch(P->d_srs, P->srs_len, P->d_srs_log, P->d_srs_flag, P->st);
+    P->exp_words = plk_msm_exp_words_dev();
+    rc = P->exp_words ? plk_srs_log_launch(P->d_srs, P->srs_len, P->d_srs_log, P->d_srs_flag, P->st) : PLK_ERR_HIP;
     if (!rc && (hipMemcpyAsync(&flag, P->d_srs_flag, 4, hipMemcpyDeviceToHost, P->st) != hipSuccess ||
                 hipStreamSynchronize(P->st) != hipSuccess))
       rc = PLK_ERR_HIP;
@@ -2075,6 +2159,16 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   // ---- the 9 commitments: one batched MSM over the arena (srs_eval_at_s, src/srs.h:53-68)
   const uint64_t nm = std::min<uint64_t>(P->cmax, P->srs_len);
   // (the 9 result records are zeroed at plk_prover_create and every launch leaves them re-armed)
+  if (!P->srs_irregular && plk_opt(PLK_OPT_PROVE_SRS_LOGS) && plk_opt(PLK_OPT_PROVE_PACK_FUSE)) {
+    // commitments + trimmed lengths + packing in one launch (commit_pack_kernel)
+    const uint64_t bx = std::max<uint64_t>(std::min<uint64_t>(2048 / 9, std::max<uint64_t>(1, ((nm >> 4) + CP_T - 1) / CP_T)),
+                                           (uint64_t)ntrims);
+    hipLaunchKernelGGL(commit_pack_kernel, dim3((unsigned)bx, 10), dim3(CP_T), 0, P->st, P->d_srs_log, P->arena,
+                       (uint64_t)P->cstride, nm, P->d_res, P->exp_words, trims, ntrims, P->d_S, P->d_stat,
+                       P->d_res_host, ++P->seq, P->d_done);
+    PLK_HIP(hipGetLastError());
+    return PLK_OK;
+  }
   if (!P->srs_irregular && plk_opt(PLK_OPT_PROVE_SRS_LOGS)) {
     RC(plk_msm_log_batch_launch(P->d_srs_log, 0, P->arena, P->cstride, nm, 9, P->d_res, P->st));
   } else if (!P->srs_irregular) {

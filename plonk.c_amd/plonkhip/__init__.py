@@ -89,7 +89,8 @@ OPTIONS = {"TINY_CALLS": 1, "PROVE_SYNC": 2, "POLY_BLOCK_L": 3, "POLY_BLOCK_S": 
            "MSM_MAX_BLOCKS": 11, "MSM_GROUPS": 12, "MSM_COPIES": 13, "MSM_HALF": 14, "MSM_SHARD_MIN": 15,
            "NTT_CENTER_SUM": 16, "MSM_HOST_LANES": 17,
            "PROVE_DERIVE_T2A": 18, "NTT_TABLE_SHARE": 19, "NTT_LAUNCH_LOG": 20,
-           "PROVE_FUSE_DIV": 21, "PROVE_SRS_LOGS": 22}
+           "PROVE_FUSE_DIV": 21, "PROVE_SRS_LOGS": 22,
+           "PROVE_PACK_FUSE": 23}
 
 PLK_PROVE_STRICT = 1
 PLK_PROVE_PREPROCESSED = 2

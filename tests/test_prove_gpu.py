@@ -89,15 +89,19 @@ def test_round5_divisions_vs_oracle(hip, oracle, n, seed, z):
 @pytest.mark.parametrize("n,seed", [(37, 71), (4096, 72), (20000, 73)])
 def test_commitments_srs_log_form(hip, oracle, n, seed):
     """The 9 commitments from the SRS in log form (PROVE_SRS_LOGS = 1: srs_log_kernel once at
-    create, msm_log_kernel per proof; committed lengths n + 2 .. n + 3, so 16-point groups plus
-    a ragged tail) and from the G1 form give the oracle's proof."""
+    create; per proof commit_pack_kernel -- commitments, trimmed lengths and packing in one
+    launch -- or msm_log_kernel + trim_pack_kernel; committed lengths n + 2 .. n + 3, so 16-point
+    groups plus a ragged tail) and from the G1 form give the oracle's proof, and the strict
+    rejection (its status words) is the same in every form."""
     polys, chal, rnd, zh, pts = _synthetic(n, seed, 2 * n + 8)
     want = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes()).rounds(polys, chal, rnd, strict=False)
     pr = hip.Prover(n, zh, pts)
     dev = [torch.from_numpy(p).to("cuda") for p in polys]
-    for logs in (1, 0, 1):
-        with hip.options(PROVE_SRS_LOGS=logs):
-            assert pr.rounds_dev(dev, chal, rnd, strict=False).hex() == want.hex(), logs
+    for logs, fuse in ((1, 1), (1, 0), (0, 1), (1, 1)):
+        with hip.options(PROVE_SRS_LOGS=logs, PROVE_PACK_FUSE=fuse):
+            assert pr.rounds_dev(dev, chal, rnd, strict=False).hex() == want.hex(), (logs, fuse)
+            with pytest.raises(hip.PlonkHipError, match="remainder"):
+                pr.rounds_dev(dev, chal, rnd, strict=True)
 
 
 @pytest.mark.parametrize("n,seed", [(8, 1), (37, 2), (256, 3), (1000, 4), (3000, 5), (2100, 6), (5000, 7)])

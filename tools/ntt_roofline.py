@@ -6,7 +6,7 @@ full occupancy -- the integer-VALU roof of this arithmetic on this chip).
     python tools/ntt_roofline.py <run_results.db> <bfly_peak.json> [--prove [--plan plan.json] | --all] [--json out]
 
 --prove: the kernels of the LAST prove call of the trace (tools/prove_bench.py; calls end with
-trim_pack_kernel); --all (default): every wt_* dispatch, aggregated per (kernel, grid).
+trim_pack_kernel or commit_pack_kernel); --all (default): every wt_* dispatch, aggregated per (kernel, grid).
 
 Butterflies counted (the algorithmic work, radix-2 count):
   wt_fwd/wt_inv_kernel<TB, R, M, ...>: blocks x 2^(TB-1) x M  (blocks = grid_x / workgroup x grid_y;
@@ -59,7 +59,7 @@ def main():
     rows = list(sqlite3.connect(db).execute(
         "select name, grid_x, grid_y, workgroup_x, duration, start from kernels order by start"))
     if "--prove" in sys.argv:
-        idx = [i for i, r in enumerate(rows) if "trim_pack" in r[0]]
+        idx = [i for i, r in enumerate(rows) if "trim_pack" in r[0] or "commit_pack" in r[0]]
         rows = rows[idx[-2] + 1:idx[-1] + 1]
     # (--all --plan: the plan of the whole traced run, every pass launch in order)
     plan = None

@@ -7,7 +7,7 @@ import sys
 
 rows = list(sqlite3.connect(sys.argv[1]).execute(
     "select name, duration, start, end, grid_x, grid_y, workgroup_x from kernels order by start"))
-idx = [i for i, r in enumerate(rows) if "trim_pack" in r[0]]
+idx = [i for i, r in enumerate(rows) if "trim_pack" in r[0] or "commit_pack" in r[0]]
 seg = rows[idx[-2] + 1:idx[-1] + 1]
 t0, prev = seg[0][2], seg[0][2]
 for name, dur, s, e, gx, gy, wx in seg:
