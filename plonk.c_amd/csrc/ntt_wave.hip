@@ -1193,7 +1193,9 @@ uint32_t center_blocks() {
   if (!nb) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    nb = (PLK_NTT_CW13 >= 8 ? 2u : 1u) * (uint32_t)(cus > 0 ? cus : 256);   // the resident blocks
+    // the resident blocks: the launch bound's waves per SIMD x 4 SIMDs over the block's waves
+    const uint32_t per_cu = std::max<uint32_t>(1u, (uint32_t)PLK_NTT_CW13 * 4u * 64u / (uint32_t)wt_ntc(13));
+    nb = per_cu * (uint32_t)(cus > 0 ? cus : 256);
     resident.store(nb, std::memory_order_relaxed);
   }
   return nb;
