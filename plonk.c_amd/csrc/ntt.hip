@@ -29,6 +29,8 @@
 #include "plk_device.h"
 #include "plk_internal.h"
 
+#include <chrono>
+
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -389,6 +391,19 @@ void free_tw(TwHost& t) {
 
 }  // namespace
 
+static int64_t g_marks[16];
+void plk_host_mark(int id) {
+  if (id >= 0 && id < 16 && (id == 0 || !g_marks[id]))   // (the first time of each point after mark 0)
+    g_marks[id] = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+void plk_host_marks_print(void) {
+  fprintf(stderr, "host marks (us from mark 0):");
+  for (int i = 1; i < 16; i++)
+    if (g_marks[i]) fprintf(stderr, " %d:%.1f", i, (g_marks[i] - g_marks[0]) / 1e3);
+  fprintf(stderr, "\n");
+  for (int i = 0; i < 16; i++) g_marks[i] = 0;
+}
+
 int plk_cur_device(void) {
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= PLK_MAX_DEVICES) d = 0;
@@ -604,6 +619,7 @@ static size_t pass_lds(int M, int C, bool center) {
 // d_nz (single products only): the trimmed length, computed by the last inverse pass
 static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, void* d_work, hipStream_t st,
                      uint32_t* d_nz = nullptr) {
+  PLK_MARK(3);
   // F29 (lazy reduction, fewer VALU per butterfly) whenever every convolution term fits it
   bool use29 = plk_opt(PLK_OPT_NTT_F29) && k <= f29::TWO_ADICITY;
   for (int i = 0; i < m; i++) {
@@ -828,6 +844,7 @@ int plk_poly_mul_pretransform(const uint8_t* d_b, uint64_t lb, int k, int field,
 // whole group; job i of a group uses 2^(k+3) bytes of d_work at offset i 2^(k+3)).  The
 // prover's round-3 products come in such groups (7 at 2^21, then 3 + 2 at 2^22 for n = 2^20).
 int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, size_t work_bytes, hipStream_t st) {
+  PLK_MARK(2);
   int ks[64];
   uint64_t es[64];
   if (nj > 64) {

@@ -1441,6 +1441,7 @@ void merge_groups(WJobs& cj, WJobs& ij, int nj) {
 
 template <int TB, class F>
 int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t st) {
+  PLK_MARK(4);
   const WTw twf = fwd_wtw<F>(k);   // forward roots for the inverse too (wt_center_kernel)
   int Ms[4];
   const int np = wave_plan(k, TB, Ms);
@@ -1457,11 +1458,13 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
       if (!seen) arrs.a[na++] = a;
     }
   int rc;
+  PLK_MARK(5);
   for (int i = 0; i < np - 1; i++) {
     const WPass p{k, lo[i]};
     rc = i == 0 ? fwd_m<TB, true, F>(Ms[i], p, arrs, na, twf, st) : fwd_m<TB, false, F>(Ms[i], p, arrs, na, twf, st);
     if (rc) return rc;
   }
+  PLK_MARK(6);
   const uint32_t tiles = (uint32_t)((1ull << k) >> TB);
   // operands shared by several products of the batch: their lo = 0 forward pass runs once, in
   // its own launch, instead of once per product inside the center items (PLK_OPT_NTT_SHARED_FIX

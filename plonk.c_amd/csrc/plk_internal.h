@@ -35,6 +35,17 @@ int64_t plk_opt(int opt);    // current value of a PLK_OPT_* option (capi.hip)
 #define PLK_MAX_SHARDS 16
 #define PLK_MAX_DEVICES 64   // device ids with their own NTT tables (ntt.hip)
 int plk_cur_device(void);   // the calling thread's current HIP device (0 on error)
+// host-time checkpoints (timing builds only: -DPLK_HOST_MARKS=1 records steady-clock times of
+// numbered points of a proof's enqueue path and prints their deltas after each proof)
+#ifndef PLK_HOST_MARKS
+#define PLK_HOST_MARKS 0
+#endif
+void plk_host_mark(int id);
+void plk_host_marks_print(void);
+#define PLK_MARK(i) \
+  do {                          \
+    if (PLK_HOST_MARKS) plk_host_mark(i); \
+  } while (0)
 // lanes: the entries all name the primary device and stand for host threads of the single-device
 // plk_msm_g1 (PLK_OPT_MSM_HOST_LANES), not a plk_init_devices list (plk_devices reports one device)
 int plk_shards_setup(const int* ids, int n, const uint32_t* ytab, const uint8_t* exp4, const uint8_t* inv101,

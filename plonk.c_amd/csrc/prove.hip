@@ -1948,9 +1948,11 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     const PrepArgs pa{P->d_zh, FA, FB, FC, ACC, S1, S2, S3, L.lz, n, L.la, L.lzx,
                       cA, cB, cC, cZ, a2, P->B2, c2, a3, P->B3, P->C3, P->ZW, P->Z1};
     const uint64_t blocks = std::min<uint64_t>((L.lzx + 1023) / 1024, 4096);
+    PLK_MARK(0);
     hipLaunchKernelGGL(prep_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, pa, sf,
                        P->d_S, P->d_stat, (int)ST_GATE);
     PLK_HIP(hipGetLastError());
+    PLK_MARK(1);
   } else {
     // ---- round 1: a_x = (b2 + b1 x) Z_H + f_a, ...  (3 poly_mul)
     RC(pmul(P, dS + P_BLA, 2, P->d_zh, L.lz, P->blA));
@@ -2167,6 +2169,8 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
                        (uint64_t)P->cstride, nm, P->d_res, P->exp_words, trims, ntrims, P->d_S, P->d_stat,
                        P->d_res_host, ++P->seq, P->d_done);
     PLK_HIP(hipGetLastError());
+    PLK_MARK(7);
+    if (PLK_HOST_MARKS) plk_host_marks_print();
     return PLK_OK;
   }
   if (!P->srs_irregular && plk_opt(PLK_OPT_PROVE_SRS_LOGS)) {
