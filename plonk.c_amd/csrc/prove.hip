@@ -761,6 +761,35 @@ struct LinDivs {
   LinDiv d[2];
 };
 
+// acc[k] = c0 [k == 0] + c1 [k == 1] + sum_t cf[t] p_t[i + k], k < 16 (i = 0 mod 16; terms read in
+// whole 16-byte chunks, masked past their lengths).  The products go two bytes at a time: a word's
+// bytes 0 / 2 and 1 / 3 as two 16-bit lanes (w & 0x00FF00FF, (w >> 8) & 0x00FF00FF) times cf[t] by
+// one 24-bit multiply each -- 16 x 16 x 255 + 32 < 2^16, so no lane carries into the next -- half
+// the multiplies and extracts of a per-byte loop.
+__device__ __forceinline__ void lc16_swar(const LcArgs& a, const uint32_t (&cf)[LC_MAX], uint32_t c0, uint32_t c1,
+                                          uint64_t i, uint32_t (&acc)[16]) {
+  uint32_t E[4] = {i == 0 ? c0 : 0u, 0u, 0u, 0u}, O[4] = {i == 0 ? c1 : 0u, 0u, 0u, 0u};   // even / odd bytes
+#pragma unroll
+  for (int t = 0; t < LC_MAX; t++) {
+    if (t < a.nt) {   // uniform
+      uint32_t w[4];
+      load16_masked(a.p[t], a.len[t], i, w);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        E[q] += __umul24(cf[t], w[q] & 0x00FF00FFu);
+        O[q] += __umul24(cf[t], (w[q] >> 8) & 0x00FF00FFu);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    acc[4 * q] = E[q] & 0xFFFFu;
+    acc[4 * q + 1] = O[q] & 0xFFFFu;
+    acc[4 * q + 2] = E[q] >> 16;
+    acc[4 * q + 3] = O[q] >> 16;
+  }
+}
+
 __global__ __launch_bounds__(SCAN_T) void lin_scan_sums_kernel(LinDivs L, const uint8_t* __restrict__ S) {
   const LinDiv& D = L.d[blockIdx.y];
   if ((int)blockIdx.x >= D.nb) return;
@@ -799,18 +828,7 @@ __global__ __launch_bounds__(SCAN_T) void lincomb_scan_kernel(LcBatch b, LinDivs
   const uint32_t c0 = a.c0 >= 0 ? S[a.c0] : 0u, c1 = a.c1 >= 0 ? S[a.c1] : 0u;
   const uint64_t i = (uint64_t)blockIdx.x * SCAN_B + (uint64_t)threadIdx.x * SCAN_E;
   uint32_t acc[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) acc[k] = 0;
-  if (i == 0) { acc[0] = c0; acc[1] = c1; }
-#pragma unroll
-  for (int t = 0; t < LC_MAX; t++) {
-    if (t < a.nt) {   // uniform
-      uint32_t w[4];
-      load16_masked(a.p[t], a.len[t], i, w);
-#pragma unroll
-      for (int k = 0; k < 16; k++) acc[k] += cf[t] * ((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-    }
-  }
+  lc16_swar(a, cf, c0, c1, i, acc);
   const uint32_t av = S[D.aslot];
   uint32_t pw[16];
   pw[0] = 1;
@@ -930,18 +948,7 @@ __global__ __launch_bounds__(SCAN_T) void lincomb_divide_kernel(LcBatch b, LinDi
   const uint64_t base = (uint64_t)c * SCAN_B + (uint64_t)threadIdx.x * SCAN_E;
   const uint64_t nl = a.out_len;
   uint32_t acc[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) acc[k] = 0;
-  if (base == 0) { acc[0] = c0; acc[1] = c1; }
-#pragma unroll
-  for (int t = 0; t < LC_MAX; t++) {
-    if (t < a.nt) {   // uniform
-      uint32_t w[4];
-      load16_masked(a.p[t], a.len[t], base, w);
-#pragma unroll
-      for (int k = 0; k < 16; k++) acc[k] += cf[t] * ((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-    }
-  }
+  lc16_swar(a, cf, c0, c1, base, acc);
   const uint32_t av = __builtin_amdgcn_readfirstlane(S[D.aslot]);
   uint32_t pw[16];
   pw[0] = 1;
@@ -1945,9 +1952,9 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     uint8_t* const a2 = (local & PLK_CHAIN_T2) && !derive_t2a ? P->A2 : nullptr;
     uint8_t* const c2 = (local & PLK_CHAIN_T2) ? P->C2 : nullptr;
     uint8_t* const a3 = (local & PLK_CHAIN_T3) ? P->A3 : nullptr;
+    const uint64_t blocks = std::min<uint64_t>((L.lzx + 1023) / 1024, 4096);
     const PrepArgs pa{P->d_zh, FA, FB, FC, ACC, S1, S2, S3, L.lz, n, L.la, L.lzx,
                       cA, cB, cC, cZ, a2, P->B2, c2, a3, P->B3, P->C3, P->ZW, P->Z1};
-    const uint64_t blocks = std::min<uint64_t>((L.lzx + 1023) / 1024, 4096);
     PLK_MARK(0);
     hipLaunchKernelGGL(prep_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, pa, sf,
                        P->d_S, P->d_stat, (int)ST_GATE);

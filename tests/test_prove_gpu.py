@@ -104,6 +104,23 @@ def test_commitments_srs_log_form(hip, oracle, n, seed):
                 pr.rounds_dev(dev, chal, rnd, strict=True)
 
 
+def test_commitments_irregular_srs(hip, oracle):
+    """An SRS with non-canonical encodings (an off-curve point, a coordinate >= 101): the log-form
+    conversion flags it at create and the commitments take the exact serial folds of the raw
+    bytes (src/srs.h:59-66 through src/g1.h's formulas), whatever PROVE_SRS_LOGS says."""
+    n = 256
+    polys, chal, rnd, zh, pts = _synthetic(n, 74, 2 * n + 8)
+    pts = pts.copy()
+    pts.reshape(-1)[3 * 5:3 * 5 + 3] = [7, 7, 0]       # off the curve y^2 = x^3 + 3
+    pts.reshape(-1)[3 * 40:3 * 40 + 3] = [120, 3, 0]   # x >= 101
+    want = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes()).rounds(polys, chal, rnd, strict=False)
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    for logs in (1, 0):
+        with hip.options(PROVE_SRS_LOGS=logs):
+            assert pr.rounds_dev(dev, chal, rnd, strict=False).hex() == want.hex(), logs
+
+
 @pytest.mark.parametrize("n,seed", [(8, 1), (37, 2), (256, 3), (1000, 4), (3000, 5), (2100, 6), (5000, 7)])
 def test_rounds_shape_vs_oracle(hip, oracle, n, seed):
     """(n = 2100 and 5000: t_2 (4n + 6 coefficients) and (a b) q_m (3n + 2) need different
