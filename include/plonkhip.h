@@ -91,7 +91,9 @@ enum {
                                     converted once at plk_prover_create); 0: the G1 form (3 B) */
   PLK_OPT_PROVE_PACK_FUSE = 23,  /* 1 (with PROVE_SRS_LOGS): commitments, trimmed lengths and the proof packing
                                     in one launch (commit_pack_kernel); 0: the MSM, then trim_pack_kernel */
-  PLK_OPT_COUNT = 24
+  PLK_OPT_PROVE_EARLY_COMMITS = 24, /* 1 (with PROVE_PACK_FUSE): the 7 commitments that do not wait for round 5
+                                       run as extra rows of round 5's scan launch */
+  PLK_OPT_COUNT = 25
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
 /* Diagnostics for the offline roofline tools: with PLK_OPT_NTT_LAUNCH_LOG = 1 every NTT pass launch

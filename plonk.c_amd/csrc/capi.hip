@@ -469,6 +469,7 @@ const OptDef kOpt[PLK_OPT_COUNT] = {
     {0, 0, 1, false},                          // PROVE_FUSE_DIV (measured slower)
     {1, 0, 1, false},                          // PROVE_SRS_LOGS
     {1, 0, 1, false},                          // PROVE_PACK_FUSE
+    {1, 0, 1, false},                          // PROVE_EARLY_COMMITS
 };
 struct Opts {
   std::atomic<int64_t> v[PLK_OPT_COUNT];

@@ -816,7 +816,29 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_sums_kernel(LinDivs L, const 
 // aggregate sum_{i > 0} num[i] a^i.  Every term is 16-byte aligned and readable in whole 16-byte
 // chunks up to its length (host-checked), so each term's uint4 load is issued unconditionally
 // (clamped address, masked bytes) and all of them are in flight together.
-__global__ __launch_bounds__(SCAN_T) void lincomb_scan_kernel(LcBatch b, LinDivs L, const uint8_t* __restrict__ S) {
+// (optional) commitments that do not wait for round 5, run as extra grid rows of its scan launch:
+// rows y >= the divisions are log-form MSMs of arena rows 0 .. nrows - 1 on X blocks each
+struct EarlyMsm {
+  const uint8_t* logs;
+  const uint8_t* arena;
+  uint64_t cstride, n;
+  PlkMsmResult* res;
+  const uint32_t* exp_words;
+  int nrows, nd;
+  uint32_t X;
+};
+__global__ __launch_bounds__(SCAN_T) void lincomb_scan_kernel(LcBatch b, LinDivs L, const uint8_t* __restrict__ S,
+                                                             EarlyMsm em) {
+  if ((int)blockIdx.y >= em.nd) {   // (uniform) an early commitment row
+    __shared__ uint32_t etab[PLK_GROUP_ORDER];
+    __shared__ uint32_t wsum[SCAN_T / PLK_WAVE];
+    __shared__ uint32_t wbad[SCAN_T / PLK_WAVE];
+    const int r = (int)blockIdx.y - em.nd;
+    if (blockIdx.x >= em.X) return;
+    (void)msm_log_block<SCAN_T>(em.logs, em.arena + (uint64_t)r * em.cstride, em.n, blockIdx.x, em.X, (uint32_t)r,
+                                em.res + r, em.exp_words, etab, wsum, wbad);
+    return;
+  }
   const int d = blockIdx.y;
   const LcArgs& a = b.a[d];
   const LinDiv& D = L.d[d];
@@ -1214,9 +1236,10 @@ __global__ __launch_bounds__(PACK_T) void trim_pack_kernel(TrimArgs a, int nt, c
   if (t == 0) __hip_atomic_store((uint32_t*)(host + 60), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The 9 commitments, the trimmed lengths and the packing in ONE launch (the prover's SRS in log
-// form, PLK_OPT_PROVE_PACK_FUSE): rows y < 9 of the grid are msm_log_kernel's MSMs over the
-// arena; row 9 scans the trimmed-length buffers (block x < nt: buffer x, 4 KB per step from the
+// The commitments, the trimmed lengths and the packing in ONE launch (the prover's SRS in log
+// form, PLK_OPT_PROVE_PACK_FUSE): rows y < nrows of the grid are the log-form MSMs of arena rows
+// row0 + y (all 9, or only w_z and w_z_omega when the other 7 ran inside round 5's scan launch,
+// PLK_OPT_PROVE_EARLY_COMMITS); row nrows scans the trimmed-length buffers (block x < nt: buffer x, 4 KB per step from the
 // top; the vote buffer's block ORs its bytes) while the MSM rows stream.  Every finished record
 // and every trim block then arrives on `done`; the last arrival (one thread) packs the proof and
 // the status words into the mapped host buffer and writes the completion word, as
@@ -1224,32 +1247,18 @@ __global__ __launch_bounds__(PACK_T) void trim_pack_kernel(TrimArgs a, int nt, c
 constexpr int CP_T = 256;
 __global__ __launch_bounds__(CP_T) void commit_pack_kernel(const uint8_t* __restrict__ logs, const uint8_t* arena,
                                                            uint64_t cstride, uint64_t n, PlkMsmResult* res,
-                                                           const uint32_t* __restrict__ exp_words, TrimArgs a, int nt,
-                                                           const uint8_t* __restrict__ S, uint32_t* stat,
-                                                           uint8_t* __restrict__ host, uint32_t seq, uint32_t* done) {
+                                                           const uint32_t* __restrict__ exp_words, int row0, int nrows,
+                                                           TrimArgs a, int nt, const uint8_t* __restrict__ S,
+                                                           uint32_t* stat, uint8_t* __restrict__ host, uint32_t seq,
+                                                           uint32_t* done) {
   __shared__ uint32_t etab[PLK_GROUP_ORDER];
   __shared__ uint32_t wsum[CP_T / PLK_WAVE];
   __shared__ uint32_t wbad[CP_T / PLK_WAVE];
   bool arrive = false;
-  if (blockIdx.y < 9) {
-    const uint8_t* sc = arena + (uint64_t)blockIdx.y * cstride;
-    if (threadIdx.x < PLK_GROUP_ORDER) etab[threadIdx.x] = exp_words[threadIdx.x];
-    const uint64_t stride = (uint64_t)gridDim.x * CP_T;
-    const uint64_t ngroups = n >> 4;
-    const uint4* l4 = reinterpret_cast<const uint4*>(logs);
-    const uint4* s4 = reinterpret_cast<const uint4*>(sc);
-    uint32_t acc = 0;
-    for (uint64_t g = (uint64_t)blockIdx.x * CP_T + threadIdx.x; g < ngroups; g += stride) {
-      const uint4 l = l4[g], s = s4[g];
-      uint32_t t = __builtin_amdgcn_udot4(l.x, s.x, 0u, false);   // 16 x 101 x 255 < 2^19
-      t = __builtin_amdgcn_udot4(l.y, s.y, t, false);
-      t = __builtin_amdgcn_udot4(l.z, s.z, t, false);
-      t = __builtin_amdgcn_udot4(l.w, s.w, t, false);
-      acc += t % PLK_GROUP_ORDER;
-    }
-    const uint64_t base = ngroups << 4;
-    if (blockIdx.x == 0 && base + threadIdx.x < n) acc += (uint32_t)logs[base + threadIdx.x] * sc[base + threadIdx.x];
-    arrive = msm_finish<CP_T>(acc % PLK_GROUP_ORDER, false, res + blockIdx.y, wsum, wbad, etab);
+  if ((int)blockIdx.y < nrows) {   // arena row / record row0 + y
+    const int r = row0 + (int)blockIdx.y;
+    arrive = msm_log_block<CP_T>(logs, arena + (uint64_t)r * cstride, n, blockIdx.x, gridDim.x, (uint32_t)r, res + r,
+                                 exp_words, etab, wsum, wbad);
   } else {
     const int x = (int)blockIdx.x;
     if (x >= nt) return;   // (uniform)
@@ -1282,7 +1291,7 @@ __global__ __launch_bounds__(CP_T) void commit_pack_kernel(const uint8_t* __rest
   if (!arrive) return;
   // this record's point / this trim's word is written: release it, then arrive
   __threadfence();
-  if (atomicAdd(done, 1u) != 9u + (uint32_t)nt - 1u) return;
+  if (atomicAdd(done, 1u) != (uint32_t)nrows + (uint32_t)nt - 1u) return;
   __threadfence();   // (acquire: every other arrival's writes are visible)
   *done = 0;         // re-armed for the next proof
   const int ev[7] = {S_AZ, S_BZ, S_CZ, S_S1Z, S_S2Z, S_RZ, S_ZWZ};
@@ -1421,6 +1430,7 @@ struct plk_prover {
   PlkMsmResult* d_res = nullptr;   // 9 MSM records
   uint8_t* d_srs_log = nullptr;    // the SRS in log form (srs_log_kernel), valid when !srs_irregular
   const uint32_t* exp_words = nullptr;   // the group's EXP words on this prover's device
+  int early_rows = 0;              // commitments of this call already run by round 5's scan launch
   uint32_t* d_srs_flag = nullptr;  // srs_log_kernel's irregular flag
   uint32_t* d_done = nullptr;      // commit_pack_kernel's arrival word (re-armed by its last arrival)
   uint8_t* arena = nullptr;        // [9][cstride] committed polynomials
@@ -1651,7 +1661,9 @@ struct LinDivReq {
   uint32_t* flag;
 };
 // lcs (optional): the numerators' lincombs, computed by the aggregate launch itself
-int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs, const LcBatch* lcs = nullptr) {
+int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs, const LcBatch* lcs = nullptr,
+                  const EarlyMsm* em = nullptr) {
+  P->early_rows = 0;
   if (lcs) {   // a skipped (tiny) division would shift the numerators' order: compute them apart
     int j = 0;
     bool tiny = false;
@@ -1685,7 +1697,18 @@ int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs, const Lc
     PLK_HIP(hipGetLastError());
     return PLK_OK;
   }
-  if (lcs) hipLaunchKernelGGL(lincomb_scan_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, *lcs, L, P->d_S);
+  if (lcs) {
+    EarlyMsm e{};
+    e.nd = nd;
+    if (em && em->nrows > 0) {
+      e = *em;
+      e.nd = nd;
+      e.X = std::min<uint32_t>(e.X, (uint32_t)nbmax);
+      P->early_rows = e.nrows;
+    }
+    hipLaunchKernelGGL(lincomb_scan_kernel, dim3((unsigned)nbmax, nd + (e.nrows > 0 ? e.nrows : 0)), dim3(SCAN_T), 0,
+                       P->st, *lcs, L, P->d_S, e);
+  }
   else hipLaunchKernelGGL(lin_scan_sums_kernel, dim3((unsigned)nbmax, nd), dim3(SCAN_T), 0, P->st, L, P->d_S);
   PLK_HIP(hipGetLastError());
   // denominators poly_new({-z, 1}) and ({-z omega, 1}), src/plonk.h:604-613
@@ -2147,9 +2170,18 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
       for (int t = 0; t < nb5.a[j].nt; t++) fuse = fuse && (uintptr_t)nb5.a[j].p[t] % 16 == 0;
     }
     if (!fuse) RC(lincomb_batch(P, {nb5.a[0], nb5.a[1]}));
+    // the 7 commitments that do not wait for round 5 (a b c z t_lo t_mid t_hi) as extra rows of
+    // its scan launch (log-form SRS and the fused packing only: commit_pack_kernel then runs w_z,
+    // w_z_omega and packs)
+    EarlyMsm em{};
+    const bool early = !P->srs_irregular && plk_opt(PLK_OPT_PROVE_SRS_LOGS) && plk_opt(PLK_OPT_PROVE_PACK_FUSE) &&
+                       plk_opt(PLK_OPT_PROVE_EARLY_COMMITS);
+    if (early)
+      em = EarlyMsm{P->d_srs_log, P->arena, (uint64_t)P->cstride, std::min<uint64_t>(P->cmax, P->srs_len), P->d_res,
+                    P->exp_words, 7, 0, (uint32_t)(2048 / 9)};
     RC(divide_linear(P, {{P->W, L.lw, S_Z, cWz, P->d_stat + ST_REM_W1},
                          {P->ZZ, L.lzz, S_ZOMEGA, cWzw, P->d_stat + ST_REM_W2}},
-                     fuse ? &nb5 : nullptr));
+                     fuse ? &nb5 : nullptr, early ? &em : nullptr));
   }
   // ---- trimmed lengths for the reference's exits: computed by the packing kernel after the MSM
   TrimArgs trims{};
@@ -2172,8 +2204,9 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     // commitments + trimmed lengths + packing in one launch (commit_pack_kernel)
     const uint64_t bx = std::max<uint64_t>(std::min<uint64_t>(2048 / 9, std::max<uint64_t>(1, ((nm >> 4) + CP_T - 1) / CP_T)),
                                            (uint64_t)ntrims);
-    hipLaunchKernelGGL(commit_pack_kernel, dim3((unsigned)bx, 10), dim3(CP_T), 0, P->st, P->d_srs_log, P->arena,
-                       (uint64_t)P->cstride, nm, P->d_res, P->exp_words, trims, ntrims, P->d_S, P->d_stat,
+    const int row0 = P->early_rows == 7 ? 7 : 0, nrows = 9 - row0;
+    hipLaunchKernelGGL(commit_pack_kernel, dim3((unsigned)bx, nrows + 1), dim3(CP_T), 0, P->st, P->d_srs_log, P->arena,
+                       (uint64_t)P->cstride, nm, P->d_res, P->exp_words, row0, nrows, trims, ntrims, P->d_S, P->d_stat,
                        P->d_res_host, ++P->seq, P->d_done);
     PLK_HIP(hipGetLastError());
     PLK_MARK(7);

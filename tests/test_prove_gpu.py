@@ -90,6 +90,7 @@ def test_round5_divisions_vs_oracle(hip, oracle, n, seed, z):
 def test_commitments_srs_log_form(hip, oracle, n, seed):
     """The 9 commitments from the SRS in log form (PROVE_SRS_LOGS = 1: srs_log_kernel once at
     create; per proof commit_pack_kernel -- commitments, trimmed lengths and packing in one
+    launch, with or without the 7 commitments that do not wait for round 5 running inside its scan
     launch -- or msm_log_kernel + trim_pack_kernel; committed lengths n + 2 .. n + 3, so 16-point
     groups plus a ragged tail) and from the G1 form give the oracle's proof, and the strict
     rejection (its status words) is the same in every form."""
@@ -97,9 +98,9 @@ def test_commitments_srs_log_form(hip, oracle, n, seed):
     want = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes()).rounds(polys, chal, rnd, strict=False)
     pr = hip.Prover(n, zh, pts)
     dev = [torch.from_numpy(p).to("cuda") for p in polys]
-    for logs, fuse in ((1, 1), (1, 0), (0, 1), (1, 1)):
-        with hip.options(PROVE_SRS_LOGS=logs, PROVE_PACK_FUSE=fuse):
-            assert pr.rounds_dev(dev, chal, rnd, strict=False).hex() == want.hex(), (logs, fuse)
+    for logs, fuse, early in ((1, 1, 1), (1, 1, 0), (1, 0, 1), (0, 1, 1), (1, 1, 1)):
+        with hip.options(PROVE_SRS_LOGS=logs, PROVE_PACK_FUSE=fuse, PROVE_EARLY_COMMITS=early):
+            assert pr.rounds_dev(dev, chal, rnd, strict=False).hex() == want.hex(), (logs, fuse, early)
             with pytest.raises(hip.PlonkHipError, match="remainder"):
                 pr.rounds_dev(dev, chal, rnd, strict=True)
 
