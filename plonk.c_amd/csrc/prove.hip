@@ -426,14 +426,11 @@ struct EvArgs {
 
 __device__ void scalars_r45(uint8_t* S, uint32_t tz);
 
-// One launch per batch of evaluations: blockIdx.y = evaluation, EV_BLOCKS blocks each.  Every
-// block adds its partial sum with a ticket to its evaluation's arrival word; the last block of
-// an evaluation adds the finished value with a ticket to the top word; the last of those writes
-// every S[out] and runs the round's scalar program -- the partial / final / scalar kernels of a
-// three-launch chain in one.
-__global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict__ S, uint32_t* __restrict__ tick,
-                                                   uint32_t* __restrict__ stat) {
-  const int e = blockIdx.y;
+// Block bx of BX of evaluation e (eval_kernel's rows, or extra blocks of another launch): its
+// partial with a ticket to the row's arrival word; the row's last block writes S[out] and, with
+// `top`, takes a ticket on the top word -- whose last taker runs the round's scalar program.
+__device__ __forceinline__ void eval_row_block(const EvArgs& a, int e, uint32_t bx, uint32_t BX, uint8_t* S,
+                                               uint32_t* tick, uint32_t* stat, bool top) {
   const uint32_t x = S[a.xslot[e]];
   uint32_t pw[16];
   pw[0] = 1;
@@ -442,11 +439,11 @@ __global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict
   const uint8_t* p = a.p[e];
   const uint64_t n = a.len[e];
   uint32_t acc = 0;
-  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t gid = (uint64_t)bx * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)BX * blockDim.x * 16;
   if (x == 0) {                       // poly_eval(p, 0) = p[0]
     if (gid == 0 && n) acc = p[0];
   } else if (a.vec[e] == 2) {         // readable in whole chunks: 4 loads in flight per thread
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
     for (uint64_t i0 = gid * 16; i0 < n; i0 += 4 * stride) {
       uint32_t w[4][4];
 #pragma unroll
@@ -460,7 +457,6 @@ __global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict
       }
     }
   } else if (a.vec[e]) {              // 16 coefficients per step: i = 0 mod 16 so x^(i+k) = x^k
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
     for (uint64_t i = gid * 16; i < n; i += stride) {
       uint32_t w[4];
       load16(p, n, i, w);
@@ -470,7 +466,6 @@ __global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict
       acc = (acc + s) % HFP;
     }
   } else {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
     for (uint64_t i = gid * 16; i < n; i += stride) {
       uint32_t s = 0;
 #pragma unroll
@@ -490,17 +485,28 @@ __global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict
   const uint32_t mine = (red[0] + red[1] + red[2] + red[3]) % HFP;
   unsigned long long* row = reinterpret_cast<unsigned long long*>(tick) + e * (TICK_STRIDE / 2);
   const unsigned long long old = atomicAdd(row, (unsigned long long)mine | (1ull << 32));
-  if ((uint32_t)(old >> 32) != gridDim.x - 1) return;
+  if ((uint32_t)(old >> 32) != BX - 1) return;
   *row = 0;                                               // re-armed for the next launch
   // the row's last block publishes the value: only these <= EV_MAX blocks fence
   S[a.out[e]] = (uint8_t)(((uint32_t)old + mine) % HFP);
   __threadfence();
+  if (!top) return;
   uint32_t* topw = tick + EV_MAX * TICK_STRIDE;
   if (atomicAdd(topw, 1u) != (uint32_t)a.ne - 1) return;
   __threadfence();
   *topw = 0;
   if (a.post == EV_POST_R4) scalars_r45(S, S[S_TZ]);   // round 4's scalars (incl. r_z) and round 5's (w_z constant)
   if (a.post == EV_POST_ACC) stat[ST_ACC] = S[S_ACCW];   // acc_x(omega^n), src/plonk.h:366-368
+}
+
+// One launch per batch of evaluations: blockIdx.y = evaluation, EV_BLOCKS blocks each.  Every
+// block adds its partial sum with a ticket to its evaluation's arrival word; the last block of
+// an evaluation adds the finished value with a ticket to the top word; the last of those writes
+// every S[out] and runs the round's scalar program -- the partial / final / scalar kernels of a
+// three-launch chain in one.
+__global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict__ S, uint32_t* __restrict__ tick,
+                                                   uint32_t* __restrict__ stat) {
+  eval_row_block(a, (int)blockIdx.y, blockIdx.x, gridDim.x, S, tick, stat, true);
 }
 
 // ------------------------------------------------------------------ poly_divide
@@ -1602,7 +1608,7 @@ int lincomb(plk_prover* P, std::initializer_list<std::pair<const uint8_t*, uint6
   return PLK_OK;
 }
 
-int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64_t, int, int>> ev, int post) {
+EvArgs make_evargs(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64_t, int, int>> ev, int post) {
   EvArgs a{};
   int e = 0;
   for (const auto& t : ev) {
@@ -1618,9 +1624,18 @@ int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64
   }
   a.ne = e;
   a.post = post;
-  hipLaunchKernelGGL(eval_kernel, dim3(EV_BLOCKS, e), dim3(256), 0, P->st, a, P->d_S, P->d_tick, P->d_stat);
+  return a;
+}
+// rows [0, nrows) of a (a.ne = nrows: the top ticket counts those)
+int evals_launch(plk_prover* P, EvArgs a, int nrows) {
+  a.ne = nrows;
+  hipLaunchKernelGGL(eval_kernel, dim3(EV_BLOCKS, nrows), dim3(256), 0, P->st, a, P->d_S, P->d_tick, P->d_stat);
   PLK_HIP(hipGetLastError());
   return PLK_OK;
+}
+int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64_t, int, int>> ev, int post) {
+  const EvArgs a = make_evargs(P, ev, post);
+  return evals_launch(P, a, a.ne);
 }
 
 int pmul(plk_prover* P, const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb, uint8_t* out) {
