@@ -92,7 +92,8 @@ enum {
   PLK_OPT_PROVE_PACK_FUSE = 23,  /* 1 (with PROVE_SRS_LOGS): commitments, trimmed lengths and the proof packing
                                     in one launch (commit_pack_kernel); 0: the MSM, then trim_pack_kernel */
   PLK_OPT_PROVE_EARLY_COMMITS = 24, /* 1 (with PROVE_PACK_FUSE): the 7 commitments that do not wait for round 5
-                                       run as extra rows of round 5's scan launch */
+                                       run as extra rows of round 5's scan launch; 2: of round 4's evaluation
+                                       launch */
   PLK_OPT_COUNT = 25
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */

@@ -469,7 +469,7 @@ const OptDef kOpt[PLK_OPT_COUNT] = {
     {0, 0, 1, false},                          // PROVE_FUSE_DIV (measured slower)
     {1, 0, 1, false},                          // PROVE_SRS_LOGS
     {1, 0, 1, false},                          // PROVE_PACK_FUSE
-    {1, 0, 1, false},                          // PROVE_EARLY_COMMITS
+    {1, 0, 2, false},                          // PROVE_EARLY_COMMITS (2: in round 4's evaluation launch)
 };
 struct Opts {
   std::atomic<int64_t> v[PLK_OPT_COUNT];

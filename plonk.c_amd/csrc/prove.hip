@@ -504,8 +504,29 @@ __device__ __forceinline__ void eval_row_block(const EvArgs& a, int e, uint32_t 
 // an evaluation adds the finished value with a ticket to the top word; the last of those writes
 // every S[out] and runs the round's scalar program -- the partial / final / scalar kernels of a
 // three-launch chain in one.
+// (optional) commitments that do not wait for round 5, run as extra grid rows of an earlier launch
+// (round 5's scan, or round 4's evaluations): rows y >= nd are log-form MSMs of arena rows
+// 0 .. nrows - 1 on X blocks each
+struct EarlyMsm {
+  const uint8_t* logs;
+  const uint8_t* arena;
+  uint64_t cstride, n;
+  PlkMsmResult* res;
+  const uint32_t* exp_words;
+  int nrows, nd;
+  uint32_t X;
+};
 __global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict__ S, uint32_t* __restrict__ tick,
-                                                   uint32_t* __restrict__ stat) {
+                                                   uint32_t* __restrict__ stat, EarlyMsm em) {
+  if ((int)blockIdx.y >= a.ne) {   // (uniform) an early commitment row
+    __shared__ uint32_t etab[PLK_GROUP_ORDER];
+    __shared__ uint32_t wsum[256 / PLK_WAVE];
+    __shared__ uint32_t wbad[256 / PLK_WAVE];
+    const int r = (int)blockIdx.y - a.ne;
+    (void)msm_log_block<256>(em.logs, em.arena + (uint64_t)r * em.cstride, em.n, blockIdx.x, gridDim.x, (uint32_t)r,
+                             em.res + r, em.exp_words, etab, wsum, wbad);
+    return;
+  }
   eval_row_block(a, (int)blockIdx.y, blockIdx.x, gridDim.x, S, tick, stat, true);
 }
 
@@ -822,17 +843,6 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_sums_kernel(LinDivs L, const 
 // aggregate sum_{i > 0} num[i] a^i.  Every term is 16-byte aligned and readable in whole 16-byte
 // chunks up to its length (host-checked), so each term's uint4 load is issued unconditionally
 // (clamped address, masked bytes) and all of them are in flight together.
-// (optional) commitments that do not wait for round 5, run as extra grid rows of its scan launch:
-// rows y >= the divisions are log-form MSMs of arena rows 0 .. nrows - 1 on X blocks each
-struct EarlyMsm {
-  const uint8_t* logs;
-  const uint8_t* arena;
-  uint64_t cstride, n;
-  PlkMsmResult* res;
-  const uint32_t* exp_words;
-  int nrows, nd;
-  uint32_t X;
-};
 __global__ __launch_bounds__(SCAN_T) void lincomb_scan_kernel(LcBatch b, LinDivs L, const uint8_t* __restrict__ S,
                                                              EarlyMsm em) {
   if ((int)blockIdx.y >= em.nd) {   // (uniform) an early commitment row
@@ -1627,15 +1637,22 @@ EvArgs make_evargs(plk_prover* P, std::initializer_list<std::tuple<const uint8_t
   return a;
 }
 // rows [0, nrows) of a (a.ne = nrows: the top ticket counts those)
-int evals_launch(plk_prover* P, EvArgs a, int nrows) {
+int evals_launch(plk_prover* P, EvArgs a, int nrows, const EarlyMsm* em = nullptr) {
   a.ne = nrows;
-  hipLaunchKernelGGL(eval_kernel, dim3(EV_BLOCKS, nrows), dim3(256), 0, P->st, a, P->d_S, P->d_tick, P->d_stat);
+  EarlyMsm e{};
+  if (em && em->nrows > 0) {
+    e = *em;
+    P->early_rows = e.nrows;
+  }
+  hipLaunchKernelGGL(eval_kernel, dim3(EV_BLOCKS, nrows + e.nrows), dim3(256), 0, P->st, a, P->d_S, P->d_tick, P->d_stat,
+                     e);
   PLK_HIP(hipGetLastError());
   return PLK_OK;
 }
-int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64_t, int, int>> ev, int post) {
+int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64_t, int, int>> ev, int post,
+          const EarlyMsm* em = nullptr) {
   const EvArgs a = make_evargs(P, ev, post);
-  return evals_launch(P, a, a.ne);
+  return evals_launch(P, a, a.ne, em);
 }
 
 int pmul(plk_prover* P, const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb, uint8_t* out) {
@@ -1678,7 +1695,6 @@ struct LinDivReq {
 // lcs (optional): the numerators' lincombs, computed by the aggregate launch itself
 int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs, const LcBatch* lcs = nullptr,
                   const EarlyMsm* em = nullptr) {
-  P->early_rows = 0;
   if (lcs) {   // a skipped (tiny) division would shift the numerators' order: compute them apart
     int j = 0;
     bool tiny = false;
@@ -2161,11 +2177,20 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   // (src/plonk.h:536-571; the last product is z_x s_sigma_3 from round 3 times r3 beta z_omega_z).
   // r(x) is never materialised: r_z comes from its terms' evaluations (scalars_r4) and w_z(x)
   // takes v r(x) term by term.  One launch: the 14 evaluations + rounds 4/5 scalar programs.
+  // the 7 commitments that do not wait for round 5 (a b c z t_lo t_mid t_hi) as extra grid rows of
+  // this launch (PLK_OPT_PROVE_EARLY_COMMITS = 2) or of round 5's scan launch (= 1); log-form SRS
+  // and the fused packing only -- commit_pack_kernel then runs w_z, w_z_omega and packs
+  P->early_rows = 0;
+  const int64_t early = !P->srs_irregular && plk_opt(PLK_OPT_PROVE_SRS_LOGS) && plk_opt(PLK_OPT_PROVE_PACK_FUSE)
+                            ? plk_opt(PLK_OPT_PROVE_EARLY_COMMITS)
+                            : 0;
+  const EarlyMsm em{P->d_srs_log, P->arena, (uint64_t)P->cstride, std::min<uint64_t>(P->cmax, P->srs_len), P->d_res,
+                    P->exp_words, 7, 0, (uint32_t)(2048 / 9)};
   RC(evals(P, {{cA, L.la, S_Z, S_AZ}, {cB, L.la, S_Z, S_BZ}, {cC, L.la, S_Z, S_CZ}, {S1, n, S_Z, S_S1Z},
                {S2, n, S_Z, S_S2Z}, {P->TX, L.ltx, S_Z, S_TZ}, {P->ZW, L.lzw, S_Z, S_ZWZ}, {L1, n, S_Z, S_L1Z},
                {QM, n, S_Z, S_QMZ}, {QL, n, S_Z, S_QLZ}, {QR, n, S_Z, S_QRZ}, {QO, n, S_Z, S_QOZ},
                {cZ, L.lzx, S_Z, S_ZXZ}, {P->P3, L.lr3, S_Z, S_P3Z}},
-           EV_POST_R4));
+           EV_POST_R4, early == 2 ? &em : nullptr));
   // ---- round 5: opening polynomials (src/plonk.h:580-621)
   // w_z numerator and z(x) - z_omega_z, then both divisions, each pair in one launch per phase
   {
@@ -2185,18 +2210,9 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
       for (int t = 0; t < nb5.a[j].nt; t++) fuse = fuse && (uintptr_t)nb5.a[j].p[t] % 16 == 0;
     }
     if (!fuse) RC(lincomb_batch(P, {nb5.a[0], nb5.a[1]}));
-    // the 7 commitments that do not wait for round 5 (a b c z t_lo t_mid t_hi) as extra rows of
-    // its scan launch (log-form SRS and the fused packing only: commit_pack_kernel then runs w_z,
-    // w_z_omega and packs)
-    EarlyMsm em{};
-    const bool early = !P->srs_irregular && plk_opt(PLK_OPT_PROVE_SRS_LOGS) && plk_opt(PLK_OPT_PROVE_PACK_FUSE) &&
-                       plk_opt(PLK_OPT_PROVE_EARLY_COMMITS);
-    if (early)
-      em = EarlyMsm{P->d_srs_log, P->arena, (uint64_t)P->cstride, std::min<uint64_t>(P->cmax, P->srs_len), P->d_res,
-                    P->exp_words, 7, 0, (uint32_t)(2048 / 9)};
     RC(divide_linear(P, {{P->W, L.lw, S_Z, cWz, P->d_stat + ST_REM_W1},
                          {P->ZZ, L.lzz, S_ZOMEGA, cWzw, P->d_stat + ST_REM_W2}},
-                     fuse ? &nb5 : nullptr, early ? &em : nullptr));
+                     fuse ? &nb5 : nullptr, early == 1 ? &em : nullptr));
   }
   // ---- trimmed lengths for the reference's exits: computed by the packing kernel after the MSM
   TrimArgs trims{};

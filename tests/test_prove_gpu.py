@@ -98,7 +98,7 @@ def test_commitments_srs_log_form(hip, oracle, n, seed):
     want = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes()).rounds(polys, chal, rnd, strict=False)
     pr = hip.Prover(n, zh, pts)
     dev = [torch.from_numpy(p).to("cuda") for p in polys]
-    for logs, fuse, early in ((1, 1, 1), (1, 1, 0), (1, 0, 1), (0, 1, 1), (1, 1, 1)):
+    for logs, fuse, early in ((1, 1, 1), (1, 1, 0), (1, 1, 2), (1, 0, 1), (0, 1, 1), (1, 1, 1)):
         with hip.options(PROVE_SRS_LOGS=logs, PROVE_PACK_FUSE=fuse, PROVE_EARLY_COMMITS=early):
             assert pr.rounds_dev(dev, chal, rnd, strict=False).hex() == want.hex(), (logs, fuse, early)
             with pytest.raises(hip.PlonkHipError, match="remainder"):
