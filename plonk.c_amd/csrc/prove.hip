@@ -643,6 +643,21 @@ __global__ __launch_bounds__(256) void divide_binomial4_kernel(const uint8_t* __
   if (threadIdx.x == 0) rem_part[blockIdx.x] = vote ? 1 : 0;
 }
 
+// A word's bytes 0 / 2 (lanes02) or 1 / 3 (lanes13) as two 16-bit lanes for the two-bytes-per-
+// multiply lincombs.  The empty asm hides the mask from the optimizer: this compiler (ROCm 7.2
+// clang 22, gfx942 / gfx950) rewrites a straight-line sum of byte x (w & 0x00FF00FF) products as
+// one v_dot4_u32_u8 over byte 0 alone, dropping the byte-2 lane (tools/swar_dot4_repro.hip).
+__device__ __forceinline__ uint32_t lanes02(uint32_t w) {
+  uint32_t m = w & 0x00FF00FFu;
+  asm("" : "+v"(m));
+  return m;
+}
+__device__ __forceinline__ uint32_t lanes13(uint32_t w) {
+  uint32_t m = (w >> 8) & 0x00FF00FFu;
+  asm("" : "+v"(m));
+  return m;
+}
+
 // t(x) in one launch: the numerator lincomb (src/plonk.h:494-503) evaluated per chain element
 // (no numerator buffer: its dwords come straight from the 8 product / q_c terms), the Z_H
 // division of divide_binomial4_kernel, and the t_lo / t_mid / t_hi slices (src/plonk.h:513-519)
@@ -803,8 +818,8 @@ __device__ __forceinline__ void lc16_swar(const LcArgs& a, const uint32_t (&cf)[
       load16_masked(a.p[t], a.len[t], i, w);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
-        E[q] += __umul24(cf[t], w[q] & 0x00FF00FFu);
-        O[q] += __umul24(cf[t], (w[q] >> 8) & 0x00FF00FFu);
+        E[q] += __umul24(cf[t], lanes02(w[q]));
+        O[q] += __umul24(cf[t], lanes13(w[q]));
       }
     }
   }

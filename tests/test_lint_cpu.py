@@ -15,6 +15,10 @@ CSRC = os.path.join(ROOT, "plonk.c_amd", "csrc")
 # a hex constant with 0xFF bytes separated by zero bytes (0x00FF00FF, 0xFF00FF): byte lanes.  Contiguous
 # masks (0xFF, 0xFFFF, 0xFFFF0000) select one field and do not match.
 LANE_MASK = re.compile(r"0x0*ff(?:00)+ff(?:00|ff)*u?\b", re.IGNORECASE)
+# a product: `*` or the 24-bit multiply intrinsics (round 4's first lc16_swar had the mask inside
+# __umul24 and passed a `*`-only check; it now goes through prove.hip's lanes02 / lanes13, whose
+# empty asm keeps the combine from seeing the mask)
+MUL = re.compile(r"\*|__u?mul24|__builtin_amdgcn_mul_u?24")
 
 
 def test_no_swar_lane_masks_in_products():
@@ -25,7 +29,7 @@ def test_no_swar_lane_masks_in_products():
         with open(os.path.join(CSRC, name)) as f:
             for no, line in enumerate(f, 1):
                 code = line.split("//")[0]
-                if LANE_MASK.search(code) and "*" in code:
+                if LANE_MASK.search(code) and MUL.search(code):
                     hits.append("%s:%d: %s" % (name, no, line.strip()))
     assert not hits, "SWAR lane mask in a product (see tools/swar_probe.hip):\n" + "\n".join(hits)
 
@@ -35,3 +39,18 @@ def test_lane_mask_pattern():
     assert LANE_MASK.search("x * (y & 0xff00ff)")
     assert not LANE_MASK.search("(d & 0xFFu) * c")
     assert not LANE_MASK.search("v & 0xFFFFu")
+    assert MUL.search("E += __umul24(cf, w & 0x00FF00FFu);")
+
+
+def test_guard_defeats_the_combine():
+    """The empty-asm guard still keeps this compiler from forming the byte-0-only v_dot4
+    (compile-only: tools/swar_dot4_check.sh on tools/swar_dot4_repro.hip)."""
+    import shutil
+    import subprocess
+    import pytest
+    if not os.path.exists("/opt/rocm/bin/hipcc") or not shutil.which("awk"):
+        pytest.skip("no hipcc")
+    out = subprocess.run(["bash", os.path.join(ROOT, "tools", "swar_dot4_check.sh")], capture_output=True,
+                         text=True, timeout=300, check=True).stdout.split("\n")
+    res = dict(l.split(" ", 1) for l in out if l.strip())
+    assert res["swar_guarded"] == "dot4=0 mask=4", out
