@@ -408,6 +408,9 @@ __global__ __launch_bounds__(256) void copy3_kernel(Copy3 c) {
 // ------------------------------------------------------------------ poly_eval (batched)
 // Horner of src/poly.h:265-272 == sum c_i x^i mod 17; x^i = x^(i mod 16) for x != 0.
 constexpr int EV_MAX = 16;
+#ifndef PLK_SLICE_WORDS
+#define PLK_SLICE_WORDS 1   // numdiv_kernel: t_lo / t_mid / t_hi stored a word (or two halves) at a time
+#endif
 #ifndef PLK_EV_BLOCKS
 #define PLK_EV_BLOCKS 64
 #endif
@@ -734,13 +737,28 @@ __global__ __launch_bounds__(256) void numdiv_kernel(LcArgs a, const uint8_t* __
 #pragma unroll
         for (int b = 0; b < 4; b++)
           if ((uint32_t)k >= skip[b]) q[j0 + b] = (uint8_t)(o >> (8 * b));
+      // the slices: a whole word inside one slice as one dword (or two 16-bit halves: t_mid
+      // starts at n + 2 = 2 mod 4), else byte by byte
+      const int s0 = j0 < sl.part ? 0 : (j0 < 2 * sl.part ? 1 : 2);
+      const uint64_t o0 = j0 - (uint64_t)s0 * sl.part;
+      uint8_t* const d0 = sl.dst[s0] + o0;
+      if (PLK_SLICE_WORDS && skip[0] == 0 && skip[3] == 0 && o0 + 4 <= sl.len[s0] &&
+          (s0 == 2 || o0 + 4 <= sl.part) && ((uintptr_t)d0 & 1) == 0) {
+        if (((uintptr_t)d0 & 3) == 0) {
+          *reinterpret_cast<uint32_t*>(d0) = o;
+        } else {
+          reinterpret_cast<uint16_t*>(d0)[0] = (uint16_t)o;
+          reinterpret_cast<uint16_t*>(d0)[1] = (uint16_t)(o >> 16);
+        }
+      } else {
 #pragma unroll
-      for (int b = 0; b < 4; b++) {
-        if ((uint32_t)k < skip[b]) continue;
-        const uint64_t j = j0 + b;
-        const int si = j < sl.part ? 0 : (j < 2 * sl.part ? 1 : 2);
-        const uint64_t off = j - (uint64_t)si * sl.part;
-        if (off < sl.len[si]) sl.dst[si][off] = (uint8_t)(o >> (8 * b));
+        for (int b = 0; b < 4; b++) {
+          if ((uint32_t)k < skip[b]) continue;
+          const uint64_t j = j0 + b;
+          const int si = j < sl.part ? 0 : (j < 2 * sl.part ? 1 : 2);
+          const uint64_t off = j - (uint64_t)si * sl.part;
+          if (off < sl.len[si]) sl.dst[si][off] = (uint8_t)(o >> (8 * b));
+        }
       }
     }
   }
