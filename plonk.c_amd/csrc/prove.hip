@@ -407,9 +407,13 @@ __global__ __launch_bounds__(256) void copy3_kernel(Copy3 c) {
 
 // ------------------------------------------------------------------ poly_eval (batched)
 // Horner of src/poly.h:265-272 == sum c_i x^i mod 17; x^i = x^(i mod 16) for x != 0.
-constexpr int EV_MAX = 16;
+constexpr int EV_MAX = 16;   // evaluations per launch (arrival words)
+constexpr int EV_ROWS = 24;  // grid rows: a long evaluation runs as several rows (EvArgs::grp)
 #ifndef PLK_SLICE_WORDS
 #define PLK_SLICE_WORDS 1   // numdiv_kernel: t_lo / t_mid / t_hi stored a word (or two halves) at a time
+#endif
+#ifndef PLK_EV_SPLIT
+#define PLK_EV_SPLIT 1   // long evaluations as several grid rows (make_evargs)
 #endif
 #ifndef PLK_EV_BLOCKS
 #define PLK_EV_BLOCKS 64
@@ -418,13 +422,19 @@ constexpr int EV_BLOCKS = PLK_EV_BLOCKS;   // x 256 threads x 4 uint4 loads in f
 constexpr int TICK_STRIDE = 32;   // one 128-byte line per arrival word
 enum EvPost : int { EV_POST_NONE = 0, EV_POST_ACC = 1, EV_POST_R4 = 4 };
 struct EvArgs {
-  const uint8_t* p[EV_MAX];
-  uint64_t len[EV_MAX];
-  int xslot[EV_MAX];
-  int out[EV_MAX];
-  int vec[EV_MAX];   // pointer 16-byte aligned: uint4 loads
-  int ne;
-  int post;          // scalar program the last block runs (EvPost)
+  const uint8_t* p[EV_ROWS];
+  uint64_t len[EV_ROWS];
+  int xslot[EV_ROWS];
+  int out[EV_ROWS];
+  int vec[EV_ROWS];   // pointer 16-byte aligned: uint4 loads
+  // row -> evaluation: a row is coefficients [off, off + len) of its evaluation's polynomial
+  // (off = 0 mod 16, so x^(off + i) = x^i); the evaluation's parts rows share its arrival word
+  int grp[EV_ROWS];
+  int parts[EV_ROWS];
+  int first[EV_ROWS];   // off == 0 (the row that holds p[0])
+  int ne;               // evaluations (the top ticket counts them)
+  int nr;               // rows
+  int post;             // scalar program the last block runs (EvPost)
 };
 
 __device__ void scalars_r45(uint8_t* S, uint32_t tz);
@@ -445,7 +455,7 @@ __device__ __forceinline__ void eval_row_block(const EvArgs& a, int e, uint32_t 
   const uint64_t gid = (uint64_t)bx * blockDim.x + threadIdx.x;
   const uint64_t stride = (uint64_t)BX * blockDim.x * 16;
   if (x == 0) {                       // poly_eval(p, 0) = p[0]
-    if (gid == 0 && n) acc = p[0];
+    if (gid == 0 && n && a.first[e]) acc = p[0];
   } else if (a.vec[e] == 2) {         // readable in whole chunks: 4 loads in flight per thread
     for (uint64_t i0 = gid * 16; i0 < n; i0 += 4 * stride) {
       uint32_t w[4][4];
@@ -486,9 +496,9 @@ __device__ __forceinline__ void eval_row_block(const EvArgs& a, int e, uint32_t 
   // the partial travels inside the atomic (no fence: a device-scope release per block costs an
   // L2 writeback each, 2048 of them took 60 us): row word = sum | arrivals << 32
   const uint32_t mine = (red[0] + red[1] + red[2] + red[3]) % HFP;
-  unsigned long long* row = reinterpret_cast<unsigned long long*>(tick) + e * (TICK_STRIDE / 2);
+  unsigned long long* row = reinterpret_cast<unsigned long long*>(tick) + a.grp[e] * (TICK_STRIDE / 2);
   const unsigned long long old = atomicAdd(row, (unsigned long long)mine | (1ull << 32));
-  if ((uint32_t)(old >> 32) != BX - 1) return;
+  if ((uint32_t)(old >> 32) != BX * (uint32_t)a.parts[e] - 1) return;
   *row = 0;                                               // re-armed for the next launch
   // the row's last block publishes the value: only these <= EV_MAX blocks fence
   S[a.out[e]] = (uint8_t)(((uint32_t)old + mine) % HFP);
@@ -521,11 +531,11 @@ struct EarlyMsm {
 };
 __global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict__ S, uint32_t* __restrict__ tick,
                                                    uint32_t* __restrict__ stat, EarlyMsm em) {
-  if ((int)blockIdx.y >= a.ne) {   // (uniform) an early commitment row
+  if ((int)blockIdx.y >= a.nr) {   // (uniform) an early commitment row
     __shared__ uint32_t etab[PLK_GROUP_ORDER];
     __shared__ uint32_t wsum[256 / PLK_WAVE];
     __shared__ uint32_t wbad[256 / PLK_WAVE];
-    const int r = (int)blockIdx.y - a.ne;
+    const int r = (int)blockIdx.y - a.nr;
     (void)msm_log_block<256>(em.logs, em.arena + (uint64_t)r * em.cstride, em.n, blockIdx.x, gridDim.x, (uint32_t)r,
                              em.res + r, em.exp_words, etab, wsum, wbad);
     return;
@@ -1653,25 +1663,45 @@ int lincomb(plk_prover* P, std::initializer_list<std::pair<const uint8_t*, uint6
 
 EvArgs make_evargs(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64_t, int, int>> ev, int post) {
   EvArgs a{};
-  int e = 0;
+  // a polynomial much longer than the shortest one (t(x): 3n, the r(x) part: 2n) runs as several
+  // rows of about the shortest length, so its blocks do no more work than the others' and the
+  // launch does not wait on one row's tail
+  uint64_t base = ~0ull;
+  for (const auto& t : ev) base = std::min<uint64_t>(base, std::max<uint64_t>(std::get<1>(t), 1));
+  int spare = EV_ROWS - (int)ev.size();
+  int e = 0, r = 0;
   for (const auto& t : ev) {
-    a.p[e] = std::get<0>(t);
-    a.len[e] = std::get<1>(t);
-    a.xslot[e] = std::get<2>(t);
-    a.out[e] = std::get<3>(t);
+    const uint8_t* p = std::get<0>(t);
+    const uint64_t len = std::get<1>(t);
     // 2: aligned and readable in whole 16-byte chunks (length a multiple of 16, or inside the
     // prover's own padded allocation); 1: aligned; 0: bytes
-    const bool inside = a.p[e] >= P->mem && a.p[e] < P->mem + P->mem_bytes;
-    a.vec[e] = ((uintptr_t)a.p[e] % 16) != 0 ? 0 : ((a.len[e] % 16 == 0 || inside) ? 2 : 1);
+    const bool inside = p >= P->mem && p < P->mem + P->mem_bytes;
+    const int vec = ((uintptr_t)p % 16) != 0 ? 0 : ((len % 16 == 0 || inside) ? 2 : 1);
+    int parts = 1;
+    if (PLK_EV_SPLIT && vec && base >= 4096 && len >= 2 * base)
+      parts = (int)std::min<uint64_t>((len + base / 2) / base, (uint64_t)(1 + spare));
+    spare -= parts - 1;
+    const uint64_t chunk = ((len + parts - 1) / parts + 15) / 16 * 16;
+    for (int k = 0; k < parts; k++, r++) {
+      const uint64_t off = std::min<uint64_t>(k * chunk, len);
+      a.p[r] = p + off;
+      a.len[r] = std::min<uint64_t>(chunk, len - off);
+      a.xslot[r] = std::get<2>(t);
+      a.out[r] = std::get<3>(t);
+      a.vec[r] = vec;   // (off = 0 mod 16: the alignment and the whole-chunk reads carry over)
+      a.grp[r] = e;
+      a.parts[r] = parts;
+      a.first[r] = k == 0;
+    }
     e++;
   }
   a.ne = e;
+  a.nr = r;
   a.post = post;
   return a;
 }
-// rows [0, nrows) of a (a.ne = nrows: the top ticket counts those)
-int evals_launch(plk_prover* P, EvArgs a, int nrows, const EarlyMsm* em = nullptr) {
-  a.ne = nrows;
+int evals_launch(plk_prover* P, const EvArgs& a, const EarlyMsm* em = nullptr) {
+  const int nrows = a.nr;
   EarlyMsm e{};
   if (em && em->nrows > 0) {
     e = *em;
@@ -1685,7 +1715,7 @@ int evals_launch(plk_prover* P, EvArgs a, int nrows, const EarlyMsm* em = nullpt
 int evals(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64_t, int, int>> ev, int post,
           const EarlyMsm* em = nullptr) {
   const EvArgs a = make_evargs(P, ev, post);
-  return evals_launch(P, a, a.ne, em);
+  return evals_launch(P, a, em);
 }
 
 int pmul(plk_prover* P, const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb, uint8_t* out) {
