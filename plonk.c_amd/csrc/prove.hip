@@ -415,6 +415,9 @@ constexpr int EV_ROWS = 24;  // grid rows: a long evaluation runs as several row
 #ifndef PLK_EV_SPLIT
 #define PLK_EV_SPLIT 1   // long evaluations as several grid rows (make_evargs)
 #endif
+#ifndef PLK_CP_BX
+#define PLK_CP_BX 227   // commit_pack_kernel: blocks per MSM row at most (2048 / 9)
+#endif
 #ifndef PLK_EV_BLOCKS
 #define PLK_EV_BLOCKS 64
 #endif
@@ -2296,9 +2299,10 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   // (the 9 result records are zeroed at plk_prover_create and every launch leaves them re-armed)
   if (!P->srs_irregular && plk_opt(PLK_OPT_PROVE_SRS_LOGS) && plk_opt(PLK_OPT_PROVE_PACK_FUSE)) {
     // commitments + trimmed lengths + packing in one launch (commit_pack_kernel)
-    const uint64_t bx = std::max<uint64_t>(std::min<uint64_t>(2048 / 9, std::max<uint64_t>(1, ((nm >> 4) + CP_T - 1) / CP_T)),
-                                           (uint64_t)ntrims);
     const int row0 = P->early_rows == 7 ? 7 : 0, nrows = 9 - row0;
+    // (blocks per row: one 16-point group per thread up to PLK_CP_BX blocks)
+    const uint64_t bx = std::max<uint64_t>(std::min<uint64_t>(PLK_CP_BX, std::max<uint64_t>(1, ((nm >> 4) + CP_T - 1) / CP_T)),
+                                           (uint64_t)ntrims);
     hipLaunchKernelGGL(commit_pack_kernel, dim3((unsigned)bx, nrows + 1), dim3(CP_T), 0, P->st, P->d_srs_log, P->arena,
                        (uint64_t)P->cstride, nm, P->d_res, P->exp_words, row0, nrows, trims, ntrims, P->d_S, P->d_stat,
                        P->d_res_host, ++P->seq, P->d_done);
