@@ -418,6 +418,9 @@ constexpr int EV_ROWS = 24;  // grid rows: a long evaluation runs as several row
 #ifndef PLK_CP_BX
 #define PLK_CP_BX 227   // commit_pack_kernel: blocks per MSM row at most (2048 / 9)
 #endif
+#ifndef PLK_MSM_ROW_LENS
+#define PLK_MSM_ROW_LENS 1   // commitment MSMs over each row's own length (0: the arena stride's cmax)
+#endif
 #ifndef PLK_EV_BLOCKS
 #define PLK_EV_BLOCKS 64
 #endif
@@ -523,10 +526,16 @@ __device__ __forceinline__ void eval_row_block(const EvArgs& a, int e, uint32_t 
 // (optional) commitments that do not wait for round 5, run as extra grid rows of an earlier launch
 // (round 5's scan, or round 4's evaluations): rows y >= nd are log-form MSMs of arena rows
 // 0 .. nrows - 1 on X blocks each
+// points per commitment row: each row's own upper-bound length (the arena row is zero past it),
+// not the arena's stride -- w_z(x)'s quotient is ~2n long, the other eight ~n
+struct MsmRowLens {
+  uint64_t n[9];
+};
 struct EarlyMsm {
   const uint8_t* logs;
   const uint8_t* arena;
-  uint64_t cstride, n;
+  uint64_t cstride;
+  MsmRowLens rl;
   PlkMsmResult* res;
   const uint32_t* exp_words;
   int nrows, nd;
@@ -539,7 +548,7 @@ __global__ __launch_bounds__(256) void eval_kernel(EvArgs a, uint8_t* __restrict
     __shared__ uint32_t wsum[256 / PLK_WAVE];
     __shared__ uint32_t wbad[256 / PLK_WAVE];
     const int r = (int)blockIdx.y - a.nr;
-    (void)msm_log_block<256>(em.logs, em.arena + (uint64_t)r * em.cstride, em.n, blockIdx.x, gridDim.x, (uint32_t)r,
+    (void)msm_log_block<256>(em.logs, em.arena + (uint64_t)r * em.cstride, em.rl.n[r], blockIdx.x, gridDim.x, (uint32_t)r,
                              em.res + r, em.exp_words, etab, wsum, wbad);
     return;
   }
@@ -897,7 +906,7 @@ __global__ __launch_bounds__(SCAN_T) void lincomb_scan_kernel(LcBatch b, LinDivs
     __shared__ uint32_t wbad[SCAN_T / PLK_WAVE];
     const int r = (int)blockIdx.y - em.nd;
     if (blockIdx.x >= em.X) return;
-    (void)msm_log_block<SCAN_T>(em.logs, em.arena + (uint64_t)r * em.cstride, em.n, blockIdx.x, em.X, (uint32_t)r,
+    (void)msm_log_block<SCAN_T>(em.logs, em.arena + (uint64_t)r * em.cstride, em.rl.n[r], blockIdx.x, em.X, (uint32_t)r,
                                 em.res + r, em.exp_words, etab, wsum, wbad);
     return;
   }
@@ -1308,7 +1317,7 @@ __global__ __launch_bounds__(PACK_T) void trim_pack_kernel(TrimArgs a, int nt, c
 // trim_pack_kernel does -- its launch and its scan latency leave the proof's tail.
 constexpr int CP_T = 256;
 __global__ __launch_bounds__(CP_T) void commit_pack_kernel(const uint8_t* __restrict__ logs, const uint8_t* arena,
-                                                           uint64_t cstride, uint64_t n, PlkMsmResult* res,
+                                                           uint64_t cstride, MsmRowLens rl, PlkMsmResult* res,
                                                            const uint32_t* __restrict__ exp_words, int row0, int nrows,
                                                            TrimArgs a, int nt, const uint8_t* __restrict__ S,
                                                            uint32_t* stat, uint8_t* __restrict__ host, uint32_t seq,
@@ -1319,7 +1328,7 @@ __global__ __launch_bounds__(CP_T) void commit_pack_kernel(const uint8_t* __rest
   bool arrive = false;
   if ((int)blockIdx.y < nrows) {   // arena row / record row0 + y
     const int r = row0 + (int)blockIdx.y;
-    arrive = msm_log_block<CP_T>(logs, arena + (uint64_t)r * cstride, n, blockIdx.x, gridDim.x, (uint32_t)r, res + r,
+    arrive = msm_log_block<CP_T>(logs, arena + (uint64_t)r * cstride, rl.n[r], blockIdx.x, gridDim.x, (uint32_t)r, res + r,
                                  exp_words, etab, wsum, wbad);
   } else {
     const int x = (int)blockIdx.x;
@@ -2013,6 +2022,18 @@ struct RoundsMode {
   uint8_t *o2 = nullptr, *o3 = nullptr;
 };
 
+// the 9 commitment rows' MSM lengths: a b c z t_lo t_mid t_hi w_z w_zw (the arena rows' order),
+// each its polynomial's upper-bound length (P->cmax's terms), at most the SRS length
+MsmRowLens msm_row_lens(const plk_prover* P, const Lens& L) {
+  const uint64_t part = L.n + 2, lthi = L.ltx > 2 * part ? L.ltx - 2 * part : 1;
+  const uint64_t len[9] = {L.la, L.la, L.la, L.lzx, part, part, lthi, L.lwq, L.lwo};
+  MsmRowLens r{};
+  for (int i = 0; i < 9; i++)
+    r.n[i] = PLK_MSM_ROW_LENS ? std::min<uint64_t>(std::min<uint64_t>(len[i], P->cmax), P->srs_len)
+                              : std::min<uint64_t>(P->cmax, P->srs_len);
+  return r;
+}
+
 int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const uint8_t rnd[9], bool pre = false,
            const RoundsMode& md = RoundsMode{}) {
   const uint64_t n = P->n;
@@ -2250,8 +2271,8 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   const int64_t early = !P->srs_irregular && plk_opt(PLK_OPT_PROVE_SRS_LOGS) && plk_opt(PLK_OPT_PROVE_PACK_FUSE)
                             ? plk_opt(PLK_OPT_PROVE_EARLY_COMMITS)
                             : 0;
-  const EarlyMsm em{P->d_srs_log, P->arena, (uint64_t)P->cstride, std::min<uint64_t>(P->cmax, P->srs_len), P->d_res,
-                    P->exp_words, 7, 0, (uint32_t)(2048 / 9)};
+  const MsmRowLens rl = msm_row_lens(P, L);
+  const EarlyMsm em{P->d_srs_log, P->arena, (uint64_t)P->cstride, rl, P->d_res, P->exp_words, 7, 0, (uint32_t)(2048 / 9)};
   RC(evals(P, {{cA, L.la, S_Z, S_AZ}, {cB, L.la, S_Z, S_BZ}, {cC, L.la, S_Z, S_CZ}, {S1, n, S_Z, S_S1Z},
                {S2, n, S_Z, S_S2Z}, {P->TX, L.ltx, S_Z, S_TZ}, {P->ZW, L.lzw, S_Z, S_ZWZ}, {L1, n, S_Z, S_L1Z},
                {QM, n, S_Z, S_QMZ}, {QL, n, S_Z, S_QLZ}, {QR, n, S_Z, S_QRZ}, {QO, n, S_Z, S_QOZ},
@@ -2304,7 +2325,7 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     const uint64_t bx = std::max<uint64_t>(std::min<uint64_t>(PLK_CP_BX, std::max<uint64_t>(1, ((nm >> 4) + CP_T - 1) / CP_T)),
                                            (uint64_t)ntrims);
     hipLaunchKernelGGL(commit_pack_kernel, dim3((unsigned)bx, nrows + 1), dim3(CP_T), 0, P->st, P->d_srs_log, P->arena,
-                       (uint64_t)P->cstride, nm, P->d_res, P->exp_words, row0, nrows, trims, ntrims, P->d_S, P->d_stat,
+                       (uint64_t)P->cstride, msm_row_lens(P, L), P->d_res, P->exp_words, row0, nrows, trims, ntrims, P->d_S, P->d_stat,
                        P->d_res_host, ++P->seq, P->d_done);
     PLK_HIP(hipGetLastError());
     PLK_MARK(7);
