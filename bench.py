@@ -36,6 +36,9 @@ sys.path.insert(0, os.path.join(ROOT, "plonk.c_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
 MSM_BYTES_PER_POINT = 4  # 3 B G1 + 1 B HF read once
 NTT_BYTES_PER_ELEM = 8   # u32 read + write once
+# the MSM kernel's translation unit and every header it includes (tests/test_lint_cpu.py checks the
+# list against the #include lines): a committed PMC record is valid only for these bytes
+MSM_SOURCES = ("msm.hip", "plk_device.h", "plk_internal.h", "plk_msm_finish.h")
 
 
 def roofline_obj(alg_bytes, ms, what):
@@ -47,7 +50,10 @@ def roofline_obj(alg_bytes, ms, what):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks, one process per GPU).  Under a launcher (WORLD_SIZE set) it must equal "
+                         "WORLD_SIZE; without one, N > 1 starts `python -m torch.distributed.run --nproc-per-node N` "
+                         "on this script as a child process and exits with its status")
     ap.add_argument("--steps", type=int, default=200,
                     help="timed steps; a step is ONE batched launch of --msm-batch MSMs over distinct input sets")
     ap.add_argument("--warmup", type=int, default=3)
@@ -187,7 +193,7 @@ def kernel_source_hash():
     """SHA-256 (16 hex) of the MSM kernel's sources: a PMC record is used only for this code."""
     import hashlib
     h = hashlib.sha256()
-    for f in ("msm.hip", "plk_device.h", "plk_internal.h"):
+    for f in MSM_SOURCES:
         with open(os.path.join(ROOT, "plonk.c_amd", "csrc", f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
@@ -792,20 +798,64 @@ def prove_split_component(torch, hip, dev, dist, rank, world, gloo, log2n=20, re
                     "barrier; single_gpu_ms = rank 0 alone on the same instance"}
 
 
+def rank_launch_cmd(argv, n, port):
+    """the child command that runs this bench as n ranks on this node (torch.distributed.run, one
+    process per GPU, rendezvous on 127.0.0.1): the same arguments, so every rank parses the same
+    --gpus n and finds WORLD_SIZE = n"""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def world_from_args(args, env):
+    """(world, launch): the rank count this process belongs to, and whether it must first start
+    the ranks itself.  Decided before anything imports torch or touches a GPU: a launcher's
+    WORLD_SIZE that disagrees with --gpus is an error (the line would claim the wrong n_gpus)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        world = int(ws)
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%d ranks" % (args.gpus, world))
+        return world, False
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1 (got %d)" % n)
+    return n, n > 1
+
+
+def launch_ranks(n):
+    """start n ranks of this bench as a CHILD process (no exec: nothing here has touched the GPU,
+    and the child initialises it itself); rank 0's JSON line reaches our stdout through the
+    inherited stream; returns the child's exit status"""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(rank_launch_cmd(sys.argv[1:], n, port), env=env).returncode
+
+
 def main():
     args = parse()
+    world, spawn = world_from_args(args, os.environ)
+    if spawn:
+        sys.exit(launch_ranks(world))
     import torch
     import torch.distributed as dist
 
     import plonkhip as hip
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; PLK_DIST_BACKEND=gloo (and more ranks than GPUs) only to rehearse
     # the multi-rank path on a one-GPU box -- the driver's runs use RCCL ("nccl")
     backend = os.environ.get("PLK_DIST_BACKEND", "nccl")
-    gpu = local % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()         # (counting devices does not initialise the GPU)
+    if backend == "nccl" and world > max(1, ndev):
+        raise SystemExit("bench.py: %d ranks over RCCL need %d GPUs, %d visible (PLK_DIST_BACKEND=gloo rehearses "
+                         "more ranks than GPUs)" % (world, world, ndev))
+    gpu = local % max(1, ndev)
     torch.cuda.set_device(gpu)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -54,3 +54,47 @@ def test_guard_defeats_the_combine():
                          text=True, timeout=300, check=True).stdout.split("\n")
     res = dict(l.split(" ", 1) for l in out if l.strip())
     assert res["swar_guarded"] == "dot4=0 mask=4", out
+
+
+def _local_includes(path):
+    """the csrc-relative names a source file pulls in with #include "..." (transitively)"""
+    seen, todo = set(), [path]
+    while todo:
+        with open(os.path.join(CSRC, todo.pop())) as f:
+            for line in f:
+                m = re.match(r'\s*#\s*include\s+"([^"]+)"', line)
+                if m:
+                    name = os.path.normpath(m.group(1))
+                    if name not in seen:
+                        seen.add(name)
+                        if os.path.exists(os.path.join(CSRC, name)) and not name.startswith(".."):
+                            todo.append(name)
+    return seen
+
+
+def test_makefile_hdr_lists_every_local_include():
+    """an edit to any header a kernel includes must rebuild its object (round 4 missed
+    plk_msm_finish.h: msm.o / prove.o went stale on a finish-code edit)"""
+    with open(os.path.join(ROOT, "plonk.c_amd", "Makefile")) as f:
+        mk = f.read()
+    hdr = re.search(r"^HDR\s*:=\s*(.*)$", mk, re.M).group(1).split()
+    hdr = {os.path.normpath(h[len("csrc/"):]) if h.startswith("csrc/") else os.path.normpath(os.path.join("..", h))
+           for h in hdr}
+    missing = []
+    for name in sorted(os.listdir(CSRC)):
+        if name.endswith((".hip", ".h")):
+            for inc in _local_includes(name):
+                if inc not in hdr:
+                    missing.append("%s includes %s" % (name, inc))
+    assert not missing, "plonk.c_amd/Makefile HDR misses:\n" + "\n".join(missing)
+
+
+def test_pmc_hash_covers_msm_headers():
+    """bench.py's kernel_source_hash (which invalidates the committed PMC traffic record) must
+    cover every csrc header msm.hip includes"""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    want = {"msm.hip"} | {i for i in _local_includes("msm.hip") if not i.startswith("..")}
+    assert want <= set(bench.MSM_SOURCES), sorted(want - set(bench.MSM_SOURCES))
