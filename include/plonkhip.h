@@ -94,7 +94,10 @@ enum {
   PLK_OPT_PROVE_EARLY_COMMITS = 24, /* 1 (with PROVE_PACK_FUSE): the 7 commitments that do not wait for round 5
                                        run as extra rows of round 5's scan launch; 2: of round 4's evaluation
                                        launch */
-  PLK_OPT_COUNT = 25
+  PLK_OPT_PROVE_HELPER_COPY = 25, /* 1: helpers of plk_prover_attach_helpers on the proving device itself take
+                                     the distinct-device input path (their inputs copied into their own rows,
+                                     the rest pointed at a poison row): a one-GPU test of that branch */
+  PLK_OPT_COUNT = 26
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
 /* Diagnostics for the offline roofline tools: with PLK_OPT_NTT_LAUNCH_LOG = 1 every NTT pass launch

@@ -391,6 +391,15 @@ int init_locked(int device) {
     // on several host threads
     rc = nlist > 1 ? plk_shards_setup(list, nlist, s_ytab, s_exp4, s_inv, false) : setup_lanes(device);
     (void)hipSetDevice(device);
+    if (rc && nlist <= 1) {
+      // host lanes are an optimisation of the one-device call: if they cannot be set up (e.g. the
+      // pinned staging is refused) the library runs without them instead of failing;
+      // the reason stays readable through plk_last_error until the next error
+      const std::string why = g_err;
+      plk_shards_teardown();
+      plk_set_error("plk_init: host lanes unavailable, single-lane plk_msm_g1 (%s)", why.c_str());
+      rc = PLK_OK;
+    }
     if (rc) {
       const std::string why = g_err;
       plk_shards_teardown();
@@ -470,6 +479,7 @@ const OptDef kOpt[PLK_OPT_COUNT] = {
     {1, 0, 1, false},                          // PROVE_SRS_LOGS
     {1, 0, 1, false},                          // PROVE_PACK_FUSE
     {1, 0, 2, false},                          // PROVE_EARLY_COMMITS (2: in round 4's evaluation launch)
+    {0, 0, 1, false},                          // PROVE_HELPER_COPY (tests: the distinct-device input path on one GPU)
 };
 struct Opts {
   std::atomic<int64_t> v[PLK_OPT_COUNT];

@@ -1823,12 +1823,26 @@ int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs, const Lc
   return PLK_OK;
 }
 
+#if PLK_DIAG_DROP_HANDOFF & 1
+// diagnostic build only: holds its stream for `ticks` of the 100 MHz wall clock
+__global__ void diag_spin_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+#endif
+
 // restores the calling thread's current device on scope exit
 struct DevGuard {
   int prev;
   DevGuard() : prev(plk_cur_device()) {}
   ~DevGuard() { (void)hipSetDevice(prev); }
 };
+// a prover's work runs on ITS device whatever the calling thread's current device is: its stream
+// and buffers live there, and the launches look up the NTT / MSM tables by the current device
+// (ADVICE r4); the caller's device is restored on return
+#define PROVER_ON_DEVICE(P) \
+  DevGuard dg_;             \
+  PLK_HIP(hipSetDevice((P)->dev))
 
 // plk_prover_create on device `dev` (the library's primary, or a helper's GPU whose tables
 // plk_ctx_prepare_device built); the caller's current device is restored
@@ -2450,15 +2464,23 @@ int rounds_split(plk_prover* P, const uint8_t* const* pl, const uint8_t* const* 
     }
     const uint8_t* hp[13];
     for (int i = 0; i < 13; i++) hp[i] = hpl ? hpl[13 * (h + 1) + i] : pl[i];
-    if (!hpl && H->dev != P->dev) {   // the inputs it reads, from the proving device
+    // another GPU (or PLK_OPT_PROVE_HELPER_COPY, which runs this branch on the proving device so
+    // that a one-GPU box executes it): the 7 inputs the chains read are copied to the helper's
+    // buffers, and the 6 it must not read point at the helper's poison row (0x05 bytes, set at
+    // attach) -- never at the proving GPU's memory; a read of one changes the proof
+    if (!hpl && (H->dev != P->dev || plk_opt(PLK_OPT_PROVE_HELPER_COPY))) {
       const size_t st = hin_stride(P->n);
+      for (int i = 0; i < 13; i++) hp[i] = H->hin + 7 * st;
       for (int q = 0; q < 7 && !rc; q++) {
         uint8_t* dst = H->hin + q * st;
+        hp[HELPER_IN[q]] = dst;
+#if PLK_DIAG_DROP_HANDOFF & 4   // diagnostic build only (tests/test_prove_helpers_gpu.py): f_a not copied
+        if (q == 0) continue;
+#endif
         if (hipMemcpyPeerAsync(dst, H->dev, pl[HELPER_IN[q]], P->dev, P->n, H->st) != hipSuccess) {
           plk_set_error("split proof: input copy to device %d failed", H->dev);
           rc = PLK_ERR_HIP;
         }
-        hp[HELPER_IN[q]] = dst;
       }
       if (rc) break;
     }
@@ -2505,6 +2527,7 @@ int plk_prover_rounds_dev(plk_prover_t* P, const uint8_t* const d_polys[13], con
   for (int i = 0; i < 13; i++)
     if (!d_polys[i]) { plk_set_error("plk_prover_rounds_dev: polynomial %d is NULL", i); return PLK_ERR_ARG; }
   const bool pre = (flags & PLK_PROVE_PREPROCESSED) != 0;
+  PROVER_ON_DEVICE(P);
   int rc = P->nhelp ? rounds_split(P, d_polys, nullptr, chal, rand9, pre) : rounds(P, d_polys, chal, rand9, pre);
   if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
   return finish(P, (flags & PLK_PROVE_STRICT) != 0, 0, proof);
@@ -2545,19 +2568,26 @@ int plk_prover_attach_helpers(plk_prover_t* P, int k) {
     if ((rc = create_on(&d, ids[1 + h], &H))) break;
     P->help[P->nhelp] = H;
     P->help_mask[P->nhelp++] = masks[k - 1][h];
+    DevGuard dg;
     if (H->dev != P->dev) {
-      DevGuard dg;
       int can = 0;   // direct xGMI access both ways where the devices allow it (else staged copies)
       if (hipDeviceCanAccessPeer(&can, H->dev, P->dev) == hipSuccess && can && hipSetDevice(H->dev) == hipSuccess)
         (void)hipDeviceEnablePeerAccess(P->dev, 0);
       if (hipDeviceCanAccessPeer(&can, P->dev, H->dev) == hipSuccess && can && hipSetDevice(P->dev) == hipSuccess)
         (void)hipDeviceEnablePeerAccess(H->dev, 0);
       (void)hipGetLastError();   // (already enabled is not an error here)
-      if (hipSetDevice(H->dev) != hipSuccess || hipMalloc((void**)&H->hin, 7 * hin_stride(P->n)) != hipSuccess) {
-        H->hin = nullptr;
-        plk_set_error("plk_prover_attach_helpers: input buffers on device %d", H->dev);
-        rc = PLK_ERR_NOMEM;
-      }
+    }
+    // the helper's input rows: 7 copies of what its chains read + 1 poison row (rounds_split);
+    // every byte starts as poison, so an input that is not copied is read as poison, not as stale
+    // bytes of an earlier proof (on the same device too: PLK_OPT_PROVE_HELPER_COPY)
+    const size_t hb = 8 * hin_stride(P->n);
+    if (hipSetDevice(H->dev) != hipSuccess || hipMalloc((void**)&H->hin, hb) != hipSuccess) {
+      H->hin = nullptr;
+      plk_set_error("plk_prover_attach_helpers: input buffers on device %d", H->dev);
+      rc = PLK_ERR_NOMEM;
+    } else if (hipMemset(H->hin, 0x05, hb) != hipSuccess) {
+      plk_set_error("plk_prover_attach_helpers: input buffers on device %d", H->dev);
+      rc = PLK_ERR_HIP;
     }
   }
   if (!rc) {
@@ -2591,6 +2621,7 @@ int plk_prover_rounds_multi_dev(plk_prover_t* P, const uint8_t* const* d_polys, 
   for (int i = 0; i < 13 * ndev; i++)
     if (!d_polys[i]) { plk_set_error("plk_prover_rounds_multi_dev: polynomial %d of set %d is NULL", i % 13, i / 13); return PLK_ERR_ARG; }
   const bool pre = (flags & PLK_PROVE_PREPROCESSED) != 0;
+  PROVER_ON_DEVICE(P);
   int rc = P->nhelp ? rounds_split(P, d_polys, d_polys, chal, rand9, pre) : rounds(P, d_polys, chal, rand9, pre);
   if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
   return finish(P, (flags & PLK_PROVE_STRICT) != 0, 0, proof);
@@ -2629,9 +2660,18 @@ int plk_prover_chains_dev(plk_prover_t* P, const uint8_t* const d_polys[13], con
   int rc = check_chain_args("plk_prover_chains_dev", P, d_polys, chal, rand9, which, d_t2, d_t3);
   if (rc) return rc;
   if (!which) return PLK_OK;
+  PROVER_ON_DEVICE(P);
   // write-after-read: the previous call's d_t2 / d_t3 may still be read by work on `done` (e.g.
   // an RCCL send of the last products): this call's products are written only after it
   if ((rc = stream_after(P->st, (hipStream_t)done, P->ev))) return rc;
+#if PLK_DIAG_DROP_HANDOFF & 1
+  // diagnostic build: the products are poisoned first and written ~20 ms later, so a consumer
+  // with no ordering behind this call reads poison however the streams are scheduled in time
+  if (d_t2) PLK_HIP(hipMemsetAsync(d_t2, 0x05, plk_prover_chain_bytes(P, PLK_CHAIN_T2), P->st));
+  if (d_t3) PLK_HIP(hipMemsetAsync(d_t3, 0x05, plk_prover_chain_bytes(P, PLK_CHAIN_T3), P->st));
+  hipLaunchKernelGGL(diag_spin_kernel, dim3(1), dim3(64), 0, P->st, 2000000ull);
+  PLK_HIP(hipGetLastError());
+#endif
   RoundsMode md;
   md.only = which;
   md.o2 = d_t2;
@@ -2649,6 +2689,7 @@ int plk_prover_rounds_ext_dev(plk_prover_t* P, const uint8_t* const d_polys[13],
                               void* ready, uint8_t proof[34]) {
   int rc = check_chain_args("plk_prover_rounds_ext_dev", P, d_polys, chal, rand9, which, d_t2, d_t3);
   if (rc) return rc;
+  PROVER_ON_DEVICE(P);
   RoundsMode md;
   md.ext = which;
   md.t2 = d_t2;
@@ -2664,6 +2705,7 @@ int plk_prover_rounds_ext_dev(plk_prover_t* P, const uint8_t* const d_polys[13],
 
 int plk_prover_preprocess(plk_prover_t* P, const uint8_t* const d_polys[13]) {
   if (!P) { plk_set_error("plk_prover_preprocess: NULL prover"); return PLK_ERR_ARG; }
+  PROVER_ON_DEVICE(P);
   PLK_HIP(hipStreamSynchronize(P->st));   // (no round may still read the old transforms)
   for (auto& f : P->fix) f = plk_prover::Fixed{};
   (void)hipFree(P->fix_mem);
@@ -2710,6 +2752,7 @@ int plk_prover_prove(plk_prover_t* P, const plk_circuit_t* c, const uint8_t chal
     plk_set_error("plk_prover_prove: prover created without h / k1_h / k2_h / h_pows_inv");
     return PLK_ERR_ARG;
   }
+  PROVER_ON_DEVICE(P);
   const uint64_t n = P->n;
   const uint8_t* parts[11] = {c->q_m, c->q_l, c->q_r, c->q_o, c->q_c, c->copy_a, c->copy_b, c->copy_c, c->a, c->b, c->c};
   for (int i = 0; i < 11; i++)

@@ -115,3 +115,156 @@ def test_attach_errors(hip, devlist):
     with pytest.raises(hip.PlonkHipError):
         pr.rounds_multi_dev([dev], chal, rnd)         # one input set for two devices
     pr.close()
+
+
+# ---- the distinct-device input path, executed on one GPU
+HELPER_IN = (0, 1, 2, 8, 9, 10, 11)      # f_a f_b f_c s_sigma_1..3 acc_x: what a helper's chains read
+
+
+@pytest.fixture
+def helper_copy(hip):
+    """PLK_OPT_PROVE_HELPER_COPY: helpers on the proving device take the distinct-device input
+    branch of rounds_split (inputs copied into their own rows, the other six entries pointed at a
+    poison row of 0x05 bytes) -- the branch an 8-GPU node runs"""
+    hip.set_option("PROVE_HELPER_COPY", 1)
+    yield
+    hip.set_option("PROVE_HELPER_COPY", 0)
+
+
+@pytest.mark.parametrize("k", [1, 2])
+@pytest.mark.parametrize("n,seed", [(1 << 12, 7), (5000, 7), (64, 3)])
+def test_helper_input_copy_branch(hip, devlist, helper_copy, k, n, seed):
+    devlist([0] * (1 + k))
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, seed, 2 * n + 8)
+    dev = _dev(polys)
+    single = hip.Prover(n, zh, pts)
+    want = single.rounds_dev(dev, chal, rnd)
+    pr = hip.Prover(n, zh, pts)
+    pr.attach_helpers(k)
+    for _ in range(2):
+        assert pr.rounds_dev(dev, chal, rnd).hex() == want.hex()
+    # new inputs in the same device buffers: the copies must carry them (not the first call's rows)
+    polys2, _, _, _, _ = gen.prove_instance(n, seed + 1, 2 * n + 8)
+    for d, p in zip(dev, polys2):
+        d.copy_(torch.from_numpy(p))
+    assert pr.rounds_dev(dev, chal, rnd).hex() == single.rounds_dev(dev, chal, rnd).hex()
+    pr.close()
+    single.close()
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_helper_input_copy_branch_2_20(hip, devlist, helper_copy, k):
+    """config C5 through the copy branch at 2 and 3 'devices': the recorded answer"""
+    g = load_golden("prove_2_20.json")
+    n = g["n"]
+    devlist([0] * (1 + k))
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, g["seed"], g["srs_len"])
+    pr = hip.Prover(n, zh, pts)
+    pr.attach_helpers(k)
+    assert pr.rounds_dev(_dev(polys), chal, rnd).hex() == g["proof"]
+    pr.close()
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_multi_dev_helpers_read_only_their_inputs(hip, devlist, k):
+    """plk_prover_rounds_multi_dev with every helper set's six entries outside HELPER_IN pointed
+    at poison (0x05 bytes): the proof is unchanged, i.e. a helper reads nothing else (the claim
+    rounds_split's copies rest on).  Control: poisoning one HELPER_IN entry changes the proof."""
+    n = 1 << 12
+    devlist([0] * (1 + k))
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, 9, 2 * n + 8)
+    dev = _dev(polys)
+    poison = torch.full((n + 64,), 5, dtype=torch.uint8, device="cuda")
+    pr = hip.Prover(n, zh, pts)
+    want = pr.rounds_dev(dev, chal, rnd)
+    pr.attach_helpers(k)
+    hsets = [[d if i in HELPER_IN else poison for i, d in enumerate(dev)] for _ in range(k)]
+    assert pr.rounds_multi_dev([dev] + hsets, chal, rnd).hex() == want.hex()
+    bad = [list(s) for s in hsets]
+    bad[-1][HELPER_IN[0]] = poison
+    assert pr.rounds_multi_dev([dev] + bad, chal, rnd).hex() != want.hex()
+    pr.close()
+
+
+_DROP_CHILD = r"""
+import sys
+sys.path[:0] = sys.argv[1:3]
+import torch, gen, plonkhip as hip
+hip.init(0)
+hip.set_option("PROVE_HELPER_COPY", 1)
+n = 1 << 12
+polys, chal, rnd, zh, pts = gen.prove_instance(n, 7, 2 * n + 8)
+dev = [torch.from_numpy(p).to("cuda") for p in polys]
+single = hip.Prover(n, zh, pts)
+want = single.rounds_dev(dev, chal, rnd).hex()
+for k in (1, 2):
+    hip.init_devices([0] * (1 + k))
+    pr = hip.Prover(n, zh, pts)
+    pr.attach_helpers(k)
+    try:
+        got = pr.rounds_dev(dev, chal, rnd).hex()
+    except hip.PlonkHipError as e:   # (wrong chain bytes can make the proof fail its checks)
+        got = "error-%d" % e.code
+    print(k, got, want)
+    pr.close()
+hip.init_devices([0])
+"""
+
+
+def test_skipped_input_copy_is_caught():
+    """a build whose copy branch skips one of the seven input copies (f_a; PLK_DIAG_DROP_HANDOFF = 4)
+    gives wrong proof bytes at 2 and 3 'devices': the helper then reads its poison row, so the test
+    above would catch a missing copy.  The real build, in the same child form, is exact."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = [os.path.join(root, "plonk.c_amd"), os.path.join(root, "tests", "golden")]
+
+    def run(lib):
+        r = subprocess.run([sys.executable, "-c", _DROP_CHILD, *paths], capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, PLK_LIB=lib))
+        assert r.returncode == 0, r.stderr[-2000:]
+        return [l.split() for l in r.stdout.splitlines() if l[:1] in "12"]
+
+    lib = os.path.join(root, "plonk.c_amd", "build", "diag", "libplonkhip_drop4.so")
+    assert os.path.exists(lib), "diagnostic build missing: make -C plonk.c_amd diag (__graft_entry__.build does)"
+    rows = run(lib)
+    assert len(rows) == 2
+    for k, got, want in rows:
+        assert got != want, "skipped input copy not caught with %s helper(s)" % k
+    rows = run(os.path.join(root, "plonk.c_amd", "libplonkhip.so"))
+    assert len(rows) == 2 and all(got == want for _, got, want in rows)
+
+
+def test_prover_calls_from_another_thread(hip):
+    """every prover entry point runs on the prover's own device whatever the calling thread's
+    current device (tables are looked up by the current device): calls from a fresh
+    thread -- and, with two or more GPUs, from a thread current on another device -- give the
+    same proof"""
+    import threading
+    n = 1 << 12
+    polys, chal, rnd, zh, pts = gen.prove_instance(n, 11, 2 * n + 8)
+    dev = _dev(polys)
+    pr = hip.Prover(n, zh, pts)
+    want = pr.rounds_dev(dev, chal, rnd)
+    other = 1 if torch.cuda.device_count() > 1 else 0
+    out = {}
+
+    def worker():
+        try:
+            torch.cuda.set_device(other)
+            out["plain"] = pr.rounds_dev(dev, chal, rnd)
+            pr.preprocess(dev)
+            out["pre"] = pr.rounds_dev(dev, chal, rnd, preprocessed=True)
+            out["dev_after"] = torch.cuda.current_device()
+        except Exception as e:   # noqa: BLE001 -- reported below
+            out["err"] = repr(e)
+
+    t = threading.Thread(target=worker)
+    t.start()
+    t.join(120)
+    assert "err" not in out, out.get("err")
+    assert out["plain"] == want and out["pre"] == want
+    assert out["dev_after"] == other              # the caller's device is restored
+    pr.close()
