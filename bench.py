@@ -1070,6 +1070,13 @@ def main():
                 "note": "8 MSMs per launch (the prover's commitments are 9 per launch)"}
         if world == 1 and "cpu" in comps and not args.no_cpu_baseline:
             comp["cpu_reference_other"] = cpu_other_baselines(hip)
+        if "msm" in comps and torch.cuda.device_count() > 1:
+            # the C-side split proof over DISTINCT GPUs (tools/devices_probe.py) is unverified until it
+            # has matched the recorded answer on a multi-GPU node: a missing or failed probe is a failed check
+            sp = ((comp.get("host_call_msm_2^22_devices") or {}).get("all_devices") or {}).get("prove_2^20_split_from_c")
+            legs = [v for k, v in (sp or {}).items() if k.startswith("gpus_")]
+            check["distinct_device_split_from_c_matches_golden"] = bool(legs) and all(
+                v.get("matches_golden") is True for v in legs)
     if rank == 0 and comp:
         line["components"] = comp
     if rank == 0:

@@ -97,7 +97,10 @@ enum {
   PLK_OPT_PROVE_HELPER_COPY = 25, /* 1: helpers of plk_prover_attach_helpers on the proving device itself take
                                      the distinct-device input path (their inputs copied into their own rows,
                                      the rest pointed at a poison row): a one-GPU test of that branch */
-  PLK_OPT_COUNT = 26
+  PLK_OPT_PROVE_EVAL_AGG = 26,   /* 1: round 4's evaluation rows also store round 5's scan-chunk aggregates, so
+                                    both round-5 divisions finish in ONE launch (lincomb_agg_divide_kernel);
+                                    0: the numerators + aggregates launch, then the apply launch */
+  PLK_OPT_COUNT = 27
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
 /* Diagnostics for the offline roofline tools: with PLK_OPT_NTT_LAUNCH_LOG = 1 every NTT pass launch

@@ -480,6 +480,7 @@ const OptDef kOpt[PLK_OPT_COUNT] = {
     {1, 0, 1, false},                          // PROVE_PACK_FUSE
     {1, 0, 2, false},                          // PROVE_EARLY_COMMITS (2: in round 4's evaluation launch)
     {0, 0, 1, false},                          // PROVE_HELPER_COPY (tests: the distinct-device input path on one GPU)
+    {1, 0, 1, false},                          // PROVE_EVAL_AGG
 };
 struct Opts {
   std::atomic<int64_t> v[PLK_OPT_COUNT];

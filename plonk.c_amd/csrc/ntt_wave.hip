@@ -61,6 +61,9 @@ namespace {
 #ifndef PLK_NTT_CENTER_SWZ
 #define PLK_NTT_CENTER_SWZ 0   // center exchanges: 0 padded (2, swizzled only where the padding conflicts, spills)
 #endif
+#ifndef PLK_NTT_CENTER_SWZ12
+#define PLK_NTT_CENTER_SWZ12 1 // ... the same for the 2^12-tile center (round 5: swizzled, with PLK_NTT_RC12 = 3)
+#endif
 #ifndef PLK_NTT_WRAP_INLINE
 #define PLK_NTT_WRAP_INLINE 1  // wrapped tops fixed at the end of the last inverse pass (0: wrap_fix_kernel launches)
 #endif
@@ -83,10 +86,19 @@ namespace {
 #ifndef PLK_NTT_XCH_REMAT
 #define PLK_NTT_XCH_REMAT 1    // swizzled exchange addresses recomputed per pass, not held across the array loop
 #endif
+#ifndef PLK_NTT_M17
+#define PLK_NTT_M17 1          // COLT byte outputs: 1 = mod 17 of the index through an LDS table, 0 = 24-bit arithmetic
+#endif
 #ifndef PLK_NTT_U8_KRSRC
 #define PLK_NTT_U8_KRSRC 0     // byte loads: one buffer resource per register index (one offset VGPR)
 #endif
-constexpr int wt_rc(int TB) { return TB == 13 ? PLK_NTT_RC13 : PLK_NTT_R12; }
+#ifndef PLK_NTT_RC12
+// register bits per thread of the 2^12-tile center kernel: 3 = 512 threads of 8 elements, 4 rounds of
+// 3 stages per transform (3 exchanges instead of 5); with the swizzled exchanges poly_mul 2^19 x 2^19
+// 24.95-25.44 -> 23.55-23.85 us (same box, alternating, tools/c3_lib_ab.sh; 2 = 1024 threads)
+#define PLK_NTT_RC12 3
+#endif
+constexpr int wt_rc(int TB) { return TB == 13 ? PLK_NTT_RC13 : PLK_NTT_RC12; }
 constexpr int wt_ntc(int TB) { return 1 << (TB - wt_rc(TB)); }
 // register bits per thread for a tile size; the block has 2^(TB-R) threads
 constexpr int wt_r(int TB) { return TB == 13 ? PLK_NTT_R13 : PLK_NTT_R12; }
@@ -96,6 +108,12 @@ constexpr int WT_MAX_HI13 = 10;                // ... with 2^13 tiles
 constexpr uint32_t M17_LUT = 1040;             // mod-17 table of the byte outputs (F::out17_idx < 1035)
 
 __device__ __forceinline__ int wphys(int e) { return e + (e >> 5); }
+// x mod 17 for x < M17_LUT with full-rate 24-bit multiplies: floor(x / 17) = (241 x) >> 12 there
+// (checked for every x < 1040), then x - 17 q as one v_mad_i32_i24
+__device__ __forceinline__ uint32_t mod17_small(uint32_t x) {
+  const uint32_t q = __umul24(x, 241u) >> 12;
+  return (uint32_t)(__mul24((int)q, -17) + (int)x);
+}
 
 // A tile's words (or bytes) through a buffer resource on its uniform base: every access is one
 // 32-bit VGPR offset against scalar registers (no 64-bit address per element; offsets stay below
@@ -893,8 +911,8 @@ __global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs job
   }
   load_pass_tw<M, G::NT>(Tsm, tw.small);
   // (COLT byte outputs) x mod 17 for x < M17_LUT, read at F::out17_idx
-  __shared__ uint8_t m17[TO_U8 && COLT ? M17_LUT : 1];
-  if constexpr (TO_U8 && COLT) {
+  __shared__ uint8_t m17[TO_U8 && COLT && PLK_NTT_M17 ? M17_LUT : 1];
+  if constexpr (TO_U8 && COLT && PLK_NTT_M17) {
     for (uint32_t i = tid; i < M17_LUT; i += G::NT) m17[i] = (uint8_t)(i % 17u);
   }
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, true);
@@ -950,7 +968,8 @@ __global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs job
 #pragma unroll
       for (int k = 0; k < G::E; k++) {
         jj[k] = (N - ((uint32_t)tb + G::template toff_k<G::NR - 1, true>(p, of, bf, k))) & (N - 1);
-        rr[k] = COLT ? (uint32_t)m17[F::out17_idx(v[k])] : F::out17(v[k], ninv);
+        rr[k] = !COLT ? F::out17(v[k], ninv)
+                : PLK_NTT_M17 ? (uint32_t)m17[F::out17_idx(v[k])] : mod17_small(F::out17_idx(v[k]));
       }
 #pragma unroll
       for (int k = 0; k < G::E; k++) bo.stb(jj[k], rr[k]);
@@ -1103,11 +1122,11 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
       // stored this pass's output registers where their inputs were read -- so its pass is
       // skipped; xc counts the exchanges so that double buffers keep alternating)
       if (!P.afix) {
-        G::template pass<false, PLK_NTT_CENTER_SWZ>(va, tid, bufs, xc, Tf);
+        G::template pass<false, TB == 13 ? PLK_NTT_CENTER_SWZ : PLK_NTT_CENTER_SWZ12>(va, tid, bufs, xc, Tf);
         xc += G::XCH;
       }
       if (!P.bfix) {
-        G::template pass<false, PLK_NTT_CENTER_SWZ>(vb, tid, bufs, xc, Tf);
+        G::template pass<false, TB == 13 ? PLK_NTT_CENTER_SWZ : PLK_NTT_CENTER_SWZ12>(vb, tid, bufs, xc, Tf);
         xc += G::XCH;
       }
 #pragma unroll
@@ -1133,7 +1152,7 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
         for (int k = 0; k < G::E; k++) pa[k] = b_n.ld(b0, (uint32_t)k << L0);
       }
     }
-    G::template pass<true, PLK_NTT_CENTER_SWZ>(va, tid, bufs, xc, Tf);
+    G::template pass<true, TB == 13 ? PLK_NTT_CENTER_SWZ : PLK_NTT_CENTER_SWZ12>(va, tid, bufs, xc, Tf);
 #pragma unroll
     for (int k = 0; k < G::E; k++) b_c.st(bf, (uint32_t)k << LF, va[k]);
   }

@@ -426,6 +426,7 @@ constexpr int EV_ROWS = 24;  // grid rows: a long evaluation runs as several row
 #endif
 constexpr int EV_BLOCKS = PLK_EV_BLOCKS;   // x 256 threads x 4 uint4 loads in flight each
 constexpr int TICK_STRIDE = 32;   // one 128-byte line per arrival word
+constexpr int AGG_CHUNK = 4096;   // round 5's scan chunk (SCAN_B) as aggregated by the evaluation rows
 enum EvPost : int { EV_POST_NONE = 0, EV_POST_ACC = 1, EV_POST_R4 = 4 };
 struct EvArgs {
   const uint8_t* p[EV_ROWS];
@@ -438,6 +439,15 @@ struct EvArgs {
   int grp[EV_ROWS];
   int parts[EV_ROWS];
   int first[EV_ROWS];   // off == 0 (the row that holds p[0])
+  // the row's partial enters its evaluation times x^mexp (a slice of a longer polynomial whose offset
+  // is not 0 mod 16: t(x) from t_lo / t_mid / t_hi)
+  int mexp[EV_ROWS];
+  // chunk aggregates for round 5's divisions (PLK_OPT_PROVE_EVAL_AGG): col >= 0 stores, for every
+  // 4096-coefficient chunk c of the row's polynomial, sum_{i in c} p[i] x^i mod 17 at
+  // agg[16 (coff + c) + col] (coff: the row's first chunk, a split row's offset / 4096)
+  int col[EV_ROWS];
+  int coff[EV_ROWS];
+  uint8_t* agg;
   int ne;               // evaluations (the top ticket counts them)
   int nr;               // rows
   int post;             // scalar program the last block runs (EvPost)
@@ -462,6 +472,31 @@ __device__ __forceinline__ void eval_row_block(const EvArgs& a, int e, uint32_t 
   const uint64_t stride = (uint64_t)BX * blockDim.x * 16;
   if (x == 0) {                       // poly_eval(p, 0) = p[0]
     if (gid == 0 && n && a.first[e]) acc = p[0];
+  } else if (a.col[e] >= 0) {
+    // a wave per 4096-coefficient chunk (4 x 1 KiB loads in flight per lane), so the chunk's sum is
+    // one wave reduction: it is stored as round 5's scan aggregate and added into the evaluation.
+    // (make_evargs: such rows are readable in whole 16-byte chunks, split at multiples of 4096)
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t nch = (n + AGG_CHUNK - 1) / AGG_CHUNK;
+    for (uint64_t c = (uint64_t)bx * (blockDim.x >> 6) + wv; c < nch; c += (uint64_t)BX * (blockDim.x >> 6)) {
+      uint32_t w[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) load16_masked(p, n, c * AGG_CHUNK + u * 1024 + lane * 16, w[u]);
+      uint32_t s = 0;
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+#pragma unroll
+        for (int k = 0; k < 16; k++) s += pw[k] * ((w[u][k >> 2] >> (8 * (k & 3))) & 0xFFu);   // (<= 64 x 16 x 255)
+      s %= HFP;
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);   // (<= 64 x 16)
+      if (lane == 0) {
+        s = hmod(s);
+        a.agg[16 * ((uint64_t)a.coff[e] + c) + a.col[e]] = (uint8_t)s;
+        acc += s;
+      }
+    }
+    acc = hmod(acc);
   } else if (a.vec[e] == 2) {         // readable in whole chunks: 4 loads in flight per thread
     for (uint64_t i0 = gid * 16; i0 < n; i0 += 4 * stride) {
       uint32_t w[4][4];
@@ -501,7 +536,7 @@ __device__ __forceinline__ void eval_row_block(const EvArgs& a, int e, uint32_t 
   if (threadIdx.x != 0) return;
   // the partial travels inside the atomic (no fence: a device-scope release per block costs an
   // L2 writeback each, 2048 of them took 60 us): row word = sum | arrivals << 32
-  const uint32_t mine = (red[0] + red[1] + red[2] + red[3]) % HFP;
+  const uint32_t mine = (red[0] + red[1] + red[2] + red[3]) % HFP * pw[a.mexp[e]] % HFP;
   unsigned long long* row = reinterpret_cast<unsigned long long*>(tick) + a.grp[e] * (TICK_STRIDE / 2);
   const unsigned long long old = atomicAdd(row, (unsigned long long)mine | (1ull << 32));
   if ((uint32_t)(old >> 32) != BX * (uint32_t)a.parts[e] - 1) return;
@@ -799,6 +834,7 @@ __global__ __launch_bounds__(256) void numdiv_kernel(LcArgs a, const uint8_t* __
 // The prover only divides by x - z and x - z omega (d1 = 1).  Two-phase suffix scan over
 // 4096-element blocks: block aggregates, then each block reduces the aggregates after it itself.
 constexpr int SCAN_T = 256, SCAN_E = 16, SCAN_B = SCAN_T * SCAN_E;
+static_assert(SCAN_B == AGG_CHUNK, "the evaluation rows' chunk aggregates are the scan's");
 // Round 5's two divisions (by x - z and by x - z omega) are independent: one launch per phase
 // for both (blockIdx.y / the carry block = the division).
 struct LinDiv {
@@ -848,28 +884,55 @@ struct LinDivs {
 // bytes 0 / 2 and 1 / 3 as two 16-bit lanes (w & 0x00FF00FF, (w >> 8) & 0x00FF00FF) times cf[t] by
 // one 24-bit multiply each -- 16 x 16 x 255 + 32 < 2^16, so no lane carries into the next -- half
 // the multiplies and extracts of a per-byte loop.
-__device__ __forceinline__ void lc16_swar(const LcArgs& a, const uint32_t (&cf)[LC_MAX], uint32_t c0, uint32_t c1,
-                                          uint64_t i, uint32_t (&acc)[16]) {
-  uint32_t E[4] = {i == 0 ? c0 : 0u, 0u, 0u, 0u}, O[4] = {i == 0 ? c1 : 0u, 0u, 0u, 0u};   // even / odd bytes
+// p readable in whole 4 NW-byte chunks up to len (aligned to them): one unconditional load at a
+// clamped address, bytes past len masked (load16_masked for NW = 4)
+template <int NW>
+__device__ __forceinline__ void loadw_masked(const uint8_t* p, uint64_t len, uint64_t i, uint32_t (&w)[NW]) {
+  const bool in = i < len;
+  uint32_t v[NW];
+  if constexpr (NW == 4) {
+    const uint4 q = *reinterpret_cast<const uint4*>(p + (in ? i : 0));
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+    static_assert(NW == 2, "8 or 16 bytes");
+    const uint2 q = *reinterpret_cast<const uint2*>(p + (in ? i : 0));
+    v[0] = q.x; v[1] = q.y;
+  }
+#pragma unroll
+  for (int k = 0; k < NW; k++) {
+    const int64_t cnt = in ? (int64_t)len - (int64_t)(i + 4 * k) : 0;   // valid bytes in word k
+    w[k] = cnt >= 4 ? v[k] : (cnt <= 0 ? 0u : v[k] & ((1u << (8 * cnt)) - 1u));
+  }
+}
+template <int NW>
+__device__ __forceinline__ void lc_swar(const LcArgs& a, const uint32_t (&cf)[LC_MAX], uint32_t c0, uint32_t c1,
+                                        uint64_t i, uint32_t (&acc)[4 * NW]) {
+  uint32_t E[NW] = {}, O[NW] = {};   // even / odd bytes
+  E[0] = i == 0 ? c0 : 0u;
+  O[0] = i == 0 ? c1 : 0u;
 #pragma unroll
   for (int t = 0; t < LC_MAX; t++) {
     if (t < a.nt) {   // uniform
-      uint32_t w[4];
-      load16_masked(a.p[t], a.len[t], i, w);
+      uint32_t w[NW];
+      loadw_masked<NW>(a.p[t], a.len[t], i, w);
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
+      for (int q = 0; q < NW; q++) {
         E[q] += __umul24(cf[t], lanes02(w[q]));
         O[q] += __umul24(cf[t], lanes13(w[q]));
       }
     }
   }
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
+  for (int q = 0; q < NW; q++) {
     acc[4 * q] = E[q] & 0xFFFFu;
     acc[4 * q + 1] = O[q] & 0xFFFFu;
     acc[4 * q + 2] = E[q] >> 16;
     acc[4 * q + 3] = O[q] >> 16;
   }
+}
+__device__ __forceinline__ void lc16_swar(const LcArgs& a, const uint32_t (&cf)[LC_MAX], uint32_t c0, uint32_t c1,
+                                          uint64_t i, uint32_t (&acc)[16]) {
+  lc_swar<4>(a, cf, c0, c1, i, acc);
 }
 
 __global__ __launch_bounds__(SCAN_T) void lin_scan_sums_kernel(LinDivs L, const uint8_t* __restrict__ S) {
@@ -1013,6 +1076,90 @@ __global__ __launch_bounds__(SCAN_T) void lin_scan_apply_kernel(LinDivs L, const
   }
 }
 
+// The quotient bytes of one 4096-coefficient chunk of a division by x - av, from the chunk's
+// numerator bytes (nb8: this thread's E, packed), the thread's powers pt[k] = av^(base + k) and
+// ipt[k] = av^-(base + k + 1) (exponents mod 16), and the carry (this thread's part of the sum of
+// every later chunk's aggregate, < 17) -- lin_scan_apply_kernel's work on packed coefficients,
+// shared by the one-launch divisions.  T threads of E coefficients each: T E = 4096.
+template <int T, int E>
+__device__ __forceinline__ void lin_div_finish(const LcArgs& a, const LinDiv& D, const uint32_t (&cf)[LC_MAX],
+                                               uint32_t sc, uint32_t av, uint64_t base, uint64_t nl,
+                                               const uint32_t (&nb8)[E / 4], const uint32_t (&pt)[E],
+                                               const uint32_t (&ipt)[E], uint32_t carry) {
+  static_assert(T * E == SCAN_B && E % 4 == 0, "a scan chunk");
+  uint32_t w[E], tot = 0;
+#pragma unroll
+  for (int k = 0; k < E; k++) {
+    w[k] = base + k > 0 ? hmod(((nb8[k >> 2] >> (8 * (k & 3))) & 0xFFu) * pt[k]) : 0u;
+    tot += w[k];
+  }
+  // a = 0: q[j] = num[j + 1], which for the thread's last coefficient is the next thread's first
+  // (lane shuffle / LDS across waves) or, for the block's last thread, the next chunk's first
+  // coefficient (recomputed from the terms: nt byte loads, that thread only)
+  __shared__ uint32_t first[T / 64 + 1];
+  const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+  uint32_t nxt = __shfl_down(nb8[0] & 0xFFu, 1, 64);
+  if (av == 0) {   // (uniform)
+    if (lane == 0) first[wv] = nb8[0] & 0xFFu;
+    if (threadIdx.x == T - 1) {
+      const uint64_t i = base + E;
+      uint32_t s = 0;
+      for (int u = 0; u < a.nt; u++) s += i < a.len[u] ? cf[u] * a.p[u][i] : 0u;
+      first[T / 64] = i < nl ? hmod(hmod(s) * sc) : 0u;
+    }
+  }
+  // suffix sums: lanes, waves, then the later chunks' carry -- one barrier
+  const uint32_t suf = wave_suffix(tot);                 // (<= 64 x E x 16)
+  const uint32_t cw = hmod(wave_sum(carry));             // (the wave sum <= 64 x 16)
+  __shared__ uint32_t ws[2][T / 64];
+  if (lane == 0) {
+    ws[0][wv] = suf;
+    ws[1][wv] = cw;
+  }
+  __syncthreads();
+  if (av == 0 && lane == 63) nxt = first[wv + 1];
+  uint32_t run = suf - tot;
+#pragma unroll
+  for (int u = 0; u < T / 64; u++) run += (u > wv ? ws[0][u] : 0u) + ws[1][u];
+  run = hmod(run);   // (<= 4096 x 16 + T / 64 x 16 < 69632)
+  const uint64_t ql = nl - 1;
+  uint32_t o[E / 4] = {};
+#pragma unroll
+  for (int k = E - 1; k >= 0; k--) {
+    const uint64_t j = base + k;   // run = sum_{i > j} w_i (mod 17: < 17 + (E - 1) x 16 below)
+    if (j < ql) {
+      const uint32_t nx = k == E - 1 ? nxt : (nb8[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu;
+      const uint32_t v = av == 0 ? nx : hmod(hmod(run) * ipt[k]);
+      o[k >> 2] |= v << (8 * (k & 3));
+      if (j == 0 && ((nb8[0] & 0xFFu) + av * v) % HFP) atomicOr(D.flag, 1u);
+    }
+    run += w[k];
+  }
+  uint8_t* q = D.q;
+  if (D.vec && base + E <= ql) {
+    if constexpr (E == 16) *reinterpret_cast<uint4*>(q + base) = make_uint4(o[0], o[1], o[2], o[3]);
+    else *reinterpret_cast<uint2*>(q + base) = make_uint2(o[0], o[1]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < E; k++)
+      if (base + k < ql) q[base + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
+  }
+}
+// av^k and av^-(k + 1) for k < 16 (exponents mod 16: av^16 = 1 for av != 0)
+__device__ __forceinline__ void div_powers(uint32_t av, uint32_t (&pw)[16], uint32_t (&ipw)[16]) {
+  const uint32_t ai = hinv(av);
+  pw[0] = 1;
+  ipw[15] = 1;   // av^-16 = av^0
+  uint32_t x = ai;
+#pragma unroll
+  for (int j = 1; j < 16; j++) pw[j] = pw[j - 1] * av % HFP;
+#pragma unroll
+  for (int j = 0; j < 15; j++) {   // ipw[j] = ai^(j + 1)
+    ipw[j] = x;
+    x = x * ai % HFP;
+  }
+}
+
 // Round 5 in ONE launch (PLK_OPT_PROVE_FUSE_DIV): each block forms its 4096-coefficient chunk
 // of the numerator in registers (lincomb_scan_kernel's loads), publishes the chunk's aggregate
 // as one 64-bit word {epoch, sum}, then reduces the aggregates of every later chunk and finishes
@@ -1073,67 +1220,92 @@ __global__ __launch_bounds__(SCAN_T) void lincomb_divide_kernel(LcBatch b, LinDi
     carry += (uint32_t)v % HFP;
   }
   if (late) atomicOr(D.flag, SCAN_TIMEOUT);
-  // from here lin_scan_apply_kernel's work on the packed coefficients
-  uint32_t ipw[16];
-  ipw[0] = 1;
-  const uint32_t ai = hinv(av);
-#pragma unroll
-  for (int j = 1; j < 16; j++) ipw[j] = ipw[j - 1] * ai % HFP;
-  uint32_t w[SCAN_E], tot = 0;
-#pragma unroll
-  for (int k = 0; k < SCAN_E; k++) {
-    w[k] = base + k > 0 ? hmod(((nb8[k >> 2] >> (8 * (k & 3))) & 0xFFu) * pw[k]) : 0u;
-    tot += w[k];
+  uint32_t pw2[16], ipw[16];
+  div_powers(av, pw2, ipw);
+  lin_div_finish<SCAN_T, SCAN_E>(a, D, cf, sc, av, base, nl, nb8, pw2, ipw, carry % HFP);
+}
+
+// Round 5 in ONE launch with no waits (PLK_OPT_PROVE_EVAL_AGG): the scan's chunk aggregates are
+// linear in the numerator's terms -- sum_{i in c} W[i] z^i = sc sum_t cf_t sum_{i in c} p_t[i] z^i
+// (W = sc sum_t cf_t p_t; the constants sit at i = 0, 1, in chunk 0, which is never a later chunk)
+// -- and round 4 already evaluates every term at z.  Its evaluation rows store each term's chunk
+// sums (EvArgs::col, 16-byte records of agg[]: one column per term, t_lo / t_mid / t_hi as rows of
+// their own; z(omega x) evaluated at z gives z_x's sums at z omega for the second division), so
+// this launch forms its chunk of both numerators in registers, reduces the later chunks' records
+// against the round-4 coefficients (one v_dot4 per 4 columns) and writes the quotient bytes: the
+// numerators are never stored and lin_scan_apply_kernel's launch is gone.  Extra grid rows run
+// the commitments that do not wait for round 5, as lincomb_scan_kernel's do.
+struct AggMap {
+  const uint8_t* agg;        // [chunk][16] column sums (prover memory, written by eval_kernel)
+  int8_t col[2][LC_MAX];     // division d, numerator term t -> its agg column (-1: none)
+};
+// 512 threads of 8 coefficients per 4096-coefficient chunk: twice the waves of the 16-coefficient
+// form over the same ~770 chunks (one block each), so more of each block's load -> sum -> scan chain
+// overlaps (the chain, not the bytes, bounds this launch)
+constexpr int AGG_T = 512, AGG_E = SCAN_B / AGG_T;
+__global__ __launch_bounds__(AGG_T) void lincomb_agg_divide_kernel(LcBatch b, LinDivs L, const uint8_t* __restrict__ S,
+                                                                  AggMap m, EarlyMsm em) {
+  if ((int)blockIdx.y >= em.nd) {   // (uniform) an early commitment row
+    __shared__ uint32_t etab[PLK_GROUP_ORDER];
+    __shared__ uint32_t wsum[AGG_T / PLK_WAVE];
+    __shared__ uint32_t wbad[AGG_T / PLK_WAVE];
+    const int r = (int)blockIdx.y - em.nd;
+    if (blockIdx.x >= em.X) return;
+    (void)msm_log_block<AGG_T>(em.logs, em.arena + (uint64_t)r * em.cstride, em.rl.n[r], blockIdx.x, em.X, (uint32_t)r,
+                               em.res + r, em.exp_words, etab, wsum, wbad);
+    return;
   }
-  // a = 0: q[j] = num[j + 1], which for the thread's last coefficient is the next thread's first
-  // (lane shuffle / LDS across waves) or, for the block's last thread, the next chunk's first
-  // coefficient (recomputed from the terms: nt byte loads, that thread only)
-  __shared__ uint32_t first[SCAN_T / 64 + 1];
-  const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
-  uint32_t nxt = __shfl_down(nb8[0] & 0xFFu, 1, 64);
-  if (av == 0) {   // (uniform)
-    if (lane == 0) first[wv] = nb8[0] & 0xFFu;
-    if (threadIdx.x == SCAN_T - 1) {
-      const uint64_t i = base + 16;
-      uint32_t s = 0;
-      for (int u = 0; u < a.nt; u++) s += i < a.len[u] ? cf[u] * a.p[u][i] : 0u;
-      first[SCAN_T / 64] = i < nl ? hmod(hmod(s) * sc) : 0u;
-    }
-  }
-  // suffix sums: lanes, waves, then the later chunks' carry -- one barrier
-  const uint32_t suf = wave_suffix(tot);
-  const uint32_t cw = wave_sum(carry % HFP);
-  __shared__ uint32_t ws[2][SCAN_T / 64];
-  if (lane == 0) {
-    ws[0][wv] = suf;
-    ws[1][wv] = cw;
-  }
-  __syncthreads();
-  if (av == 0 && lane == 63) nxt = first[wv + 1];
-  uint32_t run = suf - tot;
+  const int d = blockIdx.y;
+  const LcArgs& a = b.a[d];
+  const LinDiv& D = L.d[d];
+  const int c = (int)blockIdx.x;
+  if (c >= D.nb) return;
+  uint32_t cf[LC_MAX];
 #pragma unroll
-  for (int u = 0; u < SCAN_T / 64; u++) run += (u > wv ? ws[0][u] : 0u) + ws[1][u];
-  const uint64_t ql = nl - 1;
-  uint32_t o[4] = {0, 0, 0, 0};
+  for (int t = 0; t < LC_MAX; t++) cf[t] = __builtin_amdgcn_readfirstlane(t < a.nt ? S[a.slot[t]] : 0u);
+  const uint32_t sc = __builtin_amdgcn_readfirstlane(S[a.scale]);
+  const uint32_t c0 = __builtin_amdgcn_readfirstlane(a.c0 >= 0 ? S[a.c0] : 0u);
+  const uint32_t c1 = __builtin_amdgcn_readfirstlane(a.c1 >= 0 ? S[a.c1] : 0u);
+  const uint64_t base = (uint64_t)c * SCAN_B + (uint64_t)threadIdx.x * AGG_E;
+  const uint64_t nl = a.out_len;
+  // the later chunks' records: one per thread loaded before the numerator's terms (a division of
+  // up to 513 chunks, ~2^21 coefficients, needs no more), the rest after
+  const uint4* rec = reinterpret_cast<const uint4*>(m.agg);
+  const int cb0 = c + 1 + (int)threadIdx.x;
+  const uint4 r0 = cb0 < D.nb ? rec[cb0] : make_uint4(0u, 0u, 0u, 0u);
+  uint32_t acc[AGG_E];
+  lc_swar<AGG_E / 4>(a, cf, c0, c1, base, acc);
+  // column weights K = sc cf_t mod 17 packed as bytes: one v_dot4_u32_u8 per record word
+  uint32_t K[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (int k = SCAN_E - 1; k >= 0; k--) {
-    const uint64_t j = base + k;   // run = sum_{i > j} w_i
-    if (j < ql) {
-      const uint32_t nx = k == 15 ? nxt : (nb8[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu;
-      const uint32_t v = av == 0 ? nx : run % HFP * ipw[(k + 1) & 15] % HFP;
-      o[k >> 2] |= v << (8 * (k & 3));
-      if (j == 0 && ((nb8[0] & 0xFFu) + av * v) % HFP) atomicOr(D.flag, 1u);
-    }
-    run += w[k];
+  for (int t = 0; t < LC_MAX; t++) {
+    const int col = m.col[d][t];
+    if (t < a.nt && col >= 0) K[col >> 2] += (cf[t] * sc % HFP) << (8 * (col & 3));
   }
-  uint8_t* q = D.q;
-  if (D.vec && base + 16 <= ql) {
-    *reinterpret_cast<uint4*>(q + base) = make_uint4(o[0], o[1], o[2], o[3]);
-  } else {
+  auto dot = [&](const uint4& r) {   // (<= 4 x 4 x 16 x 16)
+    return __builtin_amdgcn_udot4(r.x, K[0], __builtin_amdgcn_udot4(r.y, K[1], 0u, false), false) +
+           __builtin_amdgcn_udot4(r.z, K[2], __builtin_amdgcn_udot4(r.w, K[3], 0u, false), false);
+  };
+  uint32_t carry = dot(r0);
+  for (int cb = cb0 + AGG_T; cb < D.nb; cb += AGG_T) carry += dot(rec[cb]) % HFP;
+  const uint32_t av = __builtin_amdgcn_readfirstlane(S[D.aslot]);
+  uint32_t pw[16], ipw[16];
+  div_powers(av, pw, ipw);
+  // this thread's coefficients start at base = 0 or 8 (mod 16): its powers from there
+  const bool odd = (base & 15u) != 0;
+  uint32_t pt[AGG_E], ipt[AGG_E];
 #pragma unroll
-    for (int k = 0; k < 16; k++)
-      if (base + k < ql) q[base + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
+  for (int k = 0; k < AGG_E; k++) {
+    pt[k] = odd ? pw[(k + AGG_E) & 15] : pw[k];
+    ipt[k] = odd ? ipw[(k + AGG_E) & 15] : ipw[k];
   }
+  uint32_t nb8[AGG_E / 4] = {};
+#pragma unroll
+  for (int k = 0; k < AGG_E; k++) {
+    const uint32_t v = base + k < nl ? hmod(hmod(acc[k]) * sc) : 0u;   // (acc <= 16 x 16 x 255 + 32)
+    nb8[k >> 2] |= v << (8 * (k & 3));
+  }
+  lin_div_finish<AGG_T, AGG_E>(a, D, cf, sc, av, base, nl, nb8, pt, ipt, carry % HFP);
 }
 
 // (c) any other divisor: the reference's long division in one workgroup (only reached for
@@ -1495,6 +1667,7 @@ struct plk_prover {
   int t2_sum = 0;                  // round 3: (a b) q_m + t_2 computed as one sum (in T2)
   uint64_t rem_blocks = 0;
   uint32_t* d_bsum = nullptr;      // scan block sums
+  uint8_t* d_agg = nullptr;        // round 4's chunk aggregates of round 5's numerator terms [chunk][16]
   unsigned long long* d_scanw = nullptr;   // lincomb_divide_kernel's chunk words {epoch, sum}
   uint32_t scanw_stride = 0;       // words per division
   uint32_t scan_epoch = 0;         // launches of lincomb_divide_kernel so far (0: none)
@@ -1673,44 +1846,74 @@ int lincomb(plk_prover* P, std::initializer_list<std::pair<const uint8_t*, uint6
   return PLK_OK;
 }
 
-EvArgs make_evargs(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64_t, int, int>> ev, int post) {
+// one evaluation of a batch, or (join) one more row of the previous entry's evaluation
+struct EvSpec {
+  const uint8_t* p;
+  uint64_t len;
+  int xslot, out;
+  int col = -1;        // chunk-aggregate column (EvArgs::col), -1: none
+  int mexp = 0;        // the row's partial enters the evaluation times x^mexp
+  bool join = false;   // a further row of the previous entry's evaluation (no split, same out)
+};
+// agg_ok (optional): false when a row that stores chunk aggregates cannot be read in whole 16-byte
+// chunks (the aggregates are then not produced: the caller falls back to the two-launch scan)
+EvArgs make_evargs(plk_prover* P, const std::vector<EvSpec>& ev, int post, bool* agg_ok = nullptr, uint8_t* agg = nullptr) {
   EvArgs a{};
+  a.agg = agg;
+  bool ok = true;
   // a polynomial much longer than the shortest one (t(x): 3n, the r(x) part: 2n) runs as several
   // rows of about the shortest length, so its blocks do no more work than the others' and the
   // launch does not wait on one row's tail
   uint64_t base = ~0ull;
-  for (const auto& t : ev) base = std::min<uint64_t>(base, std::max<uint64_t>(std::get<1>(t), 1));
+  for (const EvSpec& t : ev) base = std::min<uint64_t>(base, std::max<uint64_t>(t.len, 1));
   int spare = EV_ROWS - (int)ev.size();
-  int e = 0, r = 0;
-  for (const auto& t : ev) {
-    const uint8_t* p = std::get<0>(t);
-    const uint64_t len = std::get<1>(t);
+  int e = -1, r = 0;
+  for (size_t q = 0; q < ev.size(); q++) {
+    const EvSpec& t = ev[q];
+    const uint8_t* p = t.p;
+    const uint64_t len = t.len;
     // 2: aligned and readable in whole 16-byte chunks (length a multiple of 16, or inside the
     // prover's own padded allocation); 1: aligned; 0: bytes
     const bool inside = p >= P->mem && p < P->mem + P->mem_bytes;
     const int vec = ((uintptr_t)p % 16) != 0 ? 0 : ((len % 16 == 0 || inside) ? 2 : 1);
+    const int col = agg && vec == 2 ? t.col : -1;
+    ok = ok && (t.col < 0 || col >= 0);
+    const bool grouped = t.join || (q + 1 < ev.size() && ev[q + 1].join);
     int parts = 1;
-    if (PLK_EV_SPLIT && vec && base >= 4096 && len >= 2 * base)
+    if (!grouped && PLK_EV_SPLIT && vec && base >= 4096 && len >= 2 * base)
       parts = (int)std::min<uint64_t>((len + base / 2) / base, (uint64_t)(1 + spare));
     spare -= parts - 1;
-    const uint64_t chunk = ((len + parts - 1) / parts + 15) / 16 * 16;
+    uint64_t chunk = ((len + parts - 1) / parts + 15) / 16 * 16;
+    if (col >= 0) chunk = (chunk + AGG_CHUNK - 1) / AGG_CHUNK * AGG_CHUNK;   // (whole scan chunks per row)
+    if (!t.join) e++;
     for (int k = 0; k < parts; k++, r++) {
       const uint64_t off = std::min<uint64_t>(k * chunk, len);
       a.p[r] = p + off;
       a.len[r] = std::min<uint64_t>(chunk, len - off);
-      a.xslot[r] = std::get<2>(t);
-      a.out[r] = std::get<3>(t);
+      a.xslot[r] = t.xslot;
+      a.out[r] = t.out;
       a.vec[r] = vec;   // (off = 0 mod 16: the alignment and the whole-chunk reads carry over)
       a.grp[r] = e;
-      a.parts[r] = parts;
-      a.first[r] = k == 0;
+      a.first[r] = k == 0 && !t.join;
+      a.mexp[r] = t.mexp;
+      a.col[r] = col;
+      a.coff[r] = (int)(off / AGG_CHUNK);
     }
-    e++;
   }
-  a.ne = e;
+  for (int i = 0; i < r; i++) {   // rows per evaluation: the arrivals its word counts (x blocks)
+    a.parts[i] = 0;
+    for (int j = 0; j < r; j++) a.parts[i] += a.grp[j] == a.grp[i];
+  }
+  a.ne = e + 1;
   a.nr = r;
   a.post = post;
+  if (agg_ok) *agg_ok = ok && agg;
   return a;
+}
+EvArgs make_evargs(plk_prover* P, std::initializer_list<std::tuple<const uint8_t*, uint64_t, int, int>> ev, int post) {
+  std::vector<EvSpec> v;
+  for (const auto& t : ev) v.push_back(EvSpec{std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t)});
+  return make_evargs(P, v, post);
 }
 int evals_launch(plk_prover* P, const EvArgs& a, const EarlyMsm* em = nullptr) {
   const int nrows = a.nr;
@@ -1768,8 +1971,9 @@ struct LinDivReq {
   uint32_t* flag;
 };
 // lcs (optional): the numerators' lincombs, computed by the aggregate launch itself
+// am (optional, with lcs): the later chunks' aggregates from round 4's evaluation rows -- ONE launch
 int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs, const LcBatch* lcs = nullptr,
-                  const EarlyMsm* em = nullptr) {
+                  const EarlyMsm* em = nullptr, const AggMap* am = nullptr) {
   if (lcs) {   // a skipped (tiny) division would shift the numerators' order: compute them apart
     int j = 0;
     bool tiny = false;
@@ -1811,6 +2015,12 @@ int divide_linear(plk_prover* P, std::initializer_list<LinDivReq> reqs, const Lc
       e.nd = nd;
       e.X = std::min<uint32_t>(e.X, (uint32_t)nbmax);
       P->early_rows = e.nrows;
+    }
+    if (am && nd == 2) {   // (both divisions present: the map's rows are [W, ZZ])
+      hipLaunchKernelGGL(lincomb_agg_divide_kernel, dim3((unsigned)nbmax, nd + (e.nrows > 0 ? e.nrows : 0)),
+                         dim3(AGG_T), 0, P->st, *lcs, L, P->d_S, *am, e);
+      PLK_HIP(hipGetLastError());
+      return PLK_OK;
     }
     hipLaunchKernelGGL(lincomb_scan_kernel, dim3((unsigned)nbmax, nd + (e.nrows > 0 ? e.nrows : 0)), dim3(SCAN_T), 0,
                        P->st, *lcs, L, P->d_S, e);
@@ -1913,6 +2123,7 @@ int create_on(const plk_plonk_desc_t* d, int dev, plk_prover_t** out) {
                o_rem = B.take(P->zh_len / 1024 + 64),
                o_bsum = B.take(4 * ((L.lw + SCAN_B - 1) / SCAN_B + 2) + 4 * ((L.lzz + SCAN_B) / SCAN_B + 2)),
                o_scanw = B.take(8 * 2 * ((std::max(L.lw, L.lzz) + SCAN_B) / SCAN_B + 2)),
+               o_agg = B.take(16 * ((std::max(L.lw, L.lzz) + SCAN_B) / SCAN_B + 2)),
                o_res = B.take(9 * sizeof(PlkMsmResult)),
                o_srslog = B.take(P->srs_len + 16), o_words = B.take(64),
                o_arena = B.take(9 * P->cstride);
@@ -1947,6 +2158,7 @@ int create_on(const plk_plonk_desc_t* d, int dev, plk_prover_t** out) {
   P->d_srs = m + o_srs; P->d_zh = m + o_zh; P->d_h3 = m + o_h3; P->d_hinv = m + o_hinv; P->d_S = m + o_S;
   P->d_stat = (uint32_t*)(m + o_stat); P->d_tick = (uint32_t*)(m + o_tick); P->d_rem = m + o_rem; P->d_bsum = (uint32_t*)(m + o_bsum);
   P->d_scanw = (unsigned long long*)(m + o_scanw);
+  P->d_agg = m + o_agg;
   P->scanw_stride = (uint32_t)((std::max(L.lw, L.lzz) + SCAN_B) / SCAN_B + 2);
   P->d_res = (PlkMsmResult*)(m + o_res); P->arena = m + o_arena;
   P->d_srs_log = m + o_srslog;
@@ -2287,33 +2499,63 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
                             : 0;
   const MsmRowLens rl = msm_row_lens(P, L);
   const EarlyMsm em{P->d_srs_log, P->arena, (uint64_t)P->cstride, rl, P->d_res, P->exp_words, 7, 0, (uint32_t)(2048 / 9)};
-  RC(evals(P, {{cA, L.la, S_Z, S_AZ}, {cB, L.la, S_Z, S_BZ}, {cC, L.la, S_Z, S_CZ}, {S1, n, S_Z, S_S1Z},
-               {S2, n, S_Z, S_S2Z}, {P->TX, L.ltx, S_Z, S_TZ}, {P->ZW, L.lzw, S_Z, S_ZWZ}, {L1, n, S_Z, S_L1Z},
-               {QM, n, S_Z, S_QMZ}, {QL, n, S_Z, S_QLZ}, {QR, n, S_Z, S_QRZ}, {QO, n, S_Z, S_QOZ},
-               {cZ, L.lzx, S_Z, S_ZXZ}, {P->P3, L.lr3, S_Z, S_P3Z}},
-           EV_POST_R4, early == 2 ? &em : nullptr));
+  // round 5's numerators (built here: with PLK_OPT_PROVE_EVAL_AGG round 4's evaluation rows also
+  // store their terms' scan-chunk aggregates, lincomb_agg_divide_kernel)
+  LcBatch nb5{};
+  // w_z(x)'s numerator terms, in agg column order (column t = term t): t_lo t_mid t_hi q_m q_l q_r
+  // q_o z_x P3 a_x b_x c_x s_sigma_1 s_sigma_2; column 14 = z(omega x) at z = z_x at z omega
+  enum { AC_TLO, AC_TMID, AC_THI, AC_QM, AC_QL, AC_QR, AC_QO, AC_ZX, AC_P3, AC_A, AC_B, AC_C, AC_S1, AC_S2, AC_ZW };
+  nb5.a[0] = make_lc({{cTlo, std::min<uint64_t>(part, L.ltx)}, {cTmid, lmid}, {cThi, lhi}, {QM, n}, {QL, n},
+                      {QR, n}, {QO, n}, {cZ, L.lzx}, {P->P3, L.lr3}, {cA, L.la}, {cB, L.la}, {cC, L.la}, {S1, n},
+                      {S2, n}},
+                     {S_ONE, S_ZN2, S_Z2N4, S_VAB, S_VAZ, S_VBZ, S_VCZ, S_VR24, S_VR3B, S_V2, S_V3, S_V4, S_V5,
+                      S_V6},
+                     S_W0, -1, S_ONE, -1, P->W, L.lw);
+  nb5.a[1] = make_lc({{cZ, L.lzx}}, {S_ONE}, S_NEGZWZ, -1, S_ONE, -1, P->ZZ, L.lzz);
+  // fused numerators need 16-byte aligned terms readable in whole 16-byte chunks: the
+  // caller's polynomials (length n) qualify when n % 16 == 0 and they are aligned
+  bool fuse = n % 16 == 0 && nb5.a[0].nt > 0 && nb5.a[1].nt > 0;
+  for (int j = 0; j < 2; j++) {
+    fuse = fuse && (uintptr_t)nb5.a[j].out % 16 == 0;
+    for (int t = 0; t < nb5.a[j].nt; t++) fuse = fuse && (uintptr_t)nb5.a[j].p[t] % 16 == 0;
+  }
+  bool agg = fuse && P->d_agg && plk_opt(PLK_OPT_PROVE_EVAL_AGG) && !plk_opt(PLK_OPT_PROVE_FUSE_DIV) &&
+             L.lw >= 2 && L.lzz >= 2;
+  EvArgs ea{};
+  if (agg) {   // t(z) from its three slices (x^(n + 2), x^(2n + 4): their offsets), every W term's chunks
+    const int m1 = (int)(part % 16), m2 = (int)(2 * part % 16);
+    ea = make_evargs(P,
+                     {{cA, L.la, S_Z, S_AZ, AC_A}, {cB, L.la, S_Z, S_BZ, AC_B}, {cC, L.la, S_Z, S_CZ, AC_C},
+                      {S1, n, S_Z, S_S1Z, AC_S1}, {S2, n, S_Z, S_S2Z, AC_S2},
+                      {cTlo, std::min<uint64_t>(part, L.ltx), S_Z, S_TZ, AC_TLO},
+                      {cTmid, lmid, S_Z, S_TZ, AC_TMID, m1, true}, {cThi, lhi, S_Z, S_TZ, AC_THI, m2, true},
+                      {P->ZW, L.lzw, S_Z, S_ZWZ, AC_ZW}, {L1, n, S_Z, S_L1Z},
+                      {QM, n, S_Z, S_QMZ, AC_QM}, {QL, n, S_Z, S_QLZ, AC_QL}, {QR, n, S_Z, S_QRZ, AC_QR},
+                      {QO, n, S_Z, S_QOZ, AC_QO}, {cZ, L.lzx, S_Z, S_ZXZ, AC_ZX}, {P->P3, L.lr3, S_Z, S_P3Z, AC_P3}},
+                     EV_POST_R4, &agg, P->d_agg);
+  }
+  if (!agg)
+    ea = make_evargs(P, {{cA, L.la, S_Z, S_AZ}, {cB, L.la, S_Z, S_BZ}, {cC, L.la, S_Z, S_CZ}, {S1, n, S_Z, S_S1Z},
+                         {S2, n, S_Z, S_S2Z}, {P->TX, L.ltx, S_Z, S_TZ}, {P->ZW, L.lzw, S_Z, S_ZWZ}, {L1, n, S_Z, S_L1Z},
+                         {QM, n, S_Z, S_QMZ}, {QL, n, S_Z, S_QLZ}, {QR, n, S_Z, S_QRZ}, {QO, n, S_Z, S_QOZ},
+                         {cZ, L.lzx, S_Z, S_ZXZ}, {P->P3, L.lr3, S_Z, S_P3Z}},
+                     EV_POST_R4);
+  RC(evals_launch(P, ea, early == 2 ? &em : nullptr));
   // ---- round 5: opening polynomials (src/plonk.h:580-621)
-  // w_z numerator and z(x) - z_omega_z, then both divisions, each pair in one launch per phase
+  // w_z numerator and z(x) - z_omega_z, then both divisions: one launch with the aggregates of
+  // round 4, else each pair in one launch per phase
   {
-    LcBatch nb5{};
-    nb5.a[0] = make_lc({{cTlo, std::min<uint64_t>(part, L.ltx)}, {cTmid, lmid}, {cThi, lhi}, {QM, n}, {QL, n},
-                        {QR, n}, {QO, n}, {cZ, L.lzx}, {P->P3, L.lr3}, {cA, L.la}, {cB, L.la}, {cC, L.la}, {S1, n},
-                        {S2, n}},
-                       {S_ONE, S_ZN2, S_Z2N4, S_VAB, S_VAZ, S_VBZ, S_VCZ, S_VR24, S_VR3B, S_V2, S_V3, S_V4, S_V5,
-                        S_V6},
-                       S_W0, -1, S_ONE, -1, P->W, L.lw);
-    nb5.a[1] = make_lc({{cZ, L.lzx}}, {S_ONE}, S_NEGZWZ, -1, S_ONE, -1, P->ZZ, L.lzz);
-    // fused numerators need 16-byte aligned terms readable in whole 16-byte chunks: the
-    // caller's polynomials (length n) qualify when n % 16 == 0 and they are aligned
-    bool fuse = n % 16 == 0 && nb5.a[0].nt > 0 && nb5.a[1].nt > 0;
-    for (int j = 0; j < 2; j++) {
-      fuse = fuse && (uintptr_t)nb5.a[j].out % 16 == 0;
-      for (int t = 0; t < nb5.a[j].nt; t++) fuse = fuse && (uintptr_t)nb5.a[j].p[t] % 16 == 0;
+    AggMap am{};
+    if (agg) {
+      am.agg = P->d_agg;
+      for (int t = 0; t < LC_MAX; t++) am.col[0][t] = am.col[1][t] = -1;
+      for (int t = 0; t < nb5.a[0].nt; t++) am.col[0][t] = (int8_t)t;   // (AC_* order)
+      am.col[1][0] = AC_ZW;
     }
     if (!fuse) RC(lincomb_batch(P, {nb5.a[0], nb5.a[1]}));
     RC(divide_linear(P, {{P->W, L.lw, S_Z, cWz, P->d_stat + ST_REM_W1},
                          {P->ZZ, L.lzz, S_ZOMEGA, cWzw, P->d_stat + ST_REM_W2}},
-                     fuse ? &nb5 : nullptr, early == 1 ? &em : nullptr));
+                     fuse ? &nb5 : nullptr, early == 1 ? &em : nullptr, agg ? &am : nullptr));
   }
   // ---- trimmed lengths for the reference's exits: computed by the packing kernel after the MSM
   TrimArgs trims{};

@@ -62,11 +62,13 @@ def _synthetic(n, seed, srs_len):
 @pytest.mark.parametrize("n,seed,z", [(256, 61, 0), (256, 62, 1), (4096, 63, 0), (16384, 61, 0), (16384, 64, 0),
                                       (16384, 65, None), (65536, 61, 0), (65536, 67, 16)])
 def test_round5_divisions_vs_oracle(hip, oracle, n, seed, z):
-    """Round 5's numerators and divisions by x - z, x - z omega: the one-launch form
-    (PROVE_FUSE_DIV = 1, lincomb_divide_kernel: chunks in reverse block order, each waiting for
-    the later chunks' aggregates) and the two-launch form give the oracle's proof, from 1 to ~32
-    chunks per division.  z = 0 is the shift q[j] = num[j + 1], which crosses lanes, waves and
-    chunks (src/poly.h:124-177 with divisor x - 0)."""
+    """Round 5's numerators and divisions by x - z, x - z omega: the one-launch forms -- the
+    chunk aggregates from round 4's evaluation rows (PROVE_EVAL_AGG = 1, the default:
+    lincomb_agg_divide_kernel, with the early commitments in its grid, in round 4's, or in neither)
+    and the look-back form (PROVE_FUSE_DIV = 1, lincomb_divide_kernel: chunks in reverse block
+    order, each waiting for the later chunks' aggregates) -- and the two-launch form give the
+    oracle's proof, from 1 to ~32 chunks per division.  z = 0 is the shift q[j] = num[j + 1], which
+    crosses lanes, waves and chunks (src/poly.h:124-177 with divisor x - 0)."""
     polys, chal, rnd, zh, pts = _synthetic(n, seed, 2 * n + 8)
     chal = list(chal)
     if z is not None:
@@ -77,13 +79,13 @@ def test_round5_divisions_vs_oracle(hip, oracle, n, seed, z):
         want = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes()).rounds(polys, chal, rnd, strict=False)
     except ProveError:   # (16384, 64, 0): t(x) too short for its slices -- the reference exits there too
         want = None
-    for fuse in (1, 0, 1):
-        with hip.options(PROVE_FUSE_DIV=fuse):
+    for fuse, agg, early in ((1, 0, 1), (0, 1, 1), (0, 0, 1), (0, 1, 2), (0, 1, 0), (1, 1, 1), (0, 1, 1)):
+        with hip.options(PROVE_FUSE_DIV=fuse, PROVE_EVAL_AGG=agg, PROVE_EARLY_COMMITS=early):
             if want is None:
                 with pytest.raises(hip.PlonkHipError):
                     pr.rounds_dev(dev, chal, rnd, strict=False)
             else:
-                assert pr.rounds_dev(dev, chal, rnd, strict=False).hex() == want.hex(), fuse
+                assert pr.rounds_dev(dev, chal, rnd, strict=False).hex() == want.hex(), (fuse, agg, early)
 
 
 @pytest.mark.parametrize("n,seed", [(37, 71), (4096, 72), (20000, 73)])

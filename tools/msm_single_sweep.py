@@ -20,7 +20,7 @@ hip.init(0)
 dev = torch.device("cuda", 0)
 n, sets = 1 << 22, 40
 pts, sc = make_msm_sets(torch, n, sets, dev, 1234)
-env = {k: v for k, v in os.environ.items() if k.startswith("PLK_MSM")}
+env = {k: v for k, v in os.environ.items() if k.startswith("PLK_MSM") or k == "PLK_TUNE"}
 best = min((single_msm_component(torch, hip, pts, sc, n, sets, dev) for _ in range(3)),
            key=lambda c: c["device_us_per_msm"])
 print(json.dumps({"env": env, "us": best["device_us_per_msm"], "median_us": best["median_us"], "frac": best["frac"]}))
