@@ -14,7 +14,10 @@ with the same ordering hazards:
 A consumer that does not order itself behind the current stream at the right point reads bytes
 that are not there yet -- exactly what a missing ready= / done= ordering would do over RCCL.
 
-Two things keep a missing ordering from being hidden by timing:
+What keeps a missing ordering from being hidden by timing or by stale memory:
+* irecv poisons its target (0x05 bytes, finished before it returns), so an unordered read of it
+  sees poison, not an earlier proof's bytes left in a reused allocation; the drop-1 diagnostic
+  build likewise poisons its products and writes them ~20 ms later (prove.hip);
 * before each helper's step the current stream spins (`delay` cycles): the helper's chains start
   behind it (plk_prover_chains_dev makes its stream wait for `done` first), and so does a send
   with no ordering -- which then copies while the chains run instead of after them;
@@ -65,6 +68,11 @@ class NcclSemantics:
     def irecv(self, t, src, group=None):
         # (this stand-in serves rank 0's receives in send order; the choreography sends each chain once)
         staged, done = self.wire[0].pop(0)
+        # poison the target before the late bytes are queued (and before this call returns): a
+        # consumer with no ordering behind wait() reads the poison, never stale bytes of an earlier
+        # (correct) proof that the caching allocator handed back in `t`
+        t.fill_(0x05)
+        torch.cuda.current_stream().synchronize()
         self.side.wait_event(done)
         with torch.cuda.stream(self.side):
             torch.cuda._sleep(self.delay)
