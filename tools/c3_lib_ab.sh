@@ -3,7 +3,7 @@
 # build/var/lib_*.so, alternating, ROUNDS rounds
 set -u
 R=${1:-3}
-LIBS="plonk.c_amd/libplonkhip.so $(ls plonk.c_amd/build/var/lib_*.so)"
+LIBS=${LIBS:-"plonk.c_amd/libplonkhip.so $(ls plonk.c_amd/build/var/lib_*.so)"}
 for r in $(seq $R); do
   for lib in $LIBS; do
     echo "$(basename $lib) $(PLK_LIB=$PWD/$lib timeout -k 5 120 python3 tools/c3_time.py 2>/dev/null | grep '^{')" || exit 1

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 R=${1:-3}
 O=gpurun_out/lab
 mkdir -p $O
-LIBS="plonk.c_amd/libplonkhip.so $(ls plonk.c_amd/build/var/lib_*.so)"
+LIBS=${LIBS:-"plonk.c_amd/libplonkhip.so $(ls plonk.c_amd/build/var/lib_*.so)"}
 for r in $(seq $R); do
   for lib in $LIBS; do
     PLK_LIB=$PWD/$lib timeout -k 10 120 python3 tools/prove_bench.py ${PB_ARGS:-20} 2>/dev/null > $O/o.json || { echo "$lib failed"; exit 1; }
