@@ -59,10 +59,32 @@ namespace {
 #define PLK_NTT_SWZ 1          // XOR-swizzled (bank-conflict-free) exchange layout; 0: the 1-in-32 pad
 #endif
 #ifndef PLK_NTT_CENTER_SWZ
-#define PLK_NTT_CENTER_SWZ 0   // center exchanges: 0 padded (2, swizzled only where the padding conflicts, spills)
+// center exchanges: 3 = the padded layout with barriers only where a wave's element set changes
+// (Eng::same_sets; round 5: 2^13 centre 80.2 -> 71.3-72.3 us per launch, prove median 0.394-0.407 ->
+// 0.377-0.391 ms, alternating on one box), 0 = padded with a barrier after every exchange's writes
+// and reads, 1 / 2 = swizzled everywhere / where the padding conflicts (measured equal to 0)
+#define PLK_NTT_CENTER_SWZ 3
 #endif
 #ifndef PLK_NTT_CENTER_SWZ12
-#define PLK_NTT_CENTER_SWZ12 1 // ... the same for the 2^12-tile center (round 5: swizzled, with PLK_NTT_RC12 = 3)
+// ... the same for the 2^12-tile center: 4 = one pass-wide conflict-free swizzle with the set-based
+// barriers (round 5: poly_mul 2^19 x 2^19 24.14-24.42 -> 23.73-24.07 us alternating; 1 = swizzled
+// per exchange, double-buffered, with PLK_NTT_RC12 = 3: 25.2 -> 23.7 us)
+#define PLK_NTT_CENTER_SWZ12 4
+#endif
+#ifndef PLK_NTT_DBUF13
+// 2^13-tile high passes: two exchange buffers, one barrier per exchange (round 5: prover forward
+// passes 46.8 / 39.2 -> 45.2 / 38.4 us, inverse M = 8 31.1 -> 30.4 us, prove median -0.5..1 %)
+#define PLK_NTT_DBUF13 1
+#endif
+#ifndef PLK_NTT_ALT_ARRAYS
+// pass kernels: exchange buffers alternate across a block's arrays, no barrier between arrays (round 5:
+// prove median 0.373-0.397 vs 0.377-0.387 ms, four alternations -- off)
+#define PLK_NTT_ALT_ARRAYS 0
+#endif
+#ifndef PLK_NTT_LO_USWZ
+// standalone lo = 0 passes: the pass-wide swizzle with set-based barriers (Eng SWZ 4; round 5: 2^20
+// forward F29 13.1-13.3 -> 12.5-12.55 us, BabyBear 13.5 -> 12.85-12.9 us, three alternations)
+#define PLK_NTT_LO_USWZ 1
 #endif
 #ifndef PLK_NTT_WRAP_INLINE
 #define PLK_NTT_WRAP_INLINE 1  // wrapped tops fixed at the end of the last inverse pass (0: wrap_fix_kernel launches)
@@ -346,7 +368,10 @@ struct Eng {
   static constexpr bool HIGH = M < TB;
   static constexpr int NR = (M + R - 1) / R;   // rounds
   static constexpr int BUF = (1 << TB) + (1 << TB) / 32;   // padded exchange buffer (words)
-  static constexpr bool DBUF = TB <= 12;
+  // double-buffered exchanges (one barrier each): 2^12 tiles, and the high passes of 2^13 tiles
+  // with PLK_NTT_DBUF13 (2 x 33 KB + their small tables: still two blocks per CU; the lo = 0
+  // kernels keep one buffer beside their 2^13-word twiddle table)
+  static constexpr bool DBUF = TB <= 12 || (PLK_NTT_DBUF13 && M < TB);
   static constexpr int XCH = NR - 1;            // exchanges per pass
   static constexpr int NBUF = XCH == 0 ? 0 : (XCH > 1 && DBUF ? 2 : 1);
 
@@ -533,12 +558,124 @@ struct Eng {
   // registers (mapping from) -> LDS -> registers (mapping to).  Double-buffered: one barrier
   // suffices (the buffer written next was last read before the previous barrier); single
   // buffer: a second barrier before the buffer is written again.
+  // Barriers an exchange needs (round 5).  A round's mapping gives every wave a SET of elements,
+  // fixed by the element bits its thread-id bits >= 6 (the wave id) select.  Exchange q writes the
+  // wave's round-q set and reads its round-(q + 1) set; with ONE layout for every exchange of a
+  // kernel (the padded one, SWZ = 3) two waves' accesses can only meet on a word when their sets
+  // differ, so:
+  //   * a wave's reads of exchange q and another wave's writes of exchange q + 1 are both of round
+  //     q + 1's sets -- disjoint -- so no barrier trails an exchange and one buffer suffices;
+  //   * an exchange whose two rounds give every wave the SAME set (wave_local) moves data only
+  //     inside each wave, and a wave's LDS operations run in order: no barrier at all;
+  //   * between passes (the previous pass's last reads, the next pass's first writes) the caller
+  //     puts a barrier unless same_sets says those rounds' sets coincide.
+  static constexpr bool same_sets(int qa, bool ia, int qb, bool ib) {
+    for (int i = 6; i < TB - R; i++)
+      if (lane_bit(qa, ia, i) != lane_bit(qb, ib, i)) return false;
+    return true;
+  }
+  static constexpr bool wave_local(int q, bool inv) { return same_sets(q, inv, q + 1, inv); }
+  // One XOR swizzle for EVERY round of a lo = 0 pass in both directions (SWZ = 4): masks m[j] for
+  // the element bits j >= 5 that some round puts on a half-wave's 32 lanes, found by depth-first
+  // search so that each round's 5 lane vectors are independent (conflict-free); with one layout the
+  // barrier rules above hold.  (TB 12 / R 3 and TB 13 / R 3 have one; uswz_ok says so.)
+  static constexpr bool uswz_rounds_ok(const uint32_t* m, int upto) {   // rounds whose bits are <= upto
+    for (int d = 0; d < 2; d++)
+      for (int q = 0; q < NR; q++) {
+        uint32_t v[5] = {};
+        bool skip = false;
+        for (int i = 0; i < 5; i++) {
+          const int b = lane_bit(q, d == 1, i);
+          if (b > upto) skip = true;
+          v[i] = b < 5 ? 1u << b : m[b];
+        }
+        if (!skip && !indep5(v, 5)) return false;
+      }
+    return true;
+  }
+  static constexpr bool uswz_dfs(uint32_t* m, int j) {
+    if (j >= TB) return true;
+    if (j < 5) return uswz_dfs(m, 5);
+    bool used = false;   // does any round put element bit j on a lane?
+    for (int d = 0; d < 2; d++)
+      for (int q = 0; q < NR; q++)
+        for (int i = 0; i < 5; i++) used = used || lane_bit(q, d == 1, i) == j;
+    if (!used) {
+      m[j] = 0;
+      return uswz_dfs(m, j + 1);
+    }
+    for (uint32_t c = 1; c < 32; c++) {
+      m[j] = c;
+      if (uswz_rounds_ok(m, j) && uswz_dfs(m, j + 1)) return true;
+    }
+    m[j] = 0;
+    return false;
+  }
+  static constexpr Swz uswz() {
+    Swz s{};
+    uswz_dfs(s.m, 5);
+    return s;
+  }
+  static constexpr bool uswz_ok() {
+    const Swz s = uswz();
+    return uswz_rounds_ok(s.m, 31);
+  }
+  __device__ static __forceinline__ uint32_t uswz_h(uint32_t e) {
+    constexpr Swz s = uswz();
+    uint32_t h = 0;
+#pragma unroll
+    for (int j = 5; j < TB; j++)
+      if (s.m[j]) h ^= ((e >> j) & 1u) ? s.m[j] : 0u;
+    return h;
+  }
+  // the wave's own LDS writes before its reads of other lanes' words (rocPRIM's wave_barrier)
+  __device__ static __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+
   // SWZ: 0 = the padded layout, 1 = the swizzled layout wherever it is conflict-free, 2 = the
-  // swizzled layout only where the padded one conflicts (fewer live address registers: the center)
+  // swizzled layout only where the padded one conflicts (fewer live address registers: the center),
+  // 3 = the padded layout with only the barriers above (one buffer), 4 = the same with the
+  // pass-wide swizzle uswz (conflict-free)
   template <int Q, bool INV, int SWZ>
   __device__ static __forceinline__ void exchange(uint32_t (&v)[E], uint32_t* buf, uint32_t bf, int lbf, uint32_t bt,
                                                   int lbt) {
     if (PLK_NTT_DIAG & 2) return;
+    if constexpr (SWZ == 4) {
+      static_assert(uswz_ok(), "no pass-wide conflict-free swizzle for this tile shape");
+      uint32_t xw4 = (bf ^ uswz_h(bf)) << 2, xr4 = (bt ^ uswz_h(bt)) << 2;
+      if (PLK_NTT_XCH_REMAT) {
+        asm volatile("" : "+v"(xw4));
+        asm volatile("" : "+v"(xr4));
+      }
+      char* bb = reinterpret_cast<char*>(buf);
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        const uint32_t ek = (uint32_t)k << lbf;
+        const uint32_t lo = ((ek & 31u) ^ uswz_h(ek)) << 2, hi = (ek & ~31u) << 2;
+        *reinterpret_cast<uint32_t*>(bb + (lo ? (xw4 ^ lo) : xw4) + hi) = v[k];
+      }
+      if constexpr (wave_local(Q, INV)) wave_sync();
+      else __syncthreads();
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        const uint32_t ek = (uint32_t)k << lbt;
+        const uint32_t lo = ((ek & 31u) ^ uswz_h(ek)) << 2, hi = (ek & ~31u) << 2;
+        v[k] = *reinterpret_cast<const uint32_t*>(bb + (lo ? (xr4 ^ lo) : xr4) + hi);
+      }
+      return;
+    }
+    if constexpr (SWZ == 3) {
+#pragma unroll
+      for (int k = 0; k < E; k++) buf[wphys((int)(bf + ((uint32_t)k << lbf)))] = v[k];
+      if constexpr (wave_local(Q, INV)) wave_sync();
+      else __syncthreads();
+#pragma unroll
+      for (int k = 0; k < E; k++) v[k] = buf[wphys((int)(bt + ((uint32_t)k << lbt)))];
+      return;
+    }
     if (PLK_NTT_SWZ && SWZ && swz_ok(Q, INV) && (SWZ == 1 || !pad_ok(Q, INV))) {
       // e = base | k << lb (disjoint bits) and h is linear: h(e) = h(base) ^ h(k << lb).  h only
       // moves bits < 5 and the bits >= 5 of k << lb are disjoint from base's, so the word is
@@ -594,7 +731,7 @@ struct Eng {
                                               const uint32_t* Tsm) {
     round<Q, INV, PW, TRIV0>(v, base_q<Q>(tid, INV), Tsm);
     if constexpr (Q + 1 < NR) {
-      exchange<Q, INV, SWZ>(v, bufs + (DBUF ? ((xc + Q) & 1) * BUF : 0), base_q<Q>(tid, INV), lbq(Q, INV),
+      exchange<Q, INV, SWZ>(v, bufs + (DBUF && SWZ < 3 ? ((xc + Q) & 1) * BUF : 0), base_q<Q>(tid, INV), lbq(Q, INV),
                             base_q<Q + 1>(tid, INV), lbq(Q + 1, INV));
       pass<INV, SWZ, PW, TRIV0, Q + 1>(v, tid, bufs, xc, Tsm);
     }
@@ -775,10 +912,15 @@ __global__ __launch_bounds__(wt_nt(TB), TB == 13 && M == TB ? 4 : 8) void wt_fwd
   if (FROM_U8 && PLK_NTT_BYTE_LUT && tid < 256) lut[tid] = F::byte_val(tid);
   if constexpr (PW) load_pass_tw_pairs<M, G::NT>(Tsm, tw.small);
   else load_pass_tw<M, G::NT>(Tsm, tw.small);
+  // exchange layout: the lo = 0 pass of a standalone transform may take the pass-wide swizzle
+  constexpr int XSWZ = M == TB && PLK_NTT_LO_USWZ ? 4 : 1;
+  // (xc continues over the arrays: with alternating buffers the one an array's first exchange
+  // writes was last read before the previous array's last exchange barrier -- no barrier needed)
+  constexpr bool ALT = PLK_NTT_ALT_ARRAYS && G::DBUF && XSWZ < 3;
   for (int q = 0;; q++) {
-    // (q = 0: the tables are in LDS; q > 0: every thread's reads of the previous array's last
-    // exchange are done before this one's first exchange writes)
-    __syncthreads();
+    // (q = 0: the tables are in LDS; q > 0 without ALT: every thread's reads of the previous
+    // array's last exchange are done before this one's first exchange writes)
+    if (q == 0 || !ALT) __syncthreads();
     if constexpr (FROM_U8 && PLK_NTT_BYTE_LUT) {
 #pragma unroll
       for (int k = 0; k < G::E; k++) v[k] = lut[v[k]];
@@ -788,7 +930,7 @@ __global__ __launch_bounds__(wt_nt(TB), TB == 13 && M == TB ? 4 : 8) void wt_fwd
     // butterflies (the barriers wait for LDS only: the loads stay in flight across them)
     uint32_t nv[G::E];
     if (PLK_NTT_PREFETCH && more) load(ai + 1, nv);
-    G::template pass<false, 1, PW, true>(v, tid, bufs, 0, Tsm);
+    G::template pass<false, XSWZ, PW, true>(v, tid, bufs, ALT ? q * G::XCH : 0, Tsm);
     const TileBuf bd(arrs.a[ai].d + tb);
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
@@ -918,6 +1060,8 @@ __global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs job
   const uint32_t bf = G::template base_q<G::NR - 1>(tid, true);
   const uint32_t of = G::toff(p, bf);
   const uint32_t N = 1u << p.k;   // (k <= 27: every index fits 32 bits)
+  constexpr int XSWZ = M == TB && PLK_NTT_LO_USWZ ? 4 : 1;
+  constexpr bool ALT = PLK_NTT_ALT_ARRAYS && G::DBUF && XSWZ < 3;
   for (int q = 0;; q++) {
     const WJob& jb = jobs.j[ji];   // (sum-group members are not in the grid: no inverse of their own)
     uint8_t* out8 = jb.out8;
@@ -947,9 +1091,10 @@ __global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs job
     // the next job's loads before this one's rounds (wt_fwd_kernel)
     uint32_t nv[G::E];
     if (PF && more) load(ji + 1, nv);
-    // (q = 0: the stage twiddles are in LDS; q > 0: the previous job's last exchange reads are done)
-    __syncthreads();
-    G::template pass<true>(v, tid, bufs, 0, Tsm);
+    // (q = 0: the stage twiddles are in LDS; q > 0 without ALT: the previous job's last exchange
+    // reads are done; with ALT the buffers alternate over the jobs, wt_fwd_kernel)
+    if (q == 0 || !ALT) __syncthreads();
+    G::template pass<true, XSWZ>(v, tid, bufs, ALT ? q * G::XCH : 0, Tsm);
     uint32_t last = 0;      // 1 + the largest index this thread left a non-zero byte at
     const uint32_t lim = out_len < N ? (uint32_t)out_len : N;
     const uint32_t ntop = (uint32_t)jb.ntop;   // (read once: the byte stores below may alias the job table)
@@ -1070,8 +1215,10 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
   using G = Eng<TB, R, TB, F>;
   static_assert(G::NT == wt_ntc(TB), "tile block size");
   static_assert(G::lbq(G::NR - 1, false) == 0 && G::lbq(0, true) == 0, "center mapping");
+  constexpr int CSWZ = TB == 13 ? PLK_NTT_CENTER_SWZ : PLK_NTT_CENTER_SWZ12;
+  constexpr bool UNI = CSWZ >= 3;   // one layout, barriers only where sets change (Eng::same_sets)
   __shared__ uint32_t Tlds[1 << TB];
-  __shared__ uint32_t bufs[(G::DBUF ? 2 : 1) * G::BUF];
+  __shared__ uint32_t bufs[(G::DBUF && !UNI ? 2 : 1) * G::BUF];
   const uint32_t* Tf = Tlds;
   const uint32_t tid = threadIdx.x;
   const uint32_t b0 = G::template base_q<0>(tid, false);
@@ -1117,16 +1264,21 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
         va[k] = pre ? pa[k] : b_a.ld(b0, (uint32_t)k << L0);   // (the per-register part in the SGPR offset)
         vb[k] = b_b.ld(b0, (uint32_t)k << L0);
       }
-      if (q == 0) __syncthreads();   // (the previous item's last exchange read)
+      // (the previous item's or pair's last exchange reads; with UNI the previous pair's too.
+      // Skipping it where Eng::same_sets allows -- the inverse's last round and the forward's first
+      // give the waves the same sets -- measured no faster: kept)
+      if (q == 0 || UNI) __syncthreads();
       // (afix / bfix: the operand's transform is finished -- plk_wave_pretransform / wt_fixfwd_kernel
       // stored this pass's output registers where their inputs were read -- so its pass is
       // skipped; xc counts the exchanges so that double buffers keep alternating)
       if (!P.afix) {
-        G::template pass<false, TB == 13 ? PLK_NTT_CENTER_SWZ : PLK_NTT_CENTER_SWZ12>(va, tid, bufs, xc, Tf);
+        G::template pass<false, CSWZ>(va, tid, bufs, xc, Tf);
         xc += G::XCH;
       }
       if (!P.bfix) {
-        G::template pass<false, TB == 13 ? PLK_NTT_CENTER_SWZ : PLK_NTT_CENTER_SWZ12>(vb, tid, bufs, xc, Tf);
+        // (UNI: a's last reads against b's first writes)
+        if (UNI && !P.afix && !G::same_sets(G::NR - 1, false, 0, false)) __syncthreads();
+        G::template pass<false, CSWZ>(vb, tid, bufs, xc, Tf);
         xc += G::XCH;
       }
 #pragma unroll
@@ -1152,7 +1304,9 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
         for (int k = 0; k < G::E; k++) pa[k] = b_n.ld(b0, (uint32_t)k << L0);
       }
     }
-    G::template pass<true, TB == 13 ? PLK_NTT_CENTER_SWZ : PLK_NTT_CENTER_SWZ12>(va, tid, bufs, xc, Tf);
+    // (UNI: the forward passes' last reads against the inverse pass's first writes)
+    if (UNI && !G::same_sets(G::NR - 1, false, 0, true)) __syncthreads();
+    G::template pass<true, CSWZ>(va, tid, bufs, xc, Tf);
 #pragma unroll
     for (int k = 0; k < G::E; k++) b_c.st(bf, (uint32_t)k << LF, va[k]);
   }
@@ -1166,9 +1320,11 @@ template <int TB, int R, class F>
 __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_fixfwd_kernel(WPass p, WArrs arrs,
                                                                                                     WTw twf) {
   using G = Eng<TB, R, TB, F>;
+  constexpr int CSWZ0 = TB == 13 ? PLK_NTT_CENTER_SWZ : PLK_NTT_CENTER_SWZ12;
+  constexpr int CSWZ = CSWZ0 >= 3 ? CSWZ0 : 0;
   uint32_t* d = arrs.a[blockIdx.y].d;
   __shared__ uint32_t Tlds[1 << TB];
-  __shared__ uint32_t bufs[(G::DBUF ? 2 : 1) * G::BUF];
+  __shared__ uint32_t bufs[(G::DBUF && CSWZ < 3 ? 2 : 1) * G::BUF];
   const uint32_t tid = threadIdx.x, tile = blockIdx.x;
   const uint32_t b0 = G::template base_q<0>(tid, false);
   constexpr int L0 = G::lbq(0, false);
@@ -1178,7 +1334,7 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_fi
   for (int k = 0; k < G::E; k++) v[k] = bt.ld(b0, (uint32_t)k << L0);
   load_pass_tw<TB, G::NT>(Tlds, twf.small);
   __syncthreads();
-  G::template pass<false, false>(v, tid, bufs, G::XCH, Tlds);
+  G::template pass<false, CSWZ>(v, tid, bufs, G::XCH, Tlds);
 #pragma unroll
   for (int k = 0; k < G::E; k++) bt.st(b0, (uint32_t)k << L0, v[k]);
 }
