@@ -76,6 +76,12 @@ namespace {
 // passes 46.8 / 39.2 -> 45.2 / 38.4 us, inverse M = 8 31.1 -> 30.4 us, prove median -0.5..1 %)
 #define PLK_NTT_DBUF13 1
 #endif
+#ifndef PLK_NTT_CENTER12_2BUF
+#define PLK_NTT_CENTER12_2BUF 0   // the 2^12 centre's b pass in its own buffer (no barrier between a's and b's passes)
+#endif
+#ifndef PLK_NTT_TRIBUF
+#define PLK_NTT_TRIBUF 0       // swizzled double-buffered passes: a third buffer lets wave-local exchanges skip their barrier
+#endif
 #ifndef PLK_NTT_ALT_ARRAYS
 // pass kernels: exchange buffers alternate across a block's arrays, no barrier between arrays (round 5:
 // prove median 0.373-0.397 vs 0.377-0.387 ms, four alternations -- off)
@@ -628,6 +634,21 @@ struct Eng {
       if (s.m[j]) h ^= ((e >> j) & 1u) ? s.m[j] : 0u;
     return h;
   }
+  // Three exchange buffers rotating (PLK_NTT_TRIBUF, swizzled double-buffered passes): a wave-local
+  // exchange then needs no barrier -- its words are its own wave's, and the block exchanges on
+  // either side (the reads of the one before, the writes of the one after, which can run beside it
+  // in other waves) use the other two buffers.  Only where no two wave-local exchanges follow each
+  // other (longer runs would need more buffers): the 2^12-tile high passes of 7-8 bits.
+  static constexpr int wl_run(bool inv) {
+    int mx = 0, run = 0;
+    for (int q = 0; q + 1 < NR; q++) {
+      run = wave_local(q, inv) ? run + 1 : 0;
+      mx = run > mx ? run : mx;
+    }
+    return mx;
+  }
+  static constexpr bool tri(bool inv) { return PLK_NTT_TRIBUF && DBUF && wl_run(inv) == 1; }
+  static constexpr int nbuf() { return XCH == 0 ? 1 : (tri(false) || tri(true) ? 3 : (NBUF ? NBUF : 1)); }
   // the wave's own LDS writes before its reads of other lanes' words (rocPRIM's wave_barrier)
   __device__ static __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -695,7 +716,8 @@ struct Eng {
         const uint32_t lo = ((ek & 31u) ^ swz_h<Q, INV>(ek)) << 2, hi = (ek & ~31u) << 2;
         *reinterpret_cast<uint32_t*>(bb + (lo ? (xw4 ^ lo) : xw4) + hi) = v[k];
       }
-      __syncthreads();
+      if constexpr (tri(INV) && wave_local(Q, INV)) wave_sync();
+      else __syncthreads();
 #pragma unroll
       for (int k = 0; k < E; k++) {
         const uint32_t ek = (uint32_t)k << lbt;
@@ -716,7 +738,8 @@ struct Eng {
     }
 #pragma unroll
     for (int k = 0; k < E; k++) buf[wphys((int)(bf + ((uint32_t)k << lbf)))] = v[k];
-    __syncthreads();
+    if constexpr (tri(INV) && wave_local(Q, INV) && SWZ < 3) wave_sync();
+    else __syncthreads();
 #pragma unroll
     for (int k = 0; k < E; k++) v[k] = buf[wphys((int)(bt + ((uint32_t)k << lbt)))];
     if (!DBUF) __syncthreads();
@@ -731,7 +754,8 @@ struct Eng {
                                               const uint32_t* Tsm) {
     round<Q, INV, PW, TRIV0>(v, base_q<Q>(tid, INV), Tsm);
     if constexpr (Q + 1 < NR) {
-      exchange<Q, INV, SWZ>(v, bufs + (DBUF && SWZ < 3 ? ((xc + Q) & 1) * BUF : 0), base_q<Q>(tid, INV), lbq(Q, INV),
+      exchange<Q, INV, SWZ>(v, bufs + (!DBUF || SWZ >= 3 ? 0 : (tri(INV) ? ((xc + Q) % 3) : ((xc + Q) & 1)) * BUF),
+                            base_q<Q>(tid, INV), lbq(Q, INV),
                             base_q<Q + 1>(tid, INV), lbq(Q + 1, INV));
       pass<INV, SWZ, PW, TRIV0, Q + 1>(v, tid, bufs, xc, Tsm);
     }
@@ -845,7 +869,7 @@ __global__ __launch_bounds__(wt_nt(TB), TB == 13 && M == TB ? 4 : 8) void wt_fwd
   static_assert(G::NT == wt_nt(TB), "tile block size");
   constexpr bool PW = F::ADIC == f29::TWO_ADICITY;   // {w, p - w} pairs (F29's lazy DIF)
   __shared__ __attribute__((aligned(16))) uint32_t Tsm[(PW ? 2 : 1) << M];
-  __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
+  __shared__ uint32_t bufs[G::nbuf() * G::BUF];
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
 
@@ -1020,7 +1044,7 @@ __global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs job
   // spill reloads would wait for the prefetched loads anyway)
   constexpr bool PF = PLK_NTT_PREFETCH_INV && !(TO_U8 && (M > 8 || M < 4));
   __shared__ uint32_t Tsm[1 << M];
-  __shared__ uint32_t bufs[G::NBUF == 0 ? 1 : G::NBUF * G::BUF];
+  __shared__ uint32_t bufs[G::nbuf() * G::BUF];
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = block_tile();
 
@@ -1217,8 +1241,13 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
   static_assert(G::lbq(G::NR - 1, false) == 0 && G::lbq(0, true) == 0, "center mapping");
   constexpr int CSWZ = TB == 13 ? PLK_NTT_CENTER_SWZ : PLK_NTT_CENTER_SWZ12;
   constexpr bool UNI = CSWZ >= 3;   // one layout, barriers only where sets change (Eng::same_sets)
+  // (UNI, 2^12 tiles, PLK_NTT_CENTER12_2BUF) b's pass in a buffer of its own: a's last reads and b's
+  // first writes cannot meet, so no barrier between the two forward passes (the inverse pass, back in
+  // a's buffer, starts after b's first barrier, when every wave has left a's pass)
+  constexpr bool B2 = UNI && TB == 12 && PLK_NTT_CENTER12_2BUF;
+  static_assert(!B2 || !G::wave_local(0, false), "b's first exchange must carry the barrier that ends a's pass");
   __shared__ uint32_t Tlds[1 << TB];
-  __shared__ uint32_t bufs[(G::DBUF && !UNI ? 2 : 1) * G::BUF];
+  __shared__ uint32_t bufs[(G::DBUF && (!UNI || B2) ? 2 : 1) * G::BUF];
   const uint32_t* Tf = Tlds;
   const uint32_t tid = threadIdx.x;
   const uint32_t b0 = G::template base_q<0>(tid, false);
@@ -1277,8 +1306,8 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
       }
       if (!P.bfix) {
         // (UNI: a's last reads against b's first writes)
-        if (UNI && !P.afix && !G::same_sets(G::NR - 1, false, 0, false)) __syncthreads();
-        G::template pass<false, CSWZ>(vb, tid, bufs, xc, Tf);
+        if (UNI && !B2 && !P.afix && !G::same_sets(G::NR - 1, false, 0, false)) __syncthreads();
+        G::template pass<false, CSWZ>(vb, tid, B2 ? bufs + G::BUF : bufs, xc, Tf);
         xc += G::XCH;
       }
 #pragma unroll
