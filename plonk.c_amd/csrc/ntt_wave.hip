@@ -76,6 +76,13 @@ namespace {
 // passes 46.8 / 39.2 -> 45.2 / 38.4 us, inverse M = 8 31.1 -> 30.4 us, prove median -0.5..1 %)
 #define PLK_NTT_DBUF13 1
 #endif
+#ifndef PLK_NTT_CENTER_PW
+// F29 centres' twiddles as {w, p - w} pairs (no subtraction in the forward DIF): bit 0 = 2^12 tiles
+// (round 5: poly_mul 2^19 x 2^19 23.62-23.72 -> 23.34-23.48 us, three alternations), bit 1 = 2^13
+// tiles with 2^11 pairs (spills 24-32 B/lane at its 64-VGPR budget: prove median 0.383-0.390 ->
+// 0.405-0.417 ms -- off)
+#define PLK_NTT_CENTER_PW 1
+#endif
 #ifndef PLK_NTT_CENTER12_2BUF
 #define PLK_NTT_CENTER12_2BUF 0   // the 2^12 centre's b pass in its own buffer (no barrier between a's and b's passes)
 #endif
@@ -412,7 +419,9 @@ struct Eng {
   // multiply there (its x inputs are < 2p, F::dit1), DIF when TRIV0 (a forward pass whose
   // outputs go to the column multiply or the canonical store, F::dif1).  PW: the table holds
   // {w, p - w} pairs (F29 DIF without the subtraction).
-  template <int Q, bool INV, bool PW = false, bool TRIV0 = false>
+  // PWB (the centre's mixed table, PW false): stages s < PWB read {w, p - w} pairs at uint2 index
+  // 2^s + r, the others single words at 2^s + r + 2^PWB (0: single words everywhere)
+  template <int Q, bool INV, bool PW = false, bool TRIV0 = false, int PWB = 0>
   __device__ static __forceinline__ void round(uint32_t (&v)[E], uint32_t b, const uint32_t* Tsm) {
     if (PLK_NTT_DIAG & 1) return;
     constexpr int LB = lbq(Q, INV), SL = s_lo(Q, INV), SH = s_hi(Q, INV);
@@ -444,7 +453,13 @@ struct Eng {
           F::difp(v[k], v[k | (1 << q)], wp.x, wp.y, red);
           continue;
         }
-        const uint32_t w = Tsm[(1u << s) + rr];
+        if (s < PWB) {   // (compile-time after unrolling)
+          const uint2 wp = reinterpret_cast<const uint2*>(Tsm)[(1u << s) + rr];
+          if (!INV) F::difp(v[k], v[k | (1 << q)], wp.x, wp.y, red);
+          else F::dit(v[k], v[k | (1 << q)], wp.x, red);
+          continue;
+        }
+        const uint32_t w = Tsm[(1u << s) + rr + (PWB ? (1u << PWB) : 0u)];
         if (!INV) F::dif(v[k], v[k | (1 << q)], w, red);
         else F::dit(v[k], v[k | (1 << q)], w, red);
       }
@@ -749,15 +764,15 @@ struct Eng {
   // last round on exit.  xc selects the exchange buffer (it counts exchanges).
   // SWZ: the swizzled exchange layout where it is conflict-free (the center kernel passes false:
   // it has no VGPRs to spare for the two extra base registers)
-  template <bool INV, int SWZ = 1, bool PW = false, bool TRIV0 = false, int Q = 0>
+  template <bool INV, int SWZ = 1, bool PW = false, bool TRIV0 = false, int PWB = 0, int Q = 0>
   __device__ static __forceinline__ void pass(uint32_t (&v)[E], uint32_t tid, uint32_t* bufs, int xc,
                                               const uint32_t* Tsm) {
-    round<Q, INV, PW, TRIV0>(v, base_q<Q>(tid, INV), Tsm);
+    round<Q, INV, PW, TRIV0, PWB>(v, base_q<Q>(tid, INV), Tsm);
     if constexpr (Q + 1 < NR) {
       exchange<Q, INV, SWZ>(v, bufs + (!DBUF || SWZ >= 3 ? 0 : (tri(INV) ? ((xc + Q) % 3) : ((xc + Q) & 1)) * BUF),
                             base_q<Q>(tid, INV), lbq(Q, INV),
                             base_q<Q + 1>(tid, INV), lbq(Q + 1, INV));
-      pass<INV, SWZ, PW, TRIV0, Q + 1>(v, tid, bufs, xc, Tsm);
+      pass<INV, SWZ, PW, TRIV0, PWB, Q + 1>(v, tid, bufs, xc, Tsm);
     }
   }
 
@@ -838,6 +853,22 @@ __device__ __forceinline__ void load_pass_tw(uint32_t* Tsm, const uint32_t* smal
   for (int i = 0; i < ((1 << M) + NT - 1) / NT; i++) {
     const int j = i * NT + (int)threadIdx.x;
     if (j < (1 << M)) Tsm[j] = bs.ld((uint32_t)j);
+  }
+}
+
+// the centre's mixed table (Eng::round's PWB): {w, p - w} pairs for the first 2^PWB entries, the
+// others as single words at their index + 2^PWB (2^TB + 2^PWB words)
+template <int TB, int PWB, int NT>
+__device__ __forceinline__ void load_center_tw(uint32_t* T, const uint32_t* small) {
+  const TileBuf bs(small);
+#pragma unroll
+  for (int i = 0; i < ((1 << TB) + NT - 1) / NT; i++) {
+    const int j = i * NT + (int)threadIdx.x;
+    if (j < (1 << TB)) {
+      const uint32_t w = bs.ld((uint32_t)j);
+      if (j < (1 << PWB)) reinterpret_cast<uint2*>(T)[j] = make_uint2(w, f29::P - w);
+      else T[j + (1 << PWB)] = w;
+    }
   }
 }
 
@@ -1246,7 +1277,11 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
   // a's buffer, starts after b's first barrier, when every wave has left a's pass)
   constexpr bool B2 = UNI && TB == 12 && PLK_NTT_CENTER12_2BUF;
   static_assert(!B2 || !G::wave_local(0, false), "b's first exchange must carry the barrier that ends a's pass");
-  __shared__ uint32_t Tlds[1 << TB];
+  // (F29, PLK_NTT_CENTER_PW) the twiddle table's low stages as {w, p - w} pairs: the forward DIF
+  // skips its p - w subtraction there; 2^11 pairs for 2^13 tiles keep two blocks per CU in LDS
+  constexpr int CPWB = F::ADIC != f29::TWO_ADICITY ? 0
+                       : TB == 13 ? ((PLK_NTT_CENTER_PW & 2) ? 11 : 0) : ((PLK_NTT_CENTER_PW & 1) ? TB : 0);
+  __shared__ __attribute__((aligned(16))) uint32_t Tlds[(1 << TB) + (CPWB ? (1 << CPWB) : 0)];
   __shared__ uint32_t bufs[(G::DBUF && (!UNI || B2) ? 2 : 1) * G::BUF];
   const uint32_t* Tf = Tlds;
   const uint32_t tid = threadIdx.x;
@@ -1261,7 +1296,8 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
   if (blockIdx.x == 0 && tid < (uint32_t)sc.nj && jobs.j[tid].nz) *jobs.j[tid].nz = 0u;
   // the twiddle table first (a "first item" flag inside the loop had the compiler hoist the
   // table's addresses out of the loop and spill them)
-  load_pass_tw<TB, G::NT>(Tlds, twf.small);
+  if constexpr (CPWB) load_center_tw<TB, CPWB, G::NT>(Tlds, twf.small);
+  else load_pass_tw<TB, G::NT>(Tlds, twf.small);
   // the item after `it` in this block's stride that has a job (items of padding slots skipped)
   auto next_item = [&](uint32_t it) {
     for (it += gridDim.x; it < items && sc.job[it / tiles] < 0; it += gridDim.x) {
@@ -1301,13 +1337,13 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
       // stored this pass's output registers where their inputs were read -- so its pass is
       // skipped; xc counts the exchanges so that double buffers keep alternating)
       if (!P.afix) {
-        G::template pass<false, CSWZ>(va, tid, bufs, xc, Tf);
+        G::template pass<false, CSWZ, false, false, CPWB>(va, tid, bufs, xc, Tf);
         xc += G::XCH;
       }
       if (!P.bfix) {
         // (UNI: a's last reads against b's first writes)
         if (UNI && !B2 && !P.afix && !G::same_sets(G::NR - 1, false, 0, false)) __syncthreads();
-        G::template pass<false, CSWZ>(vb, tid, B2 ? bufs + G::BUF : bufs, xc, Tf);
+        G::template pass<false, CSWZ, false, false, CPWB>(vb, tid, B2 ? bufs + G::BUF : bufs, xc, Tf);
         xc += G::XCH;
       }
 #pragma unroll
@@ -1335,7 +1371,7 @@ __global__ __launch_bounds__(wt_ntc(TB), TB == 13 ? PLK_NTT_CW13 : 1) void wt_ce
     }
     // (UNI: the forward passes' last reads against the inverse pass's first writes)
     if (UNI && !G::same_sets(G::NR - 1, false, 0, true)) __syncthreads();
-    G::template pass<true, CSWZ>(va, tid, bufs, xc, Tf);
+    G::template pass<true, CSWZ, false, false, CPWB>(va, tid, bufs, xc, Tf);
 #pragma unroll
     for (int k = 0; k < G::E; k++) b_c.st(bf, (uint32_t)k << LF, va[k]);
   }
