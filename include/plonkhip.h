@@ -82,7 +82,9 @@ enum {
   PLK_OPT_MSM_HOST_LANES = 17,   /* one device: plk_msm_g1 of >= MSM_SHARD_MIN points runs its SRS memcmp,
                                     staging and uploads on this many host threads (1: one); read by
                                     plk_init / plk_init_devices */
-  PLK_OPT_PROVE_DERIVE_T2A = 18, /* 1: round 3's A2 B2 from a_x b_x by an elementwise pass (0: its own product) */
+  PLK_OPT_PROVE_DERIVE_T2A = 18, /* 1: round 3's A2 B2 from a_x b_x by an elementwise pass (0: its own product;
+                                    2, the default: that pass inside the t_2 product's first forward pass when
+                                    it runs on 2^13 tiles -- one launch fewer -- else as 1) */
   PLK_OPT_NTT_TABLE_SHARE = 19,  /* 1: a table pass runs several arrays of one tile per block (column words read once) */
   PLK_OPT_NTT_LAUNCH_LOG = 20,   /* diagnostics: 1 records the NTT passes' launch plans (plk_ntt_launch_log) */
   PLK_OPT_PROVE_FUSE_DIV = 21,   /* 1: round 5's numerators and their divisions by x - z, x - z omega in one
@@ -100,7 +102,10 @@ enum {
   PLK_OPT_PROVE_EVAL_AGG = 26,   /* 1: round 4's evaluation rows also store round 5's scan-chunk aggregates, so
                                     both round-5 divisions finish in ONE launch (lincomb_agg_divide_kernel);
                                     0: the numerators + aggregates launch, then the apply launch */
-  PLK_OPT_COUNT = 27
+  PLK_OPT_PROVE_GRAPH = 27,      /* 1: plk_prover_rounds_dev replays its launches as a HIP graph captured on the
+                                    first call with the same input addresses, preprocessed state and options
+                                    (per call only the scalar file and the completion word are set) */
+  PLK_OPT_COUNT = 28
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
 /* Diagnostics for the offline roofline tools: with PLK_OPT_NTT_LAUNCH_LOG = 1 every NTT pass launch

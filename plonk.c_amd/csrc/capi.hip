@@ -472,7 +472,7 @@ const OptDef kOpt[PLK_OPT_COUNT] = {
     {1 << 16, 1, 1ll << 40, false},            // MSM_SHARD_MIN
     {1, 0, 1, false},                          // NTT_CENTER_SUM
     {4, 1, PLK_MAX_SHARDS, false},             // MSM_HOST_LANES (read at plk_init / plk_init_devices)
-    {1, 0, 1, false},                          // PROVE_DERIVE_T2A
+    {2, 0, 2, false},                          // PROVE_DERIVE_T2A (2: in the t_2 product's first pass)
     {1, 0, 1, false},                          // NTT_TABLE_SHARE
     {0, 0, 1, false},                          // NTT_LAUNCH_LOG
     {0, 0, 1, false},                          // PROVE_FUSE_DIV (measured slower)
@@ -481,6 +481,7 @@ const OptDef kOpt[PLK_OPT_COUNT] = {
     {1, 0, 2, false},                          // PROVE_EARLY_COMMITS (2: in round 4's evaluation launch)
     {0, 0, 1, false},                          // PROVE_HELPER_COPY (tests: the distinct-device input path on one GPU)
     {1, 0, 1, false},                          // PROVE_EVAL_AGG
+    {0, 0, 1, false},                          // PROVE_GRAPH
 };
 struct Opts {
   std::atomic<int64_t> v[PLK_OPT_COUNT];

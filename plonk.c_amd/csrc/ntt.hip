@@ -694,6 +694,7 @@ static int ntt_group(const PlkPolyMulJob* g, int m, int k, const uint64_t* es, v
                 W + ((size_t)cslot[i] << k)};
     w[i].ntop = (int)e;
     w[i].bfix = fixb[i] ? 1 : 0;
+    w[i].der = j.der;
   }
   if (m == 1) w[0].nz = d_nz;
   // sum groups: a member (acc) adds its center output into its leader's first inverse pass
@@ -881,6 +882,10 @@ int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, s
       }
       ks[i] = k;
       continue;
+    }
+    if (j.der) {   // (the derived bytes come from the wave engine's first forward pass)
+      plk_set_error("poly_mul batch: job %d derives its operand but is not a transform-sized product", i);
+      return PLK_ERR_ARG;
     }
     const int rc = plk_poly_mul_launch(j.a, j.la, j.b, j.lb, j.out, nullptr, nullptr, st);
     if (rc) return rc;

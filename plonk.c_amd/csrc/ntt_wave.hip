@@ -124,6 +124,9 @@ namespace {
 #ifndef PLK_NTT_M17
 #define PLK_NTT_M17 1          // COLT byte outputs: 1 = mod 17 of the index through an LDS table, 0 = 24-bit arithmetic
 #endif
+#ifndef PLK_NTT_DERIVE
+#define PLK_NTT_DERIVE 1       // 2^13-tile first forward passes compute a derived operand (WArrs::derive); 0: compiled out
+#endif
 #ifndef PLK_NTT_U8_KRSRC
 #define PLK_NTT_U8_KRSRC 0     // byte loads: one buffer resource per register index (one offset VGPR)
 #endif
@@ -209,6 +212,8 @@ struct WArr {
 constexpr int WT_MAX_ARRS = 2 * WT_MAX_JOBS;
 struct WArrs {
   WArr a[WT_MAX_ARRS];
+  int derive = 0;   // 1: array 0's bytes are WDerive dv of a[0].s8 (first forward pass only)
+  WDerive dv{};
 };
 
 struct WTw {
@@ -885,6 +890,42 @@ __device__ __forceinline__ void load_pass_tw_pairs(uint32_t* Tsm, const uint32_t
   }
 }
 
+// Array 0 of a derived batch (WArrs::derive): the bytes of round 3's A2 B2 at the elements this
+// thread loads (WDerive; the same map as prove.hip's t2a_kernel, exact mod 17), also stored to the
+// operand's bytes ar.s8 [0, ar.ls).  Byte offsets are element indices (< 2^27); a[i - 1] at i = 0
+// is the offset 2^32 - 1, out of every range: 0.
+template <class G>
+__device__ __forceinline__ void load_derived(const WArrs& arrs, WPass p, uint64_t tb, uint32_t o0, uint32_t b0,
+                                             uint32_t (&v)[G::E]) {
+  const WDerive& dv = arrs.dv;
+  const WArr& ar = arrs.a[0];
+  const uint32_t al = dv.S[dv.s_alpha], be = dv.S[dv.s_beta], ga = dv.S[dv.s_gamma], bk1 = dv.S[dv.s_bk1];
+  const TileBuf bab(dv.ab, (uint32_t)(dv.lab < 0x7FFFFFF0ull ? dv.lab : 0x7FFFFFF0ull));
+  const TileBuf ba(dv.a, (uint32_t)(dv.la < 0x7FFFFFF0ull ? dv.la : 0x7FFFFFF0ull));
+  const TileBuf bb(dv.b, (uint32_t)(dv.la < 0x7FFFFFF0ull ? dv.la : 0x7FFFFFF0ull));
+  const TileBuf bo(ar.s8, (uint32_t)(ar.ls < 0x7FFFFFF0ull ? ar.ls : 0x7FFFFFF0ull));
+  uint32_t ix[G::E], wab[G::E], ak[G::E], bk[G::E], am[G::E], bm[G::E];
+#pragma unroll
+  for (int k = 0; k < G::E; k++) {
+    ix[k] = (uint32_t)tb + G::template toff_k<0, false>(p, o0, b0, k);
+    wab[k] = bab.ldb(ix[k]);
+    ak[k] = ba.ldb(ix[k]);
+    bk[k] = bb.ldb(ix[k]);
+    am[k] = ba.ldb(ix[k] - 1u);
+    bm[k] = bb.ldb(ix[k] - 1u);
+  }
+#pragma unroll
+  for (int k = 0; k < G::E; k++) {
+    const uint32_t i = ix[k];
+    // (gamma + beta x)(gamma + beta k1 x) at x^0, x^1, x^2
+    const uint32_t K = i == 0 ? ga * ga : i == 1 ? ga * (bk1 + be) : i == 2 ? be * bk1 : 0u;
+    // (bound: 16 + 16 * 32 + 2 * 16 * 16 + 289 < 2^11)
+    const uint32_t x = wab[k] + ga * (ak[k] + bk[k]) + bk1 * am[k] + be * bm[k] + K;
+    v[k] = (x % 17u) * al % 17u;
+    bo.stb(i, v[k]);
+  }
+}
+
 }  // namespace
 
 // Forward (DIF) pass over a batch's distinct arrays, u32 in place, or the first pass reading
@@ -944,7 +985,12 @@ __global__ __launch_bounds__(wt_nt(TB), TB == 13 && M == TB ? 4 : 8) void wt_fwd
   };
   int ai = (int)blockIdx.y * apa;
   uint32_t v[G::E];
-  load(ai, v);   // (the first array's loads go out before the tables')
+  // (the first array's loads go out before the tables'; a derived array is array 0, so only a
+  // block's first load can be one -- never a prefetch)
+  // (2^13 tiles only: the 2^12-tile byte passes -- C3's poly_mul -- keep their registers, 36 VGPRs
+  // instead of 40: poly_mul 2^19 x 2^19 +0.3 us with the branch compiled in)
+  if (PLK_NTT_DERIVE && TB == 13 && FROM_U8 && ai == 0 && arrs.derive) load_derived<G>(arrs, p, tb, o0, b0, v);
+  else load(ai, v);
   // column factor table words of the elements this thread stores (HIGH passes): the same for
   // every array of the block
   constexpr int LF = G::lbq(G::NR - 1, false);
@@ -1697,6 +1743,20 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
       for (int q = 0; q < na; q++) seen |= arrs.a[q].d == a.d;
       if (!seen) arrs.a[na++] = a;
     }
+  // a derived operand (PlkPolyMulJob::der) becomes array 0: the first forward pass computes it
+  for (int j = 0; j < nj; j++) {
+    if (!jobs.j[j].der) continue;
+    int q = 0;
+    while (q < na && arrs.a[q].d != jobs.j[j].A) q++;
+    if (!PLK_NTT_DERIVE || TB != 13 || arrs.derive || np < 2 || q == na || jobs.j[j].der->la < 1) {
+      plk_set_error("wave poly_mul: a derived operand needs 2^13 tiles, one per batch and two or more passes "
+                    "(2^%d: %d-bit tiles, %d passes)", k, TB, np);
+      return PLK_ERR_ARG;
+    }
+    std::swap(arrs.a[0], arrs.a[q]);
+    arrs.derive = 1;
+    arrs.dv = *jobs.j[j].der;
+  }
   int rc;
   PLK_MARK(5);
   for (int i = 0; i < np - 1; i++) {

@@ -91,6 +91,21 @@ int plk_poly_mul_launch(const uint8_t* d_a, uint64_t la, const uint8_t* d_b, uin
                         uint32_t* d_nz, void* d_work, hipStream_t st);
 int plk_ntt_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st);
 int plk_ntt29_launch(uint32_t* d, int k, int batch, int inverse, hipStream_t st);
+// Operand a of a product as an elementwise function of other bytes, computed by the wave
+// engine's first forward pass (which also stores the bytes to a[0, la): the last inverse pass's
+// top-coefficient terms read them): round 3's
+//   A2 B2 = alpha (ab + gamma (a + b) + beta k1 x a + beta x b + (gamma + beta x)(gamma + beta k1 x))
+// (src/plonk.h:409-434; prove.hip t2a_kernel is the same map as a launch of its own), the
+// challenges read from the prover's scalar slots S at run time
+struct WDerive {
+  const uint8_t* ab;   // a_x b_x, [0, lab)
+  const uint8_t* a;    // a_x, b_x, [0, la)
+  const uint8_t* b;
+  const uint8_t* S;
+  uint64_t la, lab;
+  int s_alpha, s_beta, s_gamma, s_bk1;   // slots of alpha, beta, gamma, beta k1 in S
+};
+
 struct PlkPolyMulJob {
   const uint8_t* a;
   uint64_t la;
@@ -106,6 +121,9 @@ struct PlkPolyMulJob {
   // which skips b's forward passes; ignored otherwise (the product is the same either way)
   const uint32_t* bt = nullptr;
   int bt_k = 0, bt_field = -1;
+  // optional: a's bytes derived in the first forward pass (WDerive; wave-engine products of two
+  // or more passes only, one per batch: PLK_ERR_ARG otherwise)
+  const WDerive* der = nullptr;
 };
 int plk_poly_mul_batch_launch(const PlkPolyMulJob* jobs, int nj, void* d_work, size_t work_bytes, hipStream_t st);
 bool plk_poly_mul_summable(uint64_t la, uint64_t lb);
@@ -151,6 +169,7 @@ struct WJob {
   int cm[2] = {-1, -1};
   int ncm = 0;
   int cskip = 0;
+  const WDerive* der = nullptr;    // (host side only: PlkPolyMulJob::der, read at launch)
 };
 constexpr int PLK_WAVE_MAX_JOBS = 12;   // jobs per launch of the wave engine (larger batches run in chunks)
 bool plk_wave_ntt_supported(int k);

@@ -1716,6 +1716,20 @@ struct plk_prover {
   // as a helper on another device: its copies of the 7 input polynomials it reads
   uint8_t* hin = nullptr;
   hipEvent_t ev_done = nullptr;          // (helper's device) its products have reached the proving device
+  // plk_prover_rounds_dev as a captured HIP graph (PLK_OPT_PROVE_GRAPH, rounds_graph): replayed
+  // while the inputs' addresses, the preprocessed transforms (fix_gen) and every option are the
+  // ones it was captured with; per call the first kernel's scalar file and the last kernel's
+  // completion word are set as node parameters
+  hipGraph_t g = nullptr;
+  hipGraphExec_t gx = nullptr;
+  hipGraphNode_t g_first = nullptr, g_last = nullptr;
+  int g_first_arg = -1, g_first_n = 0;
+  const uint8_t* g_pl[13] = {};
+  bool g_pre = false;
+  uint32_t fix_gen = 0, g_fix_gen = 0;
+  int64_t g_opt[PLK_OPT_COUNT] = {};
+  uint32_t g_seq = 0;              // the completion word the graph's last kernel writes
+  SlotFile g_sf{};                 // the scalar file its first kernel holds
 };
 
 namespace {
@@ -2206,6 +2220,7 @@ int create_on(const plk_plonk_desc_t* d, int dev, plk_prover_t** out) {
 
 void detach_helpers(plk_prover* P);
 
+void drop_graph(plk_prover* P);   // (rounds_graph)
 }  // namespace
 
 extern "C" {
@@ -2218,6 +2233,7 @@ void plk_prover_destroy(plk_prover_t* P) {
   DevGuard dg;
   (void)hipSetDevice(P->dev);
   if (P->st) (void)hipStreamSynchronize(P->st);
+  drop_graph(P);
   (void)hipFree(P->mem);
   if (P->h_res) (void)hipHostFree(P->h_res);
   (void)hipFree(P->fix_mem);
@@ -2260,13 +2276,9 @@ MsmRowLens msm_row_lens(const plk_prover* P, const Lens& L) {
   return r;
 }
 
-int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const uint8_t rnd[9], bool pre = false,
-           const RoundsMode& md = RoundsMode{}) {
-  const uint64_t n = P->n;
-  const Lens L = lens_for(n, P->zh_len);
-  const uint8_t *FA = pl[0], *FB = pl[1], *FC = pl[2], *QO = pl[3], *QM = pl[4], *QL = pl[5], *QR = pl[6],
-                *QC = pl[7], *S1 = pl[8], *S2 = pl[9], *S3 = pl[10], *ACC = pl[11], *L1 = pl[12];
-  // scalar file: challenges, constants and host-derivable powers (src/plonk.h:237-247)
+// scalar file: challenges, constants and host-derivable powers (src/plonk.h:237-247), and the
+// blinding polynomials' coefficients
+SlotFile make_slotfile(uint64_t n, const uint8_t chal[5], const uint8_t rnd[9]) {
   SlotFile sf{};
   uint8_t* S = sf.b;
   const uint32_t al = chal[0] % HFP, be = chal[1] % HFP, ga = chal[2] % HFP, z = chal[3] % HFP, v = chal[4] % HFP;
@@ -2284,6 +2296,16 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
   S[P_BLB] = rnd[3] % HFP; S[P_BLB + 1] = rnd[2] % HFP;
   S[P_BLC] = rnd[5] % HFP; S[P_BLC + 1] = rnd[4] % HFP;
   S[P_BLZ] = rnd[8] % HFP; S[P_BLZ + 1] = rnd[7] % HFP; S[P_BLZ + 2] = rnd[6] % HFP;
+  return sf;
+}
+
+int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const uint8_t rnd[9], bool pre = false,
+           const RoundsMode& md = RoundsMode{}) {
+  const uint64_t n = P->n;
+  const Lens L = lens_for(n, P->zh_len);
+  const uint8_t *FA = pl[0], *FB = pl[1], *FC = pl[2], *QO = pl[3], *QM = pl[4], *QL = pl[5], *QR = pl[6],
+                *QC = pl[7], *S1 = pl[8], *S2 = pl[9], *S3 = pl[10], *ACC = pl[11], *L1 = pl[12];
+  const SlotFile sf = make_slotfile(n, chal, rnd);
   // status: stage-A words (gate/copy/acc) are owned by the circuit path; reset the rest
   // (the aligned path's prep_kernel stores the scalar file and clears the status words itself)
   const uint8_t* ins[8] = {P->d_zh, pl[0], pl[1], pl[2], pl[11], pl[8], pl[9], pl[10]};
@@ -2401,6 +2423,14 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
                         : 0;
     P->t2_sum = grp;
     if (local & PLK_CHAIN_T2) g2.push_back({{P->T2a, L.l2a, P->T2b, t2b, md.only ? md.o2 : P->T2}, -1});
+    // PLK_OPT_PROVE_DERIVE_T2A 2: A2 B2's bytes computed by the t_2 product's first forward pass
+    // (which stores them to T2a as well) instead of t2a_kernel -- one launch fewer; products on
+    // 2^13 tiles only (2^21 and up by default, PLK_OPT_NTT_T13_MIN_K), else t2a_kernel
+    const WDerive dv{P->AB, cA, cB, dS, L.la, L.lab, S_ALPHA, S_BETA, S_GAMMA, S_BK1};
+    const bool derive_fwd = derive_t2a && plk_opt(PLK_OPT_PROVE_DERIVE_T2A) == 2 && L.l2a == L.lab &&
+                            plk_poly_mul_transform_plan(L.l2a, t2b, nullptr) >=
+                                std::max<int64_t>(14, plk_opt(PLK_OPT_NTT_T13_MIN_K));
+    if (derive_fwd) g2.back().j.der = &dv;
     if (!md.only) g2.push_back({{P->AB, L.lab, QM, n, P->ABQM, grp}, 4});
     if (local & PLK_CHAIN_T3) g2.push_back({{P->T3a, L.l2a, P->T3b, L.la + L.lzw - 1, md.only ? md.o3 : P->T3}, -1});
     if (pre) {   // preprocessed circuit: the fixed b operands' transforms (plk_prover_preprocess)
@@ -2419,7 +2449,7 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
       std::vector<PlkPolyMulJob> jobs;
       for (const J& x : *g) jobs.push_back(x.j);
       if (!jobs.empty()) RC(plk_poly_mul_batch_launch(jobs.data(), (int)jobs.size(), P->work, P->work_bytes, P->st));
-      if (g == &g1 && derive_t2a) {   // (a_x b_x is complete on the stream here)
+      if (g == &g1 && derive_t2a && !derive_fwd) {   // (a_x b_x is complete on the stream here)
         const uint64_t blocks = std::min<uint64_t>((L.lab + 1023) / 1024, 4096);
         hipLaunchKernelGGL(t2a_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, P->AB, cA, cB,
                            L.la, L.lab, dS, P->T2a);
@@ -2759,6 +2789,117 @@ int rounds_split(plk_prover* P, const uint8_t* const* pl, const uint8_t* const* 
   return rounds(P, pl, chal, rnd, pre, md);
 }
 
+// ---- rounds() as a HIP graph (PLK_OPT_PROVE_GRAPH).  A proof is 12-14 dependent launches whose
+// host cost (~3-7 us each under a runtime trace) exceeds the GPU time of the first kernels: the GPU
+// idles after the first one until the host has enqueued the next.  rounds() enqueues the same
+// launches with the same arguments for the same input addresses, options and preprocessed state
+// -- except the scalar file (the first kernel's argument: prep_kernel or scalars_init_kernel) and
+// the completion word (the last: commit_pack_kernel or trim_pack_kernel) -- so it is captured once
+// and replayed: the scalar file set as a node parameter when it changed, the completion word
+// cleared by the host before the launch (the call is synchronous: the previous replay is done)
+// and polled for the captured value.
+void drop_graph(plk_prover* P) {
+  if (P->gx) (void)hipGraphExecDestroy(P->gx);
+  if (P->g) (void)hipGraphDestroy(P->g);
+  P->gx = nullptr;
+  P->g = nullptr;
+  P->g_first = P->g_last = nullptr;
+}
+
+bool graph_matches(const plk_prover* P, const uint8_t* const* pl, bool pre) {
+  if (!P->gx || P->g_pre != pre || P->g_fix_gen != P->fix_gen) return false;
+  for (int i = 0; i < 13; i++)
+    if (P->g_pl[i] != pl[i]) return false;
+  for (int o = 1; o < PLK_OPT_COUNT; o++)
+    if (P->g_opt[o] != plk_opt(o)) return false;
+  return true;
+}
+
+// argument idx (of nargs) of kernel node `node` set to *val in the executable graph
+int graph_set_arg(plk_prover* P, hipGraphNode_t node, int nargs, int idx, void* val) {
+  hipKernelNodeParams kp{};
+  PLK_HIP(hipGraphKernelNodeGetParams(node, &kp));
+  if (!kp.kernelParams || nargs > 16) {
+    plk_set_error("prover graph: kernel node without argument pointers");
+    return PLK_ERR_HIP;
+  }
+  void* args[16];
+  for (int i = 0; i < nargs; i++) args[i] = kp.kernelParams[i];
+  args[idx] = val;
+  kp.kernelParams = args;
+  PLK_HIP(hipGraphExecKernelNodeSetParams(P->gx, node, &kp));
+  return PLK_OK;
+}
+
+// rounds() through the graph: capture (and launch) on a key change, else set the two per-call
+// parameters and replay.  The fused division's scan epochs (PLK_OPT_PROVE_FUSE_DIV) change per
+// call inside its launch: that mode runs rounds() directly.
+int rounds_graph(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const uint8_t rnd[9], bool pre) {
+  if (graph_matches(P, pl, pre)) {
+    SlotFile sf = make_slotfile(P->n, chal, rnd);
+    if (memcmp(&sf, &P->g_sf, sizeof sf)) {
+      const int rc = graph_set_arg(P, P->g_first, P->g_first_n, P->g_first_arg, &sf);
+      if (rc) {
+        drop_graph(P);
+        return rc;
+      }
+      P->g_sf = sf;
+    }
+    __atomic_store_n((uint32_t*)(P->h_res + 60), 0u, __ATOMIC_SEQ_CST);
+    P->seq = P->g_seq;
+    PLK_HIP(hipGraphLaunch(P->gx, P->st));
+    return PLK_OK;
+  }
+  drop_graph(P);
+  const uint32_t epoch = P->scan_epoch, seq = P->seq;
+  PLK_HIP(hipStreamBeginCapture(P->st, hipStreamCaptureModeThreadLocal));
+  int rc = rounds(P, pl, chal, rnd, pre);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(P->st, &g);
+  if (rc || e != hipSuccess || !g) {
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    if (rc) return rc;
+    plk_set_error("prover graph: stream capture failed: %s", hipGetErrorString(e));
+    return PLK_ERR_HIP;
+  }
+  P->g = g;
+  if (P->scan_epoch != epoch || P->seq != seq + 1) {   // (per-call state inside the launches: no replay)
+    P->seq = seq;
+    P->scan_epoch = epoch;
+    drop_graph(P);
+    return rounds(P, pl, chal, rnd, pre);
+  }
+  // the first and last kernel nodes, by function
+  size_t nn = 0;
+  PLK_HIP(hipGraphGetNodes(g, nullptr, &nn));
+  std::vector<hipGraphNode_t> nodes(nn);
+  PLK_HIP(hipGraphGetNodes(g, nodes.data(), &nn));
+  for (hipGraphNode_t nd : nodes) {
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(nd, &t) != hipSuccess || t != hipGraphNodeTypeKernel) continue;
+    hipKernelNodeParams kp{};
+    if (hipGraphKernelNodeGetParams(nd, &kp) != hipSuccess) continue;
+    if (kp.func == (void*)prep_kernel) { P->g_first = nd; P->g_first_arg = 1; P->g_first_n = 5; }
+    if (kp.func == (void*)scalars_init_kernel) { P->g_first = nd; P->g_first_arg = 0; P->g_first_n = 5; }
+    if (kp.func == (void*)commit_pack_kernel || kp.func == (void*)trim_pack_kernel) P->g_last = nd;
+  }
+  if (!P->g_first || !P->g_last || hipGraphInstantiateWithFlags(&P->gx, g, 0) != hipSuccess) {
+    P->gx = nullptr;
+    drop_graph(P);
+    plk_set_error("prover graph: no first / last kernel node or instantiation failed");
+    return PLK_ERR_HIP;
+  }
+  for (int i = 0; i < 13; i++) P->g_pl[i] = pl[i];
+  P->g_pre = pre;
+  P->g_fix_gen = P->fix_gen;
+  for (int o = 1; o < PLK_OPT_COUNT; o++) P->g_opt[o] = plk_opt(o);
+  P->g_seq = P->seq;
+  P->g_sf = make_slotfile(P->n, chal, rnd);
+  PLK_HIP(hipGraphLaunch(P->gx, P->st));   // (capture ran nothing: this call's launches)
+  return PLK_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2770,7 +2911,9 @@ int plk_prover_rounds_dev(plk_prover_t* P, const uint8_t* const d_polys[13], con
     if (!d_polys[i]) { plk_set_error("plk_prover_rounds_dev: polynomial %d is NULL", i); return PLK_ERR_ARG; }
   const bool pre = (flags & PLK_PROVE_PREPROCESSED) != 0;
   PROVER_ON_DEVICE(P);
-  int rc = P->nhelp ? rounds_split(P, d_polys, nullptr, chal, rand9, pre) : rounds(P, d_polys, chal, rand9, pre);
+  int rc = P->nhelp                         ? rounds_split(P, d_polys, nullptr, chal, rand9, pre)
+           : plk_opt(PLK_OPT_PROVE_GRAPH) ? rounds_graph(P, d_polys, chal, rand9, pre)
+                                          : rounds(P, d_polys, chal, rand9, pre);
   if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
   return finish(P, (flags & PLK_PROVE_STRICT) != 0, 0, proof);
 }
@@ -2949,6 +3092,7 @@ int plk_prover_preprocess(plk_prover_t* P, const uint8_t* const d_polys[13]) {
   if (!P) { plk_set_error("plk_prover_preprocess: NULL prover"); return PLK_ERR_ARG; }
   PROVER_ON_DEVICE(P);
   PLK_HIP(hipStreamSynchronize(P->st));   // (no round may still read the old transforms)
+  ++P->fix_gen;                            // (a captured proof graph reads the old ones: recapture)
   for (auto& f : P->fix) f = plk_prover::Fixed{};
   (void)hipFree(P->fix_mem);
   P->fix_mem = nullptr;

@@ -86,8 +86,9 @@ def test_options_without_gpu():
     defaults = {"TINY_CALLS": 1, "PROVE_SYNC": 0, "POLY_BLOCK_L": 0, "POLY_BLOCK_S": 0, "NTT_F29": 1,
                 "NTT_SHARE": 1, "NTT_SHARED_FIX": 1, "NTT_T13_MIN_K": 21, "NTT_CENTER_BLOCKS": 0,
                 "MSM_HALF": 1, "MSM_SHARD_MIN": 1 << 16, "NTT_CENTER_SUM": 1, "MSM_HOST_LANES": 4,
-                "PROVE_DERIVE_T2A": 1, "NTT_TABLE_SHARE": 1, "NTT_LAUNCH_LOG": 0,
-                "PROVE_FUSE_DIV": 0, "PROVE_SRS_LOGS": 1, "PROVE_PACK_FUSE": 1, "PROVE_EARLY_COMMITS": 1}
+                "PROVE_DERIVE_T2A": 2, "NTT_TABLE_SHARE": 1, "NTT_LAUNCH_LOG": 0,
+                "PROVE_FUSE_DIV": 0, "PROVE_SRS_LOGS": 1, "PROVE_PACK_FUSE": 1, "PROVE_EARLY_COMMITS": 1,
+                "PROVE_EVAL_AGG": 1, "PROVE_GRAPH": 0}
     for k, v in defaults.items():
         assert h.get_option(k) == v, k
     with h.options(NTT_SHARED_FIX=2, POLY_BLOCK_L=4096, POLY_BLOCK_S=513):

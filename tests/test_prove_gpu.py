@@ -232,6 +232,82 @@ def test_rounds_2_20_vs_golden(hip):
     assert got.hex() == g["proof"]
 
 
+@pytest.mark.parametrize("n,seed", [(256, 3), (3000, 5), (5000, 7), (1 << 16, 41)])
+def test_derive_t2a_modes_vs_oracle(hip, oracle, n, seed):
+    """Round 3's A2 B2 three ways (PLK_OPT_PROVE_DERIVE_T2A): its own product (0), t2a_kernel (1),
+    and inside the t_2 product's first forward pass (2, 2^13-tile products only: here t_2 runs on
+    2^12 tiles, so mode 2 takes mode 1's kernel -- the derived pass itself is checked against the
+    oracle by test_rounds_2_16_tiles13_vs_oracle, where every transform uses 2^13 tiles, and
+    against the golden at 2^20)."""
+    if n == 1 << 16:
+        c = _big_case(oracle)
+        polys, chal, rnd, zh, pts, want = c["polys"], c["chal"], c["rnd"], c["zh"], c["pts"], c["want"]
+    else:
+        polys, chal, rnd, zh, pts = _synthetic(n, seed, 2 * n + 8)
+        want = RefProver(oracle, pts.tobytes(), n, z_h=zh.tobytes()).rounds(polys, chal, rnd, strict=False)
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    for mode in (0, 1, 2):
+        with hip.options(PROVE_DERIVE_T2A=mode):
+            assert pr.rounds_dev(dev, chal, rnd, strict=False).hex() == want.hex(), mode
+
+
+def test_derive_t2a_2_20_vs_golden(hip):
+    """Config C5 with A2 B2 computed by t2a_kernel and inside the t_2 product's first forward pass."""
+    g = load_golden("prove_2_20.json")
+    n = g["n"]
+    polys, chal, rnd, zh, pts = _synthetic(n, g["seed"], g["srs_len"])
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    for mode in (1, 2):
+        with hip.options(PROVE_DERIVE_T2A=mode):
+            assert pr.rounds_dev(dev, chal, rnd).hex() == g["proof"], mode
+            pr.preprocess(dev)
+            assert pr.rounds_dev(dev, chal, rnd, preprocessed=True).hex() == g["proof"], mode
+            pr.preprocess(None)
+
+
+@pytest.mark.parametrize("n,seed", [(3000, 5), (1 << 16, 41)])
+def test_graph_replay_vs_direct(hip, n, seed):
+    """PLK_OPT_PROVE_GRAPH: the first call captures the proof's launches, later calls replay them
+    with the scalar file and the completion word set per call -- the same bytes as direct launches
+    for two challenge / blinding sets in turn, plain and preprocessed (a recapture: the fixed
+    transforms changed), after an input moved (recapture), and again with the graph off."""
+    polys, chal, rnd, zh, pts = _synthetic(n, seed, 2 * n + 8)
+    sets = [(list(chal), list(rnd)), (list(chal[1:]) + [chal[0]], list(rnd[::-1]))]
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    want = [pr.rounds_dev(dev, c, r) for c, r in sets]
+    assert want[0] != want[1]
+    with hip.options(PROVE_GRAPH=1):
+        for _ in range(3):
+            for (c, r), w in zip(sets, want):
+                assert pr.rounds_dev(dev, c, r).hex() == w.hex()
+        pr.preprocess(dev)
+        for _ in range(2):
+            for (c, r), w in zip(sets, want):
+                assert pr.rounds_dev(dev, c, r, preprocessed=True).hex() == w.hex()
+        moved = list(dev)
+        moved[5] = dev[5].clone()
+        for (c, r), w in zip(sets, want):
+            assert pr.rounds_dev(moved, c, r, preprocessed=True).hex() == w.hex()
+        pr.preprocess(None)
+        assert pr.rounds_dev(dev, *sets[1]).hex() == want[1].hex()
+    assert pr.rounds_dev(dev, *sets[0]).hex() == want[0].hex()
+
+
+def test_graph_replay_2_20_vs_golden(hip):
+    """Config C5 through the captured graph: capture, then replays, all the golden bytes."""
+    g = load_golden("prove_2_20.json")
+    n = g["n"]
+    polys, chal, rnd, zh, pts = _synthetic(n, g["seed"], g["srs_len"])
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    with hip.options(PROVE_GRAPH=1):
+        for _ in range(3):
+            assert pr.rounds_dev(dev, chal, rnd).hex() == g["proof"]
+
+
 _TILE13_SCRIPT = r"""
 import sys, numpy as np, torch
 sys.path[:0] = sys.argv[1:2]

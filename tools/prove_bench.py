@@ -18,4 +18,5 @@ hip.init(0)
 dev = torch.device("cuda", 0)
 pre = "--pre" in sys.argv   # the preprocessed-circuit path (plk_prover_preprocess) instead
 ks = [int(x) for x in sys.argv[1:] if x != "--pre"] or [16, 18, 20]
-print(json.dumps({"prove_2^%d" % k: prove_component(torch, hip, dev, k, preprocessed=pre) for k in ks}))
+reps = int(os.environ.get("PROVE_REPS", "9"))   # calls per median
+print(json.dumps({"prove_2^%d" % k: prove_component(torch, hip, dev, k, reps=reps, preprocessed=pre) for k in ks}))
