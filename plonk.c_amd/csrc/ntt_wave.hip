@@ -1498,6 +1498,9 @@ int wave_plan(int k, int TB, int* Ms) {
   return n;
 }
 
+// a 2^k transform's plan has one high pass (the column tables' case, coltab_kernel)
+bool two_pass(int k) { return k - tile_bits(k) <= (tile_bits(k) == 12 ? WT_MAX_HI12 : WT_MAX_HI13); }
+
 // column tables [field][k] (field 0 BabyBear, 1 F29) for the 2-pass plans, k = 13 .. 23
 #ifndef PLK_NTT_COLT_MIN_K
 #define PLK_NTT_COLT_MIN_K 13   // smallest transform using a column table (tuning: larger = lo * hi products)
@@ -1515,8 +1518,11 @@ template <class F>
 WTw fwd_wtw(int k) {
   const bool f29 = F::ADIC == f29::TWO_ADICITY;
   WTw w = to_wtw(f29 ? plk_ntt_tables29() : plk_ntt_tables(), false);
-  w.col = (k >= PLK_NTT_COLT_MIN_K && k >= COLT_MIN_K && k <= COLT_MAX_K) ? g_col[plk_cur_device()][f29 ? 1 : 0][k]
-                                                                          : nullptr;
+  // (a table holds the factors of the plan's ONE high pass: a three-pass plan's top pass -- 2^12
+  // tiles above 2^20 when PLK_OPT_NTT_T13_MIN_K moves the 2^13 threshold up -- multiplies lo * hi)
+  w.col = (k >= PLK_NTT_COLT_MIN_K && k >= COLT_MIN_K && k <= COLT_MAX_K && two_pass(k))
+              ? g_col[plk_cur_device()][f29 ? 1 : 0][k]
+              : nullptr;
   return w;
 }
 // the same for a product's last inverse pass: the scaled column table
@@ -1892,7 +1898,7 @@ int build_coltabs(int fi) {
     for (int s = 0; s < 2; s++) {
       const int dev = plk_cur_device();
       uint32_t*& t = s ? g_coli[dev][fi][k] : g_col[dev][fi][k];
-      if (t) continue;
+      if (t || !two_pass(k)) continue;   // (three-pass plans take no table: fwd_wtw)
       PLK_HIP(hipMalloc((void**)&t, 4ull << k));
       const WTw tw = to_wtw(fi ? plk_ntt_tables29() : plk_ntt_tables(), false);
       const unsigned blocks = (unsigned)((1ull << k) / 256);

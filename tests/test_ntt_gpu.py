@@ -194,3 +194,42 @@ def test_extreme_values_every_plan(hip, field, k, pattern):
     torch.cuda.synchronize()
     back = d.cpu().numpy().view(np.uint32).astype(np.uint64)
     assert np.array_equal(back, (x.astype(np.uint64) * np.uint64(pow(2, k, p))) % np.uint64(p)), (field, k, pattern)
+
+
+_TILE12_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path[:0] = sys.argv[1:5]
+import plonkhip as hip
+import gen
+from pyoracle import Oracle
+from test_ntt_gpu import P, P29, ntt_dif_reference
+hip.set_option("NTT_T13_MIN_K", 24)   # shapes the column tables: before plk_init
+hip.init(0)
+st = torch.cuda.current_stream()
+for k in (21, 22):
+    for p, g, fn in ((P29, 3, hip.ntt29_dev), (P, 31, hip.ntt_dev)):
+        x = np.random.default_rng(k).integers(0, p, 1 << k, dtype=np.int64)
+        d = torch.from_numpy(x.astype(np.int32)).cuda()
+        fn(d, k, False, st)
+        torch.cuda.synchronize()
+        got = d.cpu().numpy().view(np.uint32).astype(np.uint64)
+        print("ntt", k, p, bool(np.array_equal(got, ntt_dif_reference(x, k, p, g))))
+a, b = gen.poly_inputs(21, (1 << 20) - 3, (1 << 20) + 2)
+print("poly_mul", hip.poly_mul(a, b) == Oracle().poly_mul_ntt(a, b))
+"""
+
+
+def test_tile12_three_pass_plans():
+    """2^21 and 2^22 transforms on 2^12 tiles (PLK_OPT_NTT_T13_MIN_K = 24, set before plk_init: a
+    child process): three-pass plans whose top pass is not the column tables' single high pass, so
+    it multiplies lo * hi factors instead (round 5: with the table it gave wrong transforms) --
+    forward against the numpy reference in both fields, and a 2^21 product against the oracle."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = [os.path.join(root, d) for d in ("plonk.c_amd", "oracle", "tests", os.path.join("tests", "golden"))]
+    r = subprocess.run([sys.executable, "-c", _TILE12_SCRIPT] + paths, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith(("ntt", "poly_mul"))]
+    assert len(lines) == 5 and all(ln.endswith("True") for ln in lines), r.stdout
