@@ -409,3 +409,31 @@ def test_preprocessed_tensors_held_and_overwrite_needs_preprocess(hip):
     assert pr.rounds_dev(dev, chal, rnd, preprocessed=True) == want
     pr.preprocess(None)
     assert pr._fixed is None
+
+
+# every switch that changes how a 2^20 proof is computed, one at a time away from its default
+_SWEEP = [("NTT_F29", 0), ("NTT_SHARE", 0), ("NTT_SHARED_FIX", 0), ("NTT_SHARED_FIX", 2), ("NTT_CENTER_BLOCKS", 768),
+          ("NTT_CENTER_SUM", 0), ("NTT_TABLE_SHARE", 0), ("PROVE_DERIVE_T2A", 0), ("PROVE_DERIVE_T2A", 1),
+          ("PROVE_FUSE_DIV", 1), ("PROVE_SRS_LOGS", 0), ("PROVE_PACK_FUSE", 0), ("PROVE_EARLY_COMMITS", 0),
+          ("PROVE_EARLY_COMMITS", 2), ("PROVE_EVAL_AGG", 0), ("PROVE_GRAPH", 1), ("PROVE_SYNC", 1)]
+
+
+def test_option_sweep_2_20_vs_golden(hip):
+    """Config C5 with each computation switch (PLK_OPT_*) moved off its default in turn -- BabyBear
+    instead of F29, no shared operands, the shared-operand pass off / forced, another centre grid,
+    no centre sum groups, per-array column reads, A2 B2 as a product or its own kernel, the fused
+    look-back division, G1-form commitments, unfused packing, the early commitments elsewhere, the
+    two-launch division, graph replay, stream-synchronised completion -- plain and preprocessed:
+    the golden bytes every time (round 5 found a wrong-result bug behind a non-default option)."""
+    g = load_golden("prove_2_20.json")
+    n = g["n"]
+    polys, chal, rnd, zh, pts = _synthetic(n, g["seed"], g["srs_len"])
+    pr = hip.Prover(n, zh, pts)
+    dev = [torch.from_numpy(p).to("cuda") for p in polys]
+    for opt, val in _SWEEP:
+        with hip.options(**{opt: val}):
+            assert pr.rounds_dev(dev, chal, rnd).hex() == g["proof"], (opt, val)
+    pr.preprocess(dev)
+    for opt, val in _SWEEP:
+        with hip.options(**{opt: val}):
+            assert pr.rounds_dev(dev, chal, rnd, preprocessed=True).hex() == g["proof"], (opt, val, "pre")
