@@ -248,3 +248,48 @@ def test_combine_partials(hip, oracle):
     hip.msm_combine_dev(dl, shards, out, torch.cuda.current_stream())
     torch.cuda.synchronize()
     assert bytes(out.cpu().numpy()[:3]) == oracle.msm(pts, sc)
+
+
+# launch-geometry switches (PLK_OPT_MSM_*), alone and combined; {} = the built-in choice
+_GEOM = [{}, {"MSM_THREADS": 256}, {"MSM_THREADS": 1024}, {"MSM_MAX_BLOCKS": 64}, {"MSM_MAX_BLOCKS": 1000},
+         {"MSM_GROUPS": 1}, {"MSM_GROUPS": 4}, {"MSM_COPIES": 1}, {"MSM_HALF": 0},
+         {"MSM_HALF": 0, "MSM_THREADS": 1024, "MSM_GROUPS": 4, "MSM_COPIES": 1}]
+
+
+def test_geometry_options_vs_golden(hip, oracle):
+    """Every MSM launch-geometry switch (threads per block, resident blocks, groups in flight, table
+    copies, half groups) gives the recorded reference results: single device launches on the
+    golden seeded inputs (up to 2^22 points) and a ragged length against the oracle, and the batched
+    launch (the headline kernel) on 5 inputs of 2^20 + 16 points (aligned rows) and of 2^20 + 7
+    (byte-wise rows) against the oracle."""
+    import torch
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream()
+    g = load_golden("msm.json")
+    cases = [(c["out"], gen.msm_inputs(c["seed"], c["n"], c["kind"])) for c in g["large"]]
+    pts, sc = gen.msm_inputs(79, 1000003, "full")
+    cases.append((oracle.msm(pts, sc).hex(), (pts, sc)))
+    dcases = [(w, torch.from_numpy(p.reshape(-1)).to(dev), torch.from_numpy(s).to(dev), len(s)) for w, (p, s) in cases]
+    res = torch.zeros(hip.MSM_RESULT_BYTES, dtype=torch.uint8, device=dev)
+    hip.msm_result_init(res, st)
+    batch, R = 5, hip.MSM_RESULT_BYTES
+    bres = torch.zeros(batch * R, dtype=torch.uint8, device=dev)
+    for i in range(batch):
+        hip.msm_result_init(bres[i * R:(i + 1) * R], st)
+    batches = []
+    for nb in ((1 << 20) + 16, (1 << 20) + 7):
+        bp, bs = gen.msm_inputs(nb % 97, nb * batch, "full")
+        want_b = [oracle.msm(bp[i * nb:(i + 1) * nb], bs[i * nb:(i + 1) * nb]) for i in range(batch)]
+        batches.append((nb, torch.from_numpy(bp.reshape(-1)).to(dev), torch.from_numpy(bs).to(dev), want_b))
+    for opts in _GEOM:
+        with hip.options(**opts):
+            for want, dp, ds, n in dcases:
+                hip.msm_g1_dev(dp, ds, n, res, st)
+                torch.cuda.synchronize()
+                assert hip.parse_result(res.cpu().numpy())["g1"].hex() == want, (opts, n)
+            for nb, bpd, bsd, want_b in batches:
+                hip.msm_g1_batch_dev(bpd, 3 * nb, bsd, nb, nb, batch, bres, st)
+                torch.cuda.synchronize()
+                got = bres.cpu().numpy()
+                for i in range(batch):
+                    assert hip.parse_result(got[i * R:(i + 1) * R])["g1"] == want_b[i], (opts, nb, i)
