@@ -413,3 +413,19 @@ def test_batch_sum_group_mixed_shapes(hip, oracle, csum):
     assert _trim(outs[0]) == oracle.poly_mul(polys[5].tobytes(), polys[5].tobytes())
     with pytest.raises(Exception, match="does not follow"):
         _run_batch(hip, polys, [(2, 3, 0), (0, 1, 1)])
+
+
+@pytest.mark.parametrize("opts", [{"NTT_F29": 0}, {"NTT_SHARE": 0}, {"NTT_SHARED_FIX": 0}, {"NTT_SHARED_FIX": 2},
+                                  {"NTT_CENTER_BLOCKS": 300}, {"NTT_CENTER_SUM": 0}, {"NTT_TABLE_SHARE": 0},
+                                  {"POLY_BLOCK_L": 1 << 18, "POLY_BLOCK_S": 1 << 16}])
+def test_option_sweep(hip, oracle, opts):
+    """Each poly_mul switch (PLK_OPT_*) off its default: BabyBear for every product, no shared
+    operands, the shared-operand pass off / forced, a centre grid that does not divide the items,
+    no centre sum groups, per-array column reads, forced blocked pieces -- the C3-size reference
+    digests and the batch cases (shared operands across launch chunks, sum groups) unchanged."""
+    with hip.options(**opts):
+        for idx in range(3):
+            test_golden_c3_size_digests(hip, idx)
+        test_batch_shared_operands(hip, oracle)
+        test_batch_sum_group(hip, oracle)
+        test_batch_group_across_launch_chunks(hip, oracle)
