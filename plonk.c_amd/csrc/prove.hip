@@ -2838,10 +2838,9 @@ int rounds_graph(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5],
   if (graph_matches(P, pl, pre)) {
     SlotFile sf = make_slotfile(P->n, chal, rnd);
     if (memcmp(&sf, &P->g_sf, sizeof sf)) {
-      const int rc = graph_set_arg(P, P->g_first, P->g_first_n, P->g_first_arg, &sf);
-      if (rc) {
-        drop_graph(P);
-        return rc;
+      if (graph_set_arg(P, P->g_first, P->g_first_n, P->g_first_arg, &sf)) {
+        drop_graph(P);   // (the runtime would not take the parameter: direct launches)
+        return rounds(P, pl, chal, rnd, pre);
       }
       P->g_sf = sf;
     }
@@ -2852,29 +2851,37 @@ int rounds_graph(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5],
   }
   drop_graph(P);
   const uint32_t epoch = P->scan_epoch, seq = P->seq;
-  PLK_HIP(hipStreamBeginCapture(P->st, hipStreamCaptureModeThreadLocal));
+  // capture ran nothing: anything that keeps this call from a graph runs it with direct launches
+  auto direct = [&]() {
+    (void)hipGetLastError();
+    drop_graph(P);
+    P->seq = seq;
+    P->scan_epoch = epoch;
+    return rounds(P, pl, chal, rnd, pre);
+  };
+  if (hipStreamBeginCapture(P->st, hipStreamCaptureModeThreadLocal) != hipSuccess) return direct();
   int rc = rounds(P, pl, chal, rnd, pre);
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(P->st, &g);
-  if (rc || e != hipSuccess || !g) {
+  if (rc) {   // (an argument / range error: the same one a direct call reports)
     if (g) (void)hipGraphDestroy(g);
     (void)hipGetLastError();
-    if (rc) return rc;
-    plk_set_error("prover graph: stream capture failed: %s", hipGetErrorString(e));
-    return PLK_ERR_HIP;
-  }
-  P->g = g;
-  if (P->scan_epoch != epoch || P->seq != seq + 1) {   // (per-call state inside the launches: no replay)
     P->seq = seq;
     P->scan_epoch = epoch;
-    drop_graph(P);
-    return rounds(P, pl, chal, rnd, pre);
+    return rc;
   }
+  if (e != hipSuccess || !g) {
+    if (g) (void)hipGraphDestroy(g);
+    return direct();
+  }
+  P->g = g;
+  // per-call state inside the launches (the fused division's scan epochs): no replay
+  if (P->scan_epoch != epoch || P->seq != seq + 1) return direct();
   // the first and last kernel nodes, by function
   size_t nn = 0;
-  PLK_HIP(hipGraphGetNodes(g, nullptr, &nn));
+  if (hipGraphGetNodes(g, nullptr, &nn) != hipSuccess) return direct();
   std::vector<hipGraphNode_t> nodes(nn);
-  PLK_HIP(hipGraphGetNodes(g, nodes.data(), &nn));
+  if (hipGraphGetNodes(g, nodes.data(), &nn) != hipSuccess) return direct();
   for (hipGraphNode_t nd : nodes) {
     hipGraphNodeType t;
     if (hipGraphNodeGetType(nd, &t) != hipSuccess || t != hipGraphNodeTypeKernel) continue;
@@ -2886,9 +2893,7 @@ int rounds_graph(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5],
   }
   if (!P->g_first || !P->g_last || hipGraphInstantiateWithFlags(&P->gx, g, 0) != hipSuccess) {
     P->gx = nullptr;
-    drop_graph(P);
-    plk_set_error("prover graph: no first / last kernel node or instantiation failed");
-    return PLK_ERR_HIP;
+    return direct();
   }
   for (int i = 0; i < 13; i++) P->g_pl[i] = pl[i];
   P->g_pre = pre;
@@ -2896,7 +2901,7 @@ int rounds_graph(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5],
   for (int o = 1; o < PLK_OPT_COUNT; o++) P->g_opt[o] = plk_opt(o);
   P->g_seq = P->seq;
   P->g_sf = make_slotfile(P->n, chal, rnd);
-  PLK_HIP(hipGraphLaunch(P->gx, P->st));   // (capture ran nothing: this call's launches)
+  PLK_HIP(hipGraphLaunch(P->gx, P->st));   // (this call's launches)
   return PLK_OK;
 }
 
