@@ -104,7 +104,8 @@ enum {
                                     0: the numerators + aggregates launch, then the apply launch */
   PLK_OPT_PROVE_GRAPH = 27,      /* 1: plk_prover_rounds_dev replays its launches as a HIP graph captured on the
                                     first call with the same input addresses, preprocessed state and options
-                                    (per call only the scalar file and the completion word are set) */
+                                    (per call only the scalar file and the completion word are set; a call
+                                    the graph cannot serve runs direct launches) -- measured equal, off */
   PLK_OPT_COUNT = 28
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
