@@ -46,6 +46,40 @@ def test_two_rank_strong_scaling_line():
     assert "prove_2^20_gates" not in c            # the single-GPU C5 line is not repeated at N > 1
 
 
+def _plain_bench_line(n, components, batch, rotate, steps=2, timeout=540):
+    """`python bench.py --gpus n` exactly as the driver's scaling run starts it (no launcher: the bench
+    spawns its n ranks), gloo so that n ranks share the one GPU of a test box; rank 0's line"""
+    env = dict(os.environ, PLK_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", str(steps), "--warmup", "1",
+           "--msm-batch", str(batch), "--rotate-mib", str(rotate), "--components", components, "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_driver_scaling_world_sizes(n):
+    """the world sizes the driver's N = 1, 2, 4, 8 scaling run uses, rehearsed on one
+    GPU before the first 8-GPU node sees them: an n-way shard_range of every 2^22-point MSM (the 2^22
+    reference golden through the n shards), n concurrent proof replicas each matching the recorded answer,
+    and the strong-scaled proof over 3 ranks with ranks 3 .. n-1 idle through every one of its barriers."""
+    d = _plain_bench_line(n, "prove,msm", batch=4, rotate=8)
+    assert d["n_gpus"] == n and d["scaling"] == "strong" and d["config"]["parallelism"] == "dp%d" % n
+    assert d["config"]["points_per_gpu"] * n == d["config"]["points_per_msm"] == 1 << 22
+    assert d["checks"] == {"first_msm_single_gpu_recompute": True, "golden_2^22_reference": True}
+    assert d["irregular_inputs"] == 0 and d["serial_fold_fallbacks"] == 0 and d["value"] > 0
+    c = d["components"]
+    rep = c["prove_2^20_gates_replicas"]
+    assert rep["gpus"] == n and rep["matches_oracle_all_ranks"] is True and rep["deterministic_all_ranks"] is True
+    sp = c["prove_2^20_gates_split"]
+    assert sp["gpus"] == 3 and sp["matches_oracle"] is True and sp["same_as_single_gpu"] is True
+    lab = "2^%d" % (22 - (n.bit_length() - 1))
+    assert "msm_%s_one_per_launch" % lab in c and "msm_%s_8_per_launch" % lab in c
+
+
 def test_three_rank_split_proof():
     """C5 strong-scaled over three ranks: rank 1 computes the t_2 chain, rank 2 the t_3 chain, rank
     0 the rest; the proof equals the single-GPU proof and the recorded answer.  Launched the way the
