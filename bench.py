@@ -245,7 +245,7 @@ def cpu_other_baselines(hip):
     headers, gcc -O2, one thread), bounded samples: schoolbook poly_mul (src/poly.h:106-122) at
     2^14 x 2^14 and 2^15 x 2^15 with the O(la lb) extrapolation to config C3's 2^19 x 2^19, and the
     toy prove of src/plonk-test.c (src/plonk.h:223) next to the same proof through the drop-in
-    build whose hot ops run in libplonkhip."""
+    build: as shipped (toy-size calls on the host, include/plk_host.h) and with every call on the GPU."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import gen
@@ -274,16 +274,28 @@ def cpu_other_baselines(hip):
     dropin = os.path.join(ROOT, "oracle", "_ref", "libplonkref_dropin.so")
     if os.path.exists(dropin):
         D = Reference(dropin)
-        D.prove4_inproc(*args)
-        t0 = time.perf_counter()
-        for _ in range(50):
-            dproof = D.prove4_inproc(*args)
-        out["toy_prove_4_gates"]["dropin_gpu_us"] = round((time.perf_counter() - t0) / 50 * 1e6, 1)
-        out["toy_prove_4_gates"]["dropin_matches_golden"] = dproof.hex() == p["proof"]
+        toy = out["toy_prove_4_gates"]
+
+        def timed(n):
+            D.prove4_inproc(*args)
+            t0 = time.perf_counter()
+            for _ in range(n):
+                pr = D.prove4_inproc(*args)
+            return round((time.perf_counter() - t0) / n * 1e6, 2), pr.hex() == p["proof"]
+
+        # the drop-in as shipped: include/plk_host.h keeps toy-size calls on the host
+        toy["dropin_us"], toy["dropin_matches_golden"] = timed(reps)
+        toy["dropin_vs_reference_cpu"] = round(toy["dropin_us"] / ref_us, 3)
+        # the same build with the policy's threshold at 0: every poly_mul / MSM / division / evaluation /
+        # matrix call of the toy prove crosses to the GPU
+        with hip.options(DROPIN_HOST_WORK=0):
+            toy["dropin_all_gpu_us"], toy["dropin_all_gpu_matches_golden"] = timed(50)
     out["note"] = ("reference compiled from its own headers (oracle/_ref, gcc -O2), 1 thread, in-process; the toy "
-                   "prove = srs_create + plonk_new + plonk_prove of src/plonk-test.c, whose drop-in build sends its "
-                   "poly_mul / MSM / poly_divide / poly_eval / matrix ops to the GPU one tiny call at a time "
-                   "(latency-bound: ~100 host<->device round trips)")
+                   "prove = srs_create + plonk_new + plonk_prove of src/plonk-test.c; dropin_us: the same program "
+                   "built against include/ (libplonkref_dropin.so) with the default small-size policy, which keeps "
+                   "its toy-size calls on the host (include/plk_host.h, PLK_OPT_DROPIN_HOST_WORK 32768); "
+                   "dropin_all_gpu_us: the policy at 0, every poly_mul / MSM / poly_divide / poly_eval / matrix call "
+                   "on the GPU one tiny call at a time (latency-bound: ~100 host<->device round trips)")
     return out
 
 

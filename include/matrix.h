@@ -2,7 +2,8 @@
  * MATRIX layout, names and error text.  matrix_mul and matrix_inv -- what plonk_new builds the
  * Vandermonde inverse with (src/plonk.h:105-113) and interpolate_at_h applies
  * (src/plonk.h:162-195) -- run on the GPU through plk_matrix_mul / plk_matrix_inv
- * (include/plonkhip.h); the accessors are host code restated from scratch. */
+ * (include/plonkhip.h), toy sizes on the host (plk_host.h); the accessors are host
+ * code restated from scratch. */
 #ifndef MATRIX_H
 #define MATRIX_H
 
@@ -11,6 +12,7 @@
 #include <string.h>
 #include "hf.h"
 #include "plonkhip.h"
+#include "plk_host.h"
 
 typedef struct {
   size_t m;  /* rows */
@@ -82,6 +84,10 @@ static inline MATRIX matrix_mul(const MATRIX *a, const MATRIX *b) {
     exit(EXIT_FAILURE);
   }
   MATRIX r = matrix_zero(a->m, b->n);
+  if (plk_host_small_(plk_host_mul_(plk_host_mul_(a->m, a->n), b->n))) {
+    plk_host_matrix_mul((const uint8_t *)a->v, a->m, a->n, (const uint8_t *)b->v, b->n, (uint8_t *)r.v);
+    return r;
+  }
   int rc = plk_matrix_mul((const uint8_t *)a->v, a->m, a->n, (const uint8_t *)b->v, b->n, (uint8_t *)r.v);
   if (rc != PLK_OK) matrix_gpu_fail_("matrix_mul", rc);
   return r;
@@ -94,6 +100,27 @@ static inline MATRIX matrix_inv(const MATRIX *a) {
   if (a->m != a->n) {
     fprintf(stderr, "Only square matrices can be inverted\n");
     exit(EXIT_FAILURE);
+  }
+  const size_t n = a->n;
+  if (plk_host_small_(plk_host_mul_(4 * n, plk_host_mul_(n, n)))) {
+    /* src/matrix.h:150-176: Gauss-Jordan on [a | I], the right half is the inverse.  A raw pivot byte
+       would make the reference read past hf_inverses: rejected as by plk_matrix_inv */
+    for (size_t i = 0; i < n * n; i++)
+      if (a->v[i].value >= MODULO_HF) {
+        fprintf(stderr, "matrix_inv: entry %zu = %u is not a GF(17) value (reference behaviour undefined)\n", i,
+                a->v[i].value);
+        exit(EXIT_FAILURE);
+      }
+    MATRIX aug = matrix_zero(n, 2 * n);
+    for (size_t i = 0; i < n; i++) {
+      memcpy(aug.v + i * 2 * n, a->v + i * n, n);
+      aug.v[i * 2 * n + n + i] = hf_one();
+    }
+    matrix_gauss_jordan(&aug);
+    MATRIX r = matrix_zero(n, n);
+    for (size_t i = 0; i < n; i++) memcpy(r.v + i * n, aug.v + i * 2 * n + n, n);
+    matrix_free(&aug);
+    return r;
   }
   MATRIX r = matrix_zero(a->n, a->n);
   int rc = plk_matrix_inv((const uint8_t *)a->v, a->n, (uint8_t *)r.v);

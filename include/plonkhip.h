@@ -18,7 +18,9 @@
  *     The drop-in headers turn a non-zero code into the reference's convention
  *     (fprintf(stderr, ...) + exit(EXIT_FAILURE), e.g. src/srs.h:54-57);
  *   - there is no CPU fallback: without a usable GPU every compute entry point fails
- *     with PLK_ERR_NODEV.
+ *     with PLK_ERR_NODEV.  (The drop-in HEADERS keep calls of toy size on the host by their own
+ *     restated code, include/plk_host.h -- SURVEY 8(b)'s small-size policy, sized by
+ *     PLK_OPT_DROPIN_HOST_WORK; the library itself never computes on the CPU.)
  */
 #ifndef PLONKHIP_H
 #define PLONKHIP_H
@@ -106,7 +108,11 @@ enum {
                                     first call with the same input addresses, preprocessed state and options
                                     (per call only the scalar file and the completion word are set; a call
                                     the graph cannot serve runs direct launches) -- measured equal, off */
-  PLK_OPT_COUNT = 28
+  PLK_OPT_DROPIN_HOST_WORK = 28, /* drop-in headers (include/plk_host.h): a call whose host cost estimate (about
+                                    ns: la*lb MACs for poly_mul, 300 per MSM point, ...) is at most this stays
+                                    on the host; 32768 ~ one GPU round trip; 0: every call on the GPU.  The
+                                    library reads it only through plk_get_option */
+  PLK_OPT_COUNT = 29
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
 /* Diagnostics for the offline roofline tools: with PLK_OPT_NTT_LAUNCH_LOG = 1 every NTT pass launch

@@ -3,7 +3,8 @@
  * are freshly malloc'ed and freed with poly_free).  poly_mul -- the prover's hot
  * polynomial operation (17 calls per proof) -- runs on the GPU through plk_poly_mul
  * (exact NTT / direct convolution, include/plonkhip.h), and so do poly_divide and poly_eval
- * (plk_poly_divide, plk_poly_eval).  The other operations are O(n)
+ * (plk_poly_divide, plk_poly_eval), except calls of toy size, which stay on
+ * the host (plk_host.h: SURVEY 8(b)'s small-size policy).  The other operations are O(n)
  * coefficient copies and scalings, host code restated from scratch. */
 #ifndef POLY_H
 #define POLY_H
@@ -16,6 +17,7 @@
 #include <sys/types.h>
 #include "hf.h"
 #include "plonkhip.h"
+#include "plk_host.h"
 
 typedef struct {
   HF *coeffs;
@@ -70,11 +72,17 @@ static inline POLY poly_addsub_(const POLY *a, const POLY *b, int sub, const cha
 static inline POLY poly_add(const POLY *a, const POLY *b) { return poly_addsub_(a, b, 0, "poly_add"); }
 static inline POLY poly_sub(const POLY *a, const POLY *b) { return poly_addsub_(a, b, 1, "poly_sub"); }
 
-/* GPU: product over GF(17), trimmed (reference schoolbook src/poly.h:106-122) */
+/* GPU: product over GF(17), trimmed (reference schoolbook src/poly.h:106-122); toy sizes on the host */
 static inline POLY poly_mul(const POLY *a, const POLY *b) {
   size_t rl = a->len + b->len - 1;
   HF *c = (HF *)poly_xalloc_(rl, "poly_mul");
   size_t n = 0;
+  if (a->len && b->len && plk_host_small_(plk_host_mul_(a->len, b->len))) {
+    POLY r;
+    r.len = plk_host_poly_mul((const uint8_t *)a->coeffs, a->len, (const uint8_t *)b->coeffs, b->len, (uint8_t *)c);
+    r.coeffs = c;
+    return r;
+  }
   int rc = plk_poly_mul((const uint8_t *)a->coeffs, a->len, (const uint8_t *)b->coeffs, b->len,
                         (uint8_t *)c, &n);
   if (rc != PLK_OK) {
@@ -99,8 +107,19 @@ static inline void poly_divide(const POLY *num, const POLY *den, POLY *quot, POL
   HF *q = (HF *)poly_xalloc_(nl, "poly_divide");
   HF *r = (HF *)poly_xalloc_(nl, "poly_divide");
   size_t ql = 0, rl = 0;
-  int rc = plk_poly_divide((const uint8_t *)num->coeffs, nl, (const uint8_t *)den->coeffs, dl, (uint8_t *)q, &ql,
-                           (uint8_t *)r, &rl);
+  int rc;
+  if (plk_host_small_(plk_host_mul_(2 * (nl >= dl ? nl - dl + 1 : 1), dl))) {
+    rc = plk_host_poly_divide((const uint8_t *)num->coeffs, nl, (const uint8_t *)den->coeffs, dl, (uint8_t *)q, &ql,
+                              (uint8_t *)r, &rl);
+    if (rc != PLK_OK) {
+      fprintf(stderr, "poly_divide: divisor lead byte %u is not a GF(17) value (reference behaviour undefined)\n",
+              den->coeffs[dl - 1].value);
+      exit(EXIT_FAILURE);
+    }
+  } else {
+    rc = plk_poly_divide((const uint8_t *)num->coeffs, nl, (const uint8_t *)den->coeffs, dl, (uint8_t *)q, &ql,
+                         (uint8_t *)r, &rl);
+  }
   if (rc != PLK_OK) {
     fprintf(stderr, "poly_divide failed on the GPU (libplonkhip error %d): %s\n", rc, plk_last_error());
     exit(EXIT_FAILURE);
@@ -151,9 +170,13 @@ static inline void poly_free(POLY *p) {
   p->len = 0;
 }
 
-/* Horner (src/poly.h:265-272) on the GPU (plk_poly_eval: exact for every byte value) */
+/* Horner (src/poly.h:265-272) on the GPU (plk_poly_eval: exact for every byte value); toy sizes on the host */
 static inline HF poly_eval(const POLY *p, HF x) {
   HF y = {0};
+  if (plk_host_small_(plk_host_mul_(2, p->len))) {
+    y.value = plk_host_poly_eval((const uint8_t *)p->coeffs, p->len, x.value);
+    return y;
+  }
   int rc = plk_poly_eval((const uint8_t *)p->coeffs, p->len, x.value, &y.value);
   if (rc != PLK_OK) {
     fprintf(stderr, "poly_eval failed on the GPU (libplonkhip error %d): %s\n", rc, plk_last_error());

@@ -1,7 +1,8 @@
 /* Drop-in for the reference's src/srs.h: the KZG structured reference string and the
  * commitment MSM (src/srs.h:11-68).  Same guard, SRS layout and names.  srs_eval_at_s --
  * 9 calls per proof, the prover's dominant cost -- runs on the GPU through plk_msm_g1
- * (include/plonkhip.h); the reference's degree check and exit() stay on the host.
+ * (include/plonkhip.h), a toy-size call on the host (plk_host.h); the reference's degree check
+ * and exit() stay on the host.
  * srs_create reproduces the reference exactly, including that every G1 entry is a
  * multiple of the IDENTITY (src/srs.h:27-36, pinned by src/srs-test.c:15-17). */
 #ifndef SRS_H
@@ -47,13 +48,14 @@ static inline void srs_free(SRS *srs) {
   srs->len = 0;
 }
 
-/* GPU: sum_i coeffs[i] * g1s[i] (reference: serial g1_mul/g1_add fold) */
+/* GPU: sum_i coeffs[i] * g1s[i] (reference: serial g1_mul/g1_add fold); toy sizes: that fold on the host */
 static inline G1 srs_eval_at_s(const SRS *srs, const POLY *vs) {
   if (vs->len > srs->len) {
     fprintf(stderr, "Poynomial degree exceeds SRS size: POLY degree: %zu, SRS supports up to degree: %zu \n",
             vs->len, vs->len);
     exit(EXIT_FAILURE);
   }
+  if (plk_host_small_(plk_host_mul_(300, vs->len))) return plk_host_msm(srs->g1s, vs->coeffs, vs->len);
   G1 out;
   int rc = plk_msm_g1((const uint8_t *)srs->g1s, (const uint8_t *)vs->coeffs, vs->len, (uint8_t *)&out);
   if (rc != PLK_OK) {

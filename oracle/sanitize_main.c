@@ -84,6 +84,45 @@ int main(void) {
     free(a);
     free(b);
   }
+  /* the drop-in's small-size host path (include/plk_host.h) against the oracle over raw bytes */
+  for (int i = 0; i < 2000; i++) {
+    size_t la = 1 + rnd() % 80, lb = 1 + rnd() % 80, n = rnd() % 120;
+    uint8_t *a = malloc(la), *b = malloc(lb), *o = malloc(la + lb), *o2 = malloc(la + lb);
+    fill(a, la, i & 1 ? 256 : 17);
+    fill(b, lb, i & 2 ? 256 : 17);
+    if (i % 5 == 0) a[la - 1] = 0;
+    size_t l1 = plk_host_poly_mul(a, la, b, lb, o), l2 = orc_poly_mul(a, la, b, lb, o2);
+    if (l1 != l2 || memcmp(o, o2, l1)) { fprintf(stderr, "host poly_mul mismatch\n"); return 1; }
+    uint8_t x = (uint8_t)rnd();
+    if (plk_host_poly_eval(a, la, x) != orc_poly_eval(a, la, x)) { fprintf(stderr, "host poly_eval mismatch\n"); return 1; }
+    size_t dl = 1 + rnd() % (lb < 9 ? lb : 9), q1, r1, q2, r2;
+    uint8_t *q = malloc(la + 1), *r = malloc(la + 1), *qq = malloc(la + 1), *rr = malloc(la + 1);
+    fill(b, dl, 17);
+    b[dl - 1] = (uint8_t)(1 + rnd() % 16);
+    if (plk_host_poly_divide(a, la, b, dl, q, &q1, r, &r1) != PLK_OK) { fprintf(stderr, "host divide rc\n"); return 1; }
+    orc_poly_divide(a, la, b, dl, qq, &q2, rr, &r2);
+    if (q1 != q2 || r1 != r2 || memcmp(q, qq, q1) || memcmp(r, rr, r1)) {
+      fprintf(stderr, "host poly_divide mismatch\n");
+      return 1;
+    }
+    uint8_t *pts = malloc(3 * n + 1), *sc = malloc(n + 1), m1[3], m2[3];
+    fill(pts, 3 * n, i & 4 ? 256 : 101);
+    fill(sc, n, i & 8 ? 256 : 17);
+    for (size_t j = 0; j < n; j++) pts[3 * j + 2] &= 1;   /* a bool flag byte outside {0, 1} is UB in C */
+    G1 h = plk_host_msm((const G1 *)pts, (const HF *)sc, n);
+    memcpy(m1, &h, 3);
+    orc_msm_fold(pts, sc, n, m2);
+    if (memcmp(m1, m2, 3)) { fprintf(stderr, "host msm mismatch\n"); return 1; }
+    size_t mm = 1 + rnd() % 7, kk = 1 + rnd() % 7, nn = 1 + rnd() % 7;
+    uint8_t A[49], B[49], C1[49], C2[49];
+    fill(A, mm * kk, 256);
+    fill(B, kk * nn, 256);
+    plk_host_matrix_mul(A, mm, kk, B, nn, C1);
+    orc_matrix_mul(A, mm, kk, B, nn, C2);
+    if (memcmp(C1, C2, mm * nn)) { fprintf(stderr, "host matrix_mul mismatch\n"); return 1; }
+    checks += l1 + q1 + r1 + m1[0];
+    free(a); free(b); free(o); free(o2); free(q); free(r); free(qq); free(rr); free(pts); free(sc);
+  }
   /* matrices: host accessors and the restated Gauss-Jordan */
   for (int n = 1; n <= 17; n++) {
     MATRIX M = matrix_zero((size_t)n, (size_t)n), N = matrix_zero((size_t)n, (size_t)n);

@@ -482,6 +482,7 @@ const OptDef kOpt[PLK_OPT_COUNT] = {
     {0, 0, 1, false},                          // PROVE_HELPER_COPY (tests: the distinct-device input path on one GPU)
     {1, 0, 1, false},                          // PROVE_EVAL_AGG
     {0, 0, 1, false},                          // PROVE_GRAPH
+    {32768, 0, 1ll << 40, false},              // DROPIN_HOST_WORK (read by include/plk_host.h only)
 };
 struct Opts {
   std::atomic<int64_t> v[PLK_OPT_COUNT];

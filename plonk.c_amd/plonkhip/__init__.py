@@ -91,7 +91,8 @@ OPTIONS = {"TINY_CALLS": 1, "PROVE_SYNC": 2, "POLY_BLOCK_L": 3, "POLY_BLOCK_S": 
            "PROVE_DERIVE_T2A": 18, "NTT_TABLE_SHARE": 19, "NTT_LAUNCH_LOG": 20,
            "PROVE_FUSE_DIV": 21, "PROVE_SRS_LOGS": 22,
            "PROVE_PACK_FUSE": 23, "PROVE_EARLY_COMMITS": 24,
-           "PROVE_HELPER_COPY": 25, "PROVE_EVAL_AGG": 26, "PROVE_GRAPH": 27}
+           "PROVE_HELPER_COPY": 25, "PROVE_EVAL_AGG": 26, "PROVE_GRAPH": 27,
+           "DROPIN_HOST_WORK": 28}
 
 PLK_PROVE_STRICT = 1
 PLK_PROVE_PREPROCESSED = 2

@@ -1,6 +1,8 @@
 """Drop-in proof: the reference's UNMODIFIED plonk.h prover compiled against include/
 (pre-included prelude) so poly_mul / srs_eval_at_s run in libplonkhip on the GPU.  The
-34-byte proofs must equal the golden proofs recorded from the all-CPU reference.
+34-byte proofs must equal the golden proofs recorded from the all-CPU reference -- with the
+small-size policy at its default (toy calls on the host, include/plk_host.h) and at 0 (every
+call on the GPU, PLK_OPT_DROPIN_HOST_WORK).
 
 The drop-in library (oracle/_ref/libplonkref_dropin.so) can only be BUILT where
 /root/reference exists; it travels to the GPU box with the snapshot (oracle/_ref is git-ignored,
@@ -18,12 +20,16 @@ pytestmark = pytest.mark.gpu
 DROPIN = os.path.join(ROOT, "oracle", "_ref", "libplonkref_dropin.so")
 
 
-@pytest.fixture(scope="module")
-def dropin(hip):
+@pytest.fixture(scope="module", params=["default", "all_gpu"])
+def dropin(hip, request):
     assert os.path.exists(DROPIN), ("drop-in build absent: %s (make -C oracle, needs /root/reference at "
                                     "build time; it travels to the GPU box in the snapshot)" % DROPIN)
     from pyoracle import Reference
-    return Reference(DROPIN)
+    if request.param == "default":
+        yield Reference(DROPIN)
+    else:
+        with hip.options(DROPIN_HOST_WORK=0):
+            yield Reference(DROPIN)
 
 
 def test_toy_proof_bytes(dropin):
