@@ -648,6 +648,7 @@ def prove_component(torch, hip, dev, log2n, reps=9, preprocessed=False, barrier=
         out = pr.rounds_dev(polys, chal, rnd, preprocessed=preprocessed)
         t.append(time.perf_counter() - t0)
     t.sort()
+    roof, launches = prove_roofline(hip, pr, polys, chal, rnd, preprocessed, t[len(t) // 2], out)
     extra = {"preprocess_ms_once": pre_ms,
              "preprocessed": "the forward transforms of the six fixed circuit polynomials q_o q_m q_l q_r s_sigma_3 "
                              "l_1_x (PLONK's preprocessed input) computed once by plk_prover_preprocess before the "
@@ -656,7 +657,7 @@ def prove_component(torch, hip, dev, log2n, reps=9, preprocessed=False, barrier=
     # ms = the MEDIAN of the synchronous calls (the honest figure for one call; box-to-box spread
     # ~3 %); best_ms beside it
     return {"ms": round(t[len(t) // 2] * 1e3, 3), "median_ms": round(t[len(t) // 2] * 1e3, 3),
-            "best_ms": round(t[0] * 1e3, 3), "calls": reps, "gates": n, **extra,
+            "best_ms": round(t[0] * 1e3, 3), "calls": reps, "gates": n, "launches": launches, "roofline": roof, **extra,
             "deterministic": out == first, "matches_oracle": _prove_golden(n, out),
             "device_mib": round(pr.device_bytes() / 2**20, 1),
             "note": "rounds 1-5 of plonk_prove, synthetic interpolated polys (gen.prove_instance, seed 51), SRS len 2n+8, "
@@ -664,6 +665,51 @@ def prove_component(torch, hip, dev, log2n, reps=9, preprocessed=False, barrier=
                     "recorded answer of the CPU restatement oracle/prove_ref.py (tests/golden/prove_2_20.json), which is "
                     "pinned to the reference's own proofs at n = 4 -- the reference cannot prove above 4 gates "
                     "(no 2^20-point domain in GF(17)), so parity at 2^20 is pinned through that restatement"}
+
+
+def prove_roofline(hip, pr, polys, chal, rnd, preprocessed, wall_s, want, reps=7):
+    """C5's roofline for the line.  The proof's NTT kernels -- every pass of round
+    3's two product batches -- timed by hipEvents on the prover's own stream around each batch
+    (plk_prover_profile_dev, median of `reps` proofs; the span includes the boundaries between the
+    batch's launches, so the fraction is a lower bound), their radix-2 butterflies counted from the
+    library's launch plan (plk_ntt_launch_log) and priced against the butterfly peaks of
+    profiles/r02_bfly_peak.json exactly as tools/ntt_roofline.py prices rocprof durations
+    (plonkhip.roofline); the proof's algorithmic bytes (SURVEY 8(d) terms, plk_prover_alg_bytes) over
+    the median wall time against the HBM spec peak; launches = kernel nodes of the call captured as a
+    HIP graph (plk_prover_launches: counted, never run).  Returns (roofline dict, launches)."""
+    from plonkhip import roofline as RL
+    hip.ntt_launch_log()                             # (drop older records)
+    with hip.options(NTT_LAUNCH_LOG=1):
+        got, _ = pr.profile_dev(polys, chal, rnd, preprocessed)
+    plan = hip.ntt_launch_log()
+    prof = sorted((pr.profile_dev(polys, chal, rnd, preprocessed) for _ in range(reps)), key=lambda x: x[1]["ntt_ms"])
+    med = prof[len(prof) // 2][1]
+    same = got == want and all(o == want for o, _ in prof)
+    pk = RL.load_peaks(RL.PEAKS)
+    tot = RL.plan_roofline(plan, pk)
+    kernels, other = pr.launches(polys, chal, rnd, preprocessed)
+    alg = pr.alg_bytes()
+    ntt_ms = med["ntt_ms"]
+    rate = tot["butterflies"] / (ntt_ms * 1e-3)
+    roof_ms = tot["roof_s"] * 1e3
+    return {"bound": "valu", "unit": "Gbutterfly/s", "achieved": round(rate / 1e9, 1),
+            "peak": round(tot["butterflies"] / tot["roof_s"] / 1e9, 1), "frac": round(roof_ms / ntt_ms, 4),
+            "butterflies": tot["butterflies"], "roof_ms": round(roof_ms, 4), "ntt_ms": round(ntt_ms, 4),
+            "ntt_launches": tot["launches"], "span_ms": round(med["span_ms"], 4),
+            "ntt_share_of_span": round(ntt_ms / med["span_ms"], 3),
+            "ntt_hbm": {"alg_bytes": tot["bytes"], "frac": round(tot["bytes"] / HBM_PEAK_GBS / 1e9 / (ntt_ms * 1e-3), 4),
+                        "def": "8 B per element per pass and array (u32 read + write), 12 B per element per product "
+                               "in the centre (DESIGN 4)"},
+            "hbm": {"alg_bytes": alg, "achieved": round(alg / wall_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(alg / wall_s / 1e9 / HBM_PEAK_GBS, 5),
+                    "def": "SURVEY 8(d) per-op bytes over the reference's own ops of rounds 1-5 (17 poly_mul, 9 "
+                           "srs_eval_at_s, 3 poly_divide, 9 poly_eval; plk_prover_alg_bytes) / the median wall time"},
+            "same_proof_while_profiled": same,
+            "peak_source": "profiles/r02_bfly_peak.json per launch (forward / shared passes DIF, inverse DIT, centre "
+                           "(2 DIF + 1 DIT) / 3, F29 or BabyBear per the launch log); peak = the butterfly-weighted "
+                           "harmonic mean",
+            "timing": "hipEvents on the prover's stream around round 3's two product batches (plk_prover_profile_dev), "
+                      "median of %d proofs" % reps}, kernels
 
 
 def prove_split_pieces(torch, hip, dev, log2n, reps=5):

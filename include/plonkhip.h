@@ -115,10 +115,11 @@ enum {
   PLK_OPT_COUNT = 29
 };
 int plk_set_option(int opt, int64_t value);   /* PLK_ERR_ARG: unknown option or value out of range */
-/* Diagnostics for the offline roofline tools: with PLK_OPT_NTT_LAUNCH_LOG = 1 every NTT pass launch
- * is recorded as 7 ints {kind (0 forward, 1 inverse, 2 center, 3 shared lo = 0 pass), tile bits,
- * pass bits, log2 size, arrays / products, arrays per block, center pass units}; this copies up to
- * cap records into out (7 ints each), clears the log and returns the count. */
+/* Diagnostics for the roofline tools: with PLK_OPT_NTT_LAUNCH_LOG = 1 every NTT pass launch
+ * is recorded as 8 ints {kind (0 forward, 1 inverse, 2 center, 3 shared lo = 0 pass), tile bits,
+ * pass bits, log2 size, arrays / products, arrays per block, center pass units, field (0 F29,
+ * 1 BabyBear)}; this copies up to cap records into out (8 ints each), clears the log and returns
+ * the count. */
 int plk_ntt_launch_log(int32_t *out, int cap);
 int64_t plk_get_option(int opt);              /* -1 for an unknown option */
 
@@ -315,6 +316,22 @@ int plk_prover_rounds_dev(plk_prover_t *p, const uint8_t *const d_polys[13], con
  * drops them).  Proof bytes are identical with and without. */
 #define PLK_PROVE_PREPROCESSED 2
 int plk_prover_preprocess(plk_prover_t *p, const uint8_t *const d_polys[13]);
+/* Measurement of one proof (bench.py's C5 roofline; no reference counterpart).
+ * plk_prover_profile_dev = plk_prover_rounds_dev (same bytes) with hipEvents on the prover's stream
+ * around its whole launch sequence and around each of round 3's two product batches -- every NTT
+ * pass kernel of the proof; ms = {launch sequence, both batches, batch 1, batch 2} in milliseconds
+ * (one prover, no helpers).
+ * plk_prover_launches: the kernel launches (and other graph nodes: copies, memsets) of one such
+ * call, counted by capturing it as a HIP graph that is never launched (nothing runs, no state
+ * changes).
+ * plk_prover_alg_bytes: rounds 1-5's algorithmic bytes in SURVEY 8(d) terms over the reference's own
+ * ops (src/plonk.h:277-621): 17 poly_mul at la + lb + (la + lb - 1), 9 srs_eval_at_s at 4 B per point,
+ * 3 poly_divide (operands read, quotient and remainder written), 9 poly_eval (one read each). */
+int plk_prover_profile_dev(plk_prover_t *p, const uint8_t *const d_polys[13], const uint8_t chal[5],
+                           const uint8_t rand9[9], int flags, uint8_t proof[34], double ms[4]);
+int plk_prover_launches(plk_prover_t *p, const uint8_t *const d_polys[13], const uint8_t chal[5],
+                        const uint8_t rand9[9], int flags, int *kernels, int *other_nodes);
+uint64_t plk_prover_alg_bytes(const plk_prover_t *p);
 
 /* Strong-scaled proof over several GPUs (round 3's independent poly_mul jobs spread
  * across GPUs as whole jobs).  Two of round 3's product chains depend only on the proof's inputs:

@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #ifndef PLK_NTT_DIAG
@@ -1540,16 +1541,19 @@ WTw inv_wtw(int k) {
 // order, for the offline roofline tools (tools/ntt_roofline.py, tools/ntt_pmc_summary.py --plan):
 // a profiler records a launch's grid, not how many arrays its blocks walk (per_block below) or
 // how many pass units the persistent center kernel runs.  kind: 0 forward pass, 1 inverse pass,
-// 2 center (n = products, units = lo = 0 passes run per tile), 3 shared-operand lo = 0 pass.
+// 2 center (n = products, units = lo = 0 passes run per tile), 3 shared-operand lo = 0 pass;
+// field 0 = F29, 1 = BabyBear (bench.py prices each launch against its field's butterfly peak).
 struct LaunchRec {
-  int32_t kind, tb, m, k, n, per_block, units;
+  int32_t kind, tb, m, k, n, per_block, units, field;
 };
 std::mutex g_log_mu;
 std::vector<LaunchRec> g_log;
+template <class F>
 void log_launch(int kind, int tb, int m, int k, int n, int per_block, int units) {
   if (!plk_opt(PLK_OPT_NTT_LAUNCH_LOG)) return;
   std::lock_guard<std::mutex> lk(g_log_mu);
-  if (g_log.size() < 65536) g_log.push_back(LaunchRec{kind, tb, m, k, n, per_block, units});
+  if (g_log.size() < 65536)
+    g_log.push_back(LaunchRec{kind, tb, m, k, n, per_block, units, std::is_same<F, F29>::value ? 0 : 1});
 }
 
 // Arrays (jobs) per block of a table pass: several arrays of one tile share its column-table words
@@ -1583,13 +1587,13 @@ void launch_fwd(WPass p, const WArrs& arrs, int na, WTw tw, hipStream_t st) {
   if constexpr (M < TB) {
     if (tw.col && p.lo + M == p.k) {
       const int J = per_block(tiles, na);
-      log_launch(0, TB, M, p.k, na, J, 0);
+      log_launch<F>(0, TB, M, p.k, na, J, 0);
       hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, F, true>), dim3(tiles, (na + J - 1) / J), dim3(wt_nt(TB)), 0, st, p,
                          arrs, tw, na, J);
       return;
     }
   }
-  log_launch(0, TB, M, p.k, na, 1, 0);
+  log_launch<F>(0, TB, M, p.k, na, 1, 0);
   hipLaunchKernelGGL((wt_fwd_kernel<TB, R, M, U8, F>), dim3(tiles, na), dim3(wt_nt(TB)), 0, st, p, arrs, tw, na, 1);
 }
 template <int TB, int M, bool U8, class F>
@@ -1599,13 +1603,13 @@ void launch_inv(WPass p, const WJobs& jobs, int nj, WTw tw, uint32_t ninv, hipSt
   if constexpr (M < TB && U8) {
     if (tw.col && p.lo + M == p.k) {
       const int J = per_block(tiles, nj);
-      log_launch(1, TB, M, p.k, nj, J, 0);
+      log_launch<F>(1, TB, M, p.k, nj, J, 0);
       hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8, F, true>), dim3(tiles, (nj + J - 1) / J), dim3(wt_nt(TB)), 0, st, p,
                          jobs, tw, ninv, nj, J);
       return;
     }
   }
-  log_launch(1, TB, M, p.k, nj, 1, 0);
+  log_launch<F>(1, TB, M, p.k, nj, 1, 0);
   hipLaunchKernelGGL((wt_inv_kernel<TB, R, M, U8, F>), dim3(tiles, nj), dim3(wt_nt(TB)), 0, st, p, jobs, tw, ninv, nj, 1);
 }
 
@@ -1797,7 +1801,7 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
       }
     }
     if (ns) {
-      log_launch(3, TB, TB, k, ns, 1, ns);
+      log_launch<F>(3, TB, TB, k, ns, 1, ns);
       hipLaunchKernelGGL((wt_fixfwd_kernel<TB, wt_rc(TB), F>), dim3(tiles, ns), dim3(wt_ntc(TB)), 0, st, WPass{k, 0}, sh,
                          twf);
       PLK_HIP(hipGetLastError());
@@ -1812,7 +1816,7 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
   if (grid) {
     int units = 0;
     for (int j = 0; j < nj; j++) units += center_units(cj, j);
-    log_launch(2, TB, TB, k, nj, 1, units);
+    log_launch<F>(2, TB, TB, k, nj, 1, units);
     if (grp)
       hipLaunchKernelGGL((wt_center_kernel<TB, wt_rc(TB), F, true>), dim3(grid), dim3(wt_ntc(TB)), 0, st, WPass{k, 0},
                          cj, twf, sc);
@@ -1976,8 +1980,8 @@ extern "C" int plk_ntt_launch_log(int32_t* out, int cap) {
   const int n = (int)std::min<size_t>(g_log.size(), cap > 0 ? (size_t)cap : 0);
   for (int i = 0; i < n && out; i++) {
     const LaunchRec& r = g_log[i];
-    const int32_t v[7] = {r.kind, r.tb, r.m, r.k, r.n, r.per_block, r.units};
-    for (int f = 0; f < 7; f++) out[7 * i + f] = v[f];
+    const int32_t v[8] = {r.kind, r.tb, r.m, r.k, r.n, r.per_block, r.units, r.field};
+    for (int f = 0; f < 8; f++) out[8 * i + f] = v[f];
   }
   g_log.clear();
   return n;

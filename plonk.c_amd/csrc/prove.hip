@@ -1730,6 +1730,10 @@ struct plk_prover {
   int64_t g_opt[PLK_OPT_COUNT] = {};
   uint32_t g_seq = 0;              // the completion word the graph's last kernel writes
   SlotFile g_sf{};                 // the scalar file its first kernel holds
+  // plk_prover_profile_dev: events around the launch sequence [0] .. [5] and round 3's two product
+  // batches ([1]-[2], [3]-[4]: every NTT pass kernel of the proof), recorded only while tev_on
+  hipEvent_t tev[6] = {};
+  bool tev_on = false;
 };
 
 namespace {
@@ -1768,6 +1772,27 @@ Lens lens_for(uint64_t n, uint64_t lz) {
   L.lzz = L.lzx;
   L.lwo = L.lzz >= 2 ? L.lzz - 1 : 1;
   return L;
+}
+
+// SURVEY 8(d)'s algorithmic bytes of rounds 1-5 (plk_prover_alg_bytes): the reference's ops as it
+// calls them (src/plonk.h:277-621), each at its 8(d) figure -- the 17 poly_mul at la + lb + (la + lb
+// - 1) bytes (its own association, ((A2 B2) C2) z), the 9 srs_eval_at_s at 4 B per point, the 3
+// poly_divide at numerator + divisor read and quotient + remainder written, the 9 poly_eval at z
+// (src/plonk.h:527-533, 567, 574) at one read of the polynomial.  The reference's lincombs (poly_add /
+// poly_scale chains) are not counted: a lower bound on any implementation's traffic.
+uint64_t alg_bytes_for(const Lens& L) {
+  auto pm = [](uint64_t a, uint64_t b) { return a + b + (a + b - 1); };
+  const uint64_t n = L.n, lz = L.lz, part = n + 2;
+  const uint64_t lmid = L.ltx > part ? std::min<uint64_t>(part, L.ltx - part) : 1;
+  const uint64_t lhi = L.ltx > 2 * part ? L.ltx - 2 * part : 1;
+  uint64_t s = 3 * pm(2, lz) + pm(3, lz);                                        // rounds 1-2 blindings
+  s += pm(L.la, L.la) + pm(L.lab, n) + 3 * pm(L.la, n);                          // a b, (a b) q_m, a q_l ..
+  s += 2 * pm(L.la, L.la) + 2 * pm(L.l2a, L.la) + pm(L.l2b, L.lzx) + pm(L.l2b, L.lzw);   // t_2, t_3
+  s += pm(L.lz1, n) + pm(L.lzx, n);                                              // Z1 l_1, z_x s_sigma_3
+  s += 4 * (3 * L.la + L.lzx + std::min<uint64_t>(part, L.ltx) + lmid + lhi + L.lwq + L.lwo);   // commits
+  s += (L.lnum + lz + L.ltx + (lz - 1)) + (L.lw + 2 + L.lwq + 1) + (L.lzz + 2 + L.lwo + 1);     // divisions
+  s += 3 * L.la + 2 * n + L.ltx + L.lzw + n + L.lrx;                             // evaluations at z
+  return s;
 }
 
 struct Bump {
@@ -2238,7 +2263,7 @@ void plk_prover_destroy(plk_prover_t* P) {
   if (P->h_res) (void)hipHostFree(P->h_res);
   (void)hipFree(P->fix_mem);
   (void)hipFree(P->hin);
-  for (hipEvent_t e : {P->ev, P->ev_in, P->ev_done})
+  for (hipEvent_t e : {P->ev, P->ev_in, P->ev_done, P->tev[0], P->tev[1], P->tev[2], P->tev[3], P->tev[4], P->tev[5]})
     if (e) (void)hipEventDestroy(e);
   if (P->st) (void)hipStreamDestroy(P->st);
   delete P;
@@ -2448,7 +2473,10 @@ int rounds(plk_prover* P, const uint8_t* const* pl, const uint8_t chal[5], const
     for (auto* g : {&g1, &g2}) {
       std::vector<PlkPolyMulJob> jobs;
       for (const J& x : *g) jobs.push_back(x.j);
+      const int te = g == &g1 ? 1 : 3;   // (plk_prover_profile_dev)
+      if (P->tev_on) PLK_HIP(hipEventRecord(P->tev[te], P->st));
       if (!jobs.empty()) RC(plk_poly_mul_batch_launch(jobs.data(), (int)jobs.size(), P->work, P->work_bytes, P->st));
+      if (P->tev_on) PLK_HIP(hipEventRecord(P->tev[te + 1], P->st));
       if (g == &g1 && derive_t2a && !derive_fwd) {   // (a_x b_x is complete on the stream here)
         const uint64_t blocks = std::min<uint64_t>((L.lab + 1023) / 1024, 4096);
         hipLaunchKernelGGL(t2a_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, P->st, P->AB, cA, cB,
@@ -2922,6 +2950,75 @@ int plk_prover_rounds_dev(plk_prover_t* P, const uint8_t* const d_polys[13], con
   if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
   return finish(P, (flags & PLK_PROVE_STRICT) != 0, 0, proof);
 }
+
+int plk_prover_profile_dev(plk_prover_t* P, const uint8_t* const d_polys[13], const uint8_t chal[5],
+                           const uint8_t rand9[9], int flags, uint8_t proof[34], double ms[4]) {
+  if (!P || !d_polys || !chal || !rand9 || !ms) { plk_set_error("plk_prover_profile_dev: NULL argument"); return PLK_ERR_ARG; }
+  for (int i = 0; i < 13; i++)
+    if (!d_polys[i]) { plk_set_error("plk_prover_profile_dev: polynomial %d is NULL", i); return PLK_ERR_ARG; }
+  if (P->nhelp) { plk_set_error("plk_prover_profile_dev: a prover with helpers attached"); return PLK_ERR_ARG; }
+  PROVER_ON_DEVICE(P);
+  for (hipEvent_t& e : P->tev)
+    if (!e) PLK_HIP(hipEventCreate(&e));
+  PLK_HIP(hipEventRecord(P->tev[0], P->st));
+  P->tev_on = true;
+  int rc = rounds(P, d_polys, chal, rand9, (flags & PLK_PROVE_PREPROCESSED) != 0);
+  P->tev_on = false;
+  if (!rc) rc = hipEventRecord(P->tev[5], P->st) == hipSuccess ? PLK_OK : PLK_ERR_HIP;
+  if (rc) { (void)hipStreamSynchronize(P->st); return rc; }
+  if ((rc = finish(P, (flags & PLK_PROVE_STRICT) != 0, 0, proof))) return rc;
+  PLK_HIP(hipEventSynchronize(P->tev[5]));
+  float t[3];
+  PLK_HIP(hipEventElapsedTime(&t[0], P->tev[0], P->tev[5]));
+  PLK_HIP(hipEventElapsedTime(&t[1], P->tev[1], P->tev[2]));
+  PLK_HIP(hipEventElapsedTime(&t[2], P->tev[3], P->tev[4]));
+  ms[0] = t[0];
+  ms[1] = (double)t[1] + t[2];
+  ms[2] = t[1];
+  ms[3] = t[2];
+  return PLK_OK;
+}
+
+int plk_prover_launches(plk_prover_t* P, const uint8_t* const d_polys[13], const uint8_t chal[5], const uint8_t rand9[9],
+                        int flags, int* kernels, int* other_nodes) {
+  if (!P || !d_polys || !chal || !rand9 || !kernels) { plk_set_error("plk_prover_launches: NULL argument"); return PLK_ERR_ARG; }
+  for (int i = 0; i < 13; i++)
+    if (!d_polys[i]) { plk_set_error("plk_prover_launches: polynomial %d is NULL", i); return PLK_ERR_ARG; }
+  if (P->nhelp) { plk_set_error("plk_prover_launches: a prover with helpers attached"); return PLK_ERR_ARG; }
+  PROVER_ON_DEVICE(P);
+  PLK_HIP(hipStreamSynchronize(P->st));
+  const uint32_t epoch = P->scan_epoch, seq = P->seq;
+  PLK_HIP(hipStreamBeginCapture(P->st, hipStreamCaptureModeThreadLocal));
+  int rc = rounds(P, d_polys, chal, rand9, (flags & PLK_PROVE_PREPROCESSED) != 0);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(P->st, &g);
+  P->seq = seq;   // (nothing ran: the next call's completion word and scan epochs are unchanged)
+  P->scan_epoch = epoch;
+  if (!rc && (e != hipSuccess || !g)) {
+    plk_set_error("plk_prover_launches: stream capture failed (%s)", hipGetErrorString(e));
+    rc = PLK_ERR_HIP;
+  }
+  int nk = 0, no = 0;
+  size_t nn = 0;
+  if (!rc && hipGraphGetNodes(g, nullptr, &nn) == hipSuccess) {
+    std::vector<hipGraphNode_t> nodes(nn);
+    if (hipGraphGetNodes(g, nodes.data(), &nn) == hipSuccess)
+      for (hipGraphNode_t nd : nodes) {
+        hipGraphNodeType t;
+        if (hipGraphNodeGetType(nd, &t) != hipSuccess) continue;
+        if (t == hipGraphNodeTypeKernel) nk++;
+        else if (t != hipGraphNodeTypeEmpty) no++;
+      }
+  }
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
+  if (rc) return rc;
+  *kernels = nk;
+  if (other_nodes) *other_nodes = no;
+  return PLK_OK;
+}
+
+uint64_t plk_prover_alg_bytes(const plk_prover_t* P) { return P ? alg_bytes_for(lens_for(P->n, P->zh_len)) : 0; }
 
 int plk_prover_attach_helpers(plk_prover_t* P, int k) {
   if (!P || k < 0 || k > 2) { plk_set_error("plk_prover_attach_helpers: prover and 0 <= k <= 2 required"); return PLK_ERR_ARG; }

@@ -68,6 +68,10 @@ SIGNATURES = {
     "plk_prover_device_bytes": (_sz, [_vp]),
     "plk_prover_prove": (C.c_int, [_vp, _vp, _u8p, _u8p, _u8p]),
     "plk_prover_rounds_dev": (C.c_int, [_vp, C.POINTER(_vp), _u8p, _u8p, C.c_int, _u8p]),
+    "plk_prover_profile_dev": (C.c_int, [_vp, C.POINTER(_vp), _u8p, _u8p, C.c_int, _u8p, C.POINTER(C.c_double)]),
+    "plk_prover_launches": (C.c_int, [_vp, C.POINTER(_vp), _u8p, _u8p, C.c_int, C.POINTER(C.c_int),
+                                      C.POINTER(C.c_int)]),
+    "plk_prover_alg_bytes": (C.c_uint64, [_vp]),
     "plk_prover_preprocess": (C.c_int, [_vp, C.POINTER(_vp)]),
     "plk_prover_chain_bytes": (_sz, [_vp, C.c_int]),
     "plk_prover_chains_dev": (C.c_int, [_vp, C.POINTER(_vp), _u8p, _u8p, C.c_int, _vp, _vp, _vp]),
@@ -183,10 +187,10 @@ def devices():
 
 def ntt_launch_log(cap=4096):
     """plk_ntt_launch_log: the recorded NTT pass launches (PLK_OPT_NTT_LAUNCH_LOG = 1) as dicts, log cleared"""
-    buf = (C.c_int32 * (7 * cap))()
+    buf = (C.c_int32 * (8 * cap))()
     n = int(lib().plk_ntt_launch_log(buf, cap))
-    keys = ("kind", "tb", "m", "k", "n", "per_block", "units")
-    return [dict(zip(keys, buf[7 * i:7 * i + 7])) for i in range(n)]
+    keys = ("kind", "tb", "m", "k", "n", "per_block", "units", "field")
+    return [dict(zip(keys, buf[8 * i:8 * i + 8])) for i in range(n)]
 
 
 def _opt_id(name):
@@ -533,6 +537,32 @@ class Prover:
         flags = (PLK_PROVE_STRICT if strict else 0) | (PLK_PROVE_PREPROCESSED if preprocessed else 0)
         _check("plk_prover_rounds_dev", lib().plk_prover_rounds_dev(self._h, args[0], args[1], args[2], flags, out))
         return bytes(out)
+
+    def profile_dev(self, polys, chal, rand, preprocessed=False):
+        """plk_prover_profile_dev: (proof bytes, {span_ms, ntt_ms, batch1_ms, batch2_ms}) -- the proof's
+        launch sequence and its two product batches (all its NTT pass kernels) timed by hipEvents on the
+        prover's stream"""
+        args = self._args(polys, chal, rand)
+        out = (C.c_uint8 * 34)()
+        ms = (C.c_double * 4)()
+        flags = PLK_PROVE_PREPROCESSED if preprocessed else 0
+        _check("plk_prover_profile_dev",
+               lib().plk_prover_profile_dev(self._h, args[0], args[1], args[2], flags, out, ms))
+        return bytes(out), dict(zip(("span_ms", "ntt_ms", "batch1_ms", "batch2_ms"), list(ms)))
+
+    def launches(self, polys, chal, rand, preprocessed=False):
+        """plk_prover_launches: (kernel launches, other graph nodes) of one proof, counted from a
+        captured (never launched) HIP graph of the call"""
+        args = self._args(polys, chal, rand)
+        k, o = C.c_int(), C.c_int()
+        flags = PLK_PROVE_PREPROCESSED if preprocessed else 0
+        _check("plk_prover_launches",
+               lib().plk_prover_launches(self._h, args[0], args[1], args[2], flags, C.byref(k), C.byref(o)))
+        return k.value, o.value
+
+    def alg_bytes(self):
+        """plk_prover_alg_bytes: the proof's algorithmic bytes in SURVEY 8(d) terms"""
+        return int(lib().plk_prover_alg_bytes(self._h))
 
     # ---- strong-scaled proof (plk_prover_chains_dev / plk_prover_rounds_ext_dev)
     def chain_bytes(self, chain):

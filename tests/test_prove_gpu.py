@@ -232,6 +232,53 @@ def test_rounds_2_20_vs_golden(hip):
     assert got.hex() == g["proof"]
 
 
+def test_profile_and_launch_count_2_20(hip):
+    """The C5 line's measurement entry points: plk_prover_profile_dev gives the
+    recorded proof bytes with its event times consistent (both product batches inside the launch
+    sequence); plk_prover_launches counts the proof's kernels from a captured, never launched graph
+    -- 12 at 2^20 gates plain, 11 preprocessed (no shared-operand pass; DESIGN 4b,
+    profiles/r05_prove_2^20_*breakdown.txt) -- without changing what the next call
+    computes; the launch plan holds the 7 NTT pass launches of the two batches, all over F29."""
+    from plonkhip import roofline as RL
+    g = load_golden("prove_2_20.json")
+    n = g["n"]
+    polys, chal, rnd, zh, pts = _synthetic(n, g["seed"], g["srs_len"])
+    d = [torch.from_numpy(p).to("cuda") for p in polys]
+    pr = hip.Prover(n, zh, pts)
+    for pre in (False, True):
+        if pre:
+            pr.preprocess(d)
+        assert pr.launches(d, chal, rnd, preprocessed=pre) == (11 if pre else 12, 0)
+        assert pr.rounds_dev(d, chal, rnd, preprocessed=pre).hex() == g["proof"]
+        hip.ntt_launch_log()
+        with hip.options(NTT_LAUNCH_LOG=1):
+            got, ms = pr.profile_dev(d, chal, rnd, preprocessed=pre)
+        plan = hip.ntt_launch_log()
+        assert got.hex() == g["proof"]
+        assert 0 < ms["batch1_ms"] and 0 < ms["batch2_ms"] and ms["ntt_ms"] < ms["span_ms"] < 5.0, ms
+        assert [r["field"] for r in plan] == [0] * len(plan)
+        assert sorted(r["kind"] for r in plan) == ([0, 0, 1, 1, 2, 2] if pre else [0, 0, 1, 1, 2, 2, 3])
+        tot = RL.plan_roofline(plan, RL.load_peaks(RL.PEAKS))
+        assert tot["roof_s"] * 1e3 < ms["ntt_ms"]          # the roof is below the measured time
+    assert pr.alg_bytes() > 9 * 4 * n
+
+
+def test_profile_and_launches_small_vs_rounds(hip):
+    """at n = 4096 the profiled proof and the counted capture leave rounds_dev's answer unchanged,
+    call after call (the capture restores the completion-word sequence it advanced)"""
+    polys, chal, rnd, zh, pts = _synthetic(4096, 9, 2 * 4096 + 8)
+    d = [torch.from_numpy(p).to("cuda") for p in polys]
+    pr = hip.Prover(4096, zh, pts)
+    want = pr.rounds_dev(d, chal, rnd)
+    k, _ = pr.launches(d, chal, rnd)
+    assert 8 <= k <= 20
+    assert pr.rounds_dev(d, chal, rnd) == want
+    assert pr.profile_dev(d, chal, rnd)[0] == want
+    assert pr.rounds_dev(d, chal, rnd) == want
+    with hip.options(PROVE_GRAPH=1):
+        assert pr.rounds_dev(d, chal, rnd) == want and pr.rounds_dev(d, chal, rnd) == want
+
+
 @pytest.mark.parametrize("n,seed", [(256, 3), (3000, 5), (5000, 7), (1 << 16, 41)])
 def test_derive_t2a_modes_vs_oracle(hip, oracle, n, seed):
     """Round 3's A2 B2 three ways (PLK_OPT_PROVE_DERIVE_T2A): its own product (0), t2a_kernel (1),

@@ -24,12 +24,17 @@ now walk several arrays per block (grid y = array groups, not arrays), and the p
 exact counts: arrays x tiles x 2^(TB-1) x M for a pass, tiles x pass units x 2^(TB-1) x TB for the
 center (the lo = 0 passes it actually runs, fixed operands' skipped passes excluded)."""
 import json
+import os
 import re
 import sqlite3
 import sys
 from collections import defaultdict
 
-PAT = re.compile(r"wt_(fwd|inv|center)_kernel<(\d+), (\d+)(?:, (\d+))?.*?(F29|FBB)")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plonk.c_amd"))
+from plonkhip import roofline as RL  # noqa: E402  (the same accounting as bench.py's C5 line)
+
+PAT = re.compile(r"wt_(fwd|inv|center|fixfwd)_kernel<(\d+), (\d+)(?:, (\d+))?.*?(F29|FBB)")
+KIND = {"fwd": 0, "inv": 1, "center": 2, "fixfwd": 3}
 
 
 def parse(name):
@@ -41,13 +46,7 @@ def parse(name):
 
 
 def peak(kind, field, pk):
-    f = "f29" if field == "F29" else "bb"
-    dif, dit = pk[f + "_dif_Gbfly_s"] * 1e9, pk[f + "_dit_Gbfly_s"] * 1e9
-    if kind == "fwd":
-        return dif
-    if kind == "inv":
-        return dit
-    return 3.0 / (2.0 / dif + 1.0 / dit)
+    return RL.peak_bfly_s(KIND[kind], field, pk)
 
 
 def main():
@@ -65,7 +64,7 @@ def main():
     plan = None
     if "--plan" in sys.argv:
         with open(sys.argv[sys.argv.index("--plan") + 1]) as f:
-            plan = [r for r in json.load(f)["launches"] if r["kind"] in (0, 1, 2)]
+            plan = [r for r in json.load(f)["launches"] if r["kind"] in (0, 1, 2, 3)]
     disp = []
     pi = 0
     for i, (name, gx, gy, wx, dur, _) in enumerate(rows):
@@ -76,14 +75,14 @@ def main():
         if plan is not None:
             r = plan[pi]
             pi += 1
-            want = {"fwd": 0, "inv": 1, "center": 2}[kind]
-            if r["kind"] != want or r["tb"] != tb or r["m"] != mm:
+            if r["kind"] != KIND[kind] or r["tb"] != tb or r["m"] != mm:
                 raise SystemExit("plan mismatch at %s: %r" % (name, r))
-            tiles = (1 << r["k"]) >> tb
-            bfly = tiles * ((r["units"] * tb) if kind == "center" else (r["n"] * mm)) * (1 << (tb - 1))
+            bfly = RL.launch_butterflies(r)
             disp.append((name.replace("(anonymous namespace)::", "").split("(")[0], gx, gy, kind, field, bfly, dur / 1e3))
             continue
-        if kind == "center":
+        if kind == "fixfwd":
+            bfly = (gx // wx) * gy * (1 << (tb - 1)) * tb
+        elif kind == "center":
             nxt = next((r for r in rows[i + 1:] if parse(r[0]) and parse(r[0])[0] == "inv"), None)
             if nxt is None:
                 continue
