@@ -125,6 +125,9 @@ namespace {
 #ifndef PLK_NTT_M17
 #define PLK_NTT_M17 1          // COLT byte outputs: 1 = mod 17 of the index through an LDS table, 0 = 24-bit arithmetic
 #endif
+#ifndef PLK_NTT_COLI_DERIVE
+#define PLK_NTT_COLI_DERIVE 1  // last inverse passes: scaled column factors from the lo / hi roots by products (0: the table)
+#endif
 #ifndef PLK_NTT_DERIVE
 #define PLK_NTT_DERIVE 1       // 2^13-tile first forward passes compute a derived operand (WArrs::derive); 0: compiled out
 #endif
@@ -1141,7 +1144,25 @@ __global__ __launch_bounds__(wt_nt(TB), 8) void wt_inv_kernel(WPass p, WJobs job
   };
   load(ji, v);   // (the first job's loads go out before the tables')
   uint32_t cl[G::HIGH ? G::E : 1], ch[G::HIGH && !COLT ? G::E : 1];
-  if (G::HIGH) {
+  if constexpr (G::HIGH && COLT && PLK_NTT_COLI_DERIVE && G::colsq(0, true)) {
+    // The scaled column factors without the table (the 2^22 table is 16 MiB read per
+    // launch).  Round 0 is column-mapped: a thread's E words share their column L and differ only in
+    // the row bits [L0, L0 + R), so their exponents are ex0 + sum over the set register bits b of d_b
+    // (bitrev of disjoint bits adds).  cl[0] = scale(w^ex0) from the lo / hi roots, d_b's roots the
+    // same way, then each cl[k] = cl[k - 2^b] * w^(d_b) for k's top bit b: R + 1 root lookups and
+    // E - 1 + R + 2 multiplies per thread for all of the block's jobs.  Every product is fully
+    // reduced, so the words equal the table's (tests: the prover goldens, poly_mul vs the oracle).
+    // (Passes narrower than a round, M < R + L0, keep the table: their registers leave the row.)
+    const uint32_t e0 = G::col_exp(p, tile, b0);
+    cl[0] = F::scale(F::colf(tw.lo[e0 & 4095u], tw.hi[e0 >> 12]), ninv);
+#pragma unroll
+    for (int b = 0; (1 << b) < G::E; b++) {
+      const uint32_t d = G::col_exp(p, tile, b0 + (1u << (L0 + b))) - e0;
+      const uint32_t g = F::colf(tw.lo[d & 4095u], tw.hi[d >> 12]);
+#pragma unroll
+      for (int k = 1 << b; k < (2 << b) && k < G::E; k++) cl[k] = F::colf(cl[k - (1 << b)], g);
+    }
+  } else if (G::HIGH) {
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
       if constexpr (COLT) {

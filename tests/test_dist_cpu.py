@@ -97,7 +97,7 @@ def _run(world, n, batch, irregular_at):
     return got
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_sharded_msm_matches_single_device(oracle, world):
     n, batch = 10007, 3
     got = _run(world, n, batch, {})
@@ -106,12 +106,14 @@ def test_sharded_msm_matches_single_device(oracle, world):
         assert got[r] == (want, 0)
 
 
-def test_irregular_point_in_a_later_shard(oracle):
-    """an off-curve point in rank 1's shard of MSM 1 (and in rank 0's of MSM 2): those MSMs take
-    the gathered serial fold and still equal the reference fold; MSM 0 stays on the log path"""
+@pytest.mark.parametrize("world,late", [(2, 1), (8, 5)])
+def test_irregular_point_in_a_later_shard(oracle, world, late):
+    """an off-curve point in rank `late`'s shard of MSM 1 (and in rank 0's of MSM 2): those MSMs take
+    the gathered serial fold (the 8-way gather at the driver's largest world size) and still equal
+    the reference fold; MSM 0 stays on the log path"""
     from plonkhip.dist import shard_range
-    n, batch, world = 4099, 3, 2
-    lo1, _ = shard_range(n, 1, world)
+    n, batch = 4099, 3
+    lo1, _ = shard_range(n, late, world)
     irregular_at = {1: lo1 + 17, 2: 3}
     got = _run(world, n, batch, irregular_at)
     want = [oracle.msm(p, s).hex() for p, s in _inputs(n, batch, irregular_at)]
@@ -178,7 +180,7 @@ def _split_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_split_proof_choreography(world):
     """rank 1 (N = 2: t_3; N >= 3: t_2) and rank 2 (t_3) send their chains, rank 0 proves with
     exactly those, the other ranks idle; two proofs back to back keep the sends and receives

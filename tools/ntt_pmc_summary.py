@@ -12,10 +12,14 @@ kernel's algorithmic bytes (8 B per element per pass: u32 read + write; byte-inp
 passes 5 B), and VALU instructions per butterfly.  The SQ counters come from a subset of the
 shader engines and are scaled by launched waves / SQ_WAVES.""" 
 import json
+import os
 import re
 import sqlite3
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plonk.c_amd"))
+from plonkhip import roofline as RL  # noqa: E402  (bench.py's launch accounting)
 
 CLK = 2.4e9
 SIMDS = 1024
@@ -58,17 +62,24 @@ def tile_bits(name):
 
 def load_plan():
     """--plan plan.json (tools/prove_plan.py): arrays per (kind, TB, M, tiles) of the proof's table
-    passes -- their grid y counts array GROUPS since round 4 (several arrays per block)"""
+    passes -- their grid y counts array GROUPS since round 4 (several arrays per block) -- and the
+    centre / shared-operand launch records in launch order (the persistent centre's grid says
+    nothing about its items: its butterflies and bytes come from the record, plonkhip.roofline)"""
     if "--plan" not in sys.argv:
-        return {}
+        return {}, {}
     with open(sys.argv[sys.argv.index("--plan") + 1]) as f:
         launches = json.load(f)["launches"]
-    return {("fwd" if r["kind"] == 0 else "inv", r["tb"], r["m"], (1 << r["k"]) >> r["tb"]): r["n"]
-            for r in launches if r["kind"] in (0, 1)}
+    passes = {("fwd" if r["kind"] == 0 else "inv", r["tb"], r["m"], (1 << r["k"]) >> r["tb"]): r["n"]
+              for r in launches if r["kind"] in (0, 1)}
+    seq = defaultdict(list)
+    for r in launches:
+        if r["kind"] in (2, 3):
+            seq["center" if r["kind"] == 2 else "fixfwd"].append(r)
+    return passes, seq
 
 
 def main():
-    plan = load_plan()
+    plan, seq = load_plan()
     dbs = [load(p) for p in sys.argv[1:5]]
     keys = set()
     for a, _ in dbs:
@@ -79,6 +90,18 @@ def main():
           "included); valu_t: VALU-issue-bound time / duration; ldsconf: bank-conflict cycles / LDS-array cycles; "
           "lds/va: LDS / VALU instructions; traffic: 2 x FETCH_SIZE + WRITE_SIZE; alg: 8 B (u32 in + out) or "
           "5 B (byte side) per element; wait: SQ_WAIT_ANY / SQ_WAVE_CYCLES")
+    # launch order of the centre / shared-operand kernels within a proof (template arguments may differ
+    # between the two batches, so order by first dispatch rather than by the name's ordinal)
+    first = {}
+    for key, ids in dbs[0][1].items():   # (one trace: dispatch ids of different runs do not compare)
+        if ids:
+            first[key] = min(ids)
+    order = {}
+    for kind in ("center", "fixfwd"):
+        ks = sorted((k for k in first if ("wt_" + kind) in k[0] or (kind == "center" and "wt_center" in k[0])),
+                    key=lambda k: first[k])
+        for i, k in enumerate(ks):
+            order[k] = i
     for key in sorted(keys, key=lambda k: (k[0], k[4])):
         name, gx, gy, wx, ordn = key
         cs = {}
@@ -98,7 +121,12 @@ def main():
         center = "center" in name
         bfly = None
         alg = None
-        if TB and M is not None and not center and "fixfwd" not in name:
+        kseq = "center" if center else "fixfwd" if "fixfwd" in name else None
+        if kseq and order.get(key, 99) < len(seq.get(kseq, [])):
+            rec = seq[kseq][order[key]]
+            bfly = RL.launch_butterflies(rec)
+            alg = RL.launch_bytes(rec)
+        elif TB and M is not None and not center and "fixfwd" not in name:
             kind = "fwd" if "wt_fwd" in name else "inv"
             arrays = plan.get((kind, TB, M, blocks), gy)   # (blocks of the x dimension = tiles)
             bfly = blocks * arrays * (1 << (TB - 1)) * M
