@@ -70,6 +70,37 @@ def test_shapes_vs_oracle(hip, oracle, la, lb):
     assert ok, (la, lb)
 
 
+def test_random_shapes_and_bytes_vs_oracle(hip, oracle):
+    """80 seeded shapes drawn log-uniformly from 1 to 2^20 coefficients per operand (every dispatch
+    path and transform size up to 2^21 points, wrapped or not), each with operands of one of four byte
+    kinds -- canonical residues, any byte value, trailing zeros (an untrimmed input), sparse -- against
+    the oracle's independent NTT over 998244353; the same products again as one batched launch
+    (plk_poly_mul_batch_dev: one launch per pass for the whole batch of a transform size)"""
+    rng = np.random.default_rng(0x600D)
+    cases = []
+    for t in range(80):
+        la, lb = (int(2 ** rng.uniform(0, 20)) for _ in range(2))
+        kind = t % 4
+        a = rng.integers(0, 256 if kind == 1 else 17, la).astype(np.uint8)
+        b = rng.integers(0, 256 if kind == 1 else 17, lb).astype(np.uint8)
+        if kind == 2 and la > 1:
+            a[-min(la - 1, 5):] = 0
+        if kind == 3:
+            a[rng.random(la) < 0.9] = 0
+            b[rng.random(lb) < 0.9] = 0
+        want = oracle.poly_mul_ntt(a, b)
+        got = hip.poly_mul(a, b)
+        assert got == want, (t, la, lb, kind)   # (bytes compare: no megabyte diff on failure)
+        cases.append((a, b, want))
+    # the products of at least 64 x 64 coefficients (the NTT paths) as ONE batch: it groups its jobs
+    # by transform size, one launch per pass per size
+    big = [(a, b, w) for a, b, w in cases if len(a) >= 64 and len(b) >= 64]
+    pool = [x for a, b, _ in big for x in (a, b)]
+    outs = _run_batch(hip, pool, [(2 * i, 2 * i + 1, 0) for i in range(len(big))])
+    for (a, b, w), o in zip(big, outs):
+        assert _trim(o) == w, (len(a), len(b))
+
+
 def test_trailing_cancellation_and_zero(hip, oracle):
     # products whose top coefficients vanish: trimmed length < la + lb - 1
     a = np.zeros(5000, np.uint8); a[0] = 1; a[4000] = 0   # untrimmed input a = 1
