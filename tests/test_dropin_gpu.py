@@ -60,3 +60,29 @@ def test_large_through_headers(dropin):
     a, b = gen.poly_inputs(c["seed"], c["la"], c["lb"])
     out = dropin.poly_mul(a, b)
     assert gen.digest(np.frombuffer(out, np.uint8)) == c["sha256"]
+
+
+def test_both_sides_of_the_small_size_threshold(hip):
+    """The drop-in's small-size policy (include/plk_host.h) at its default: calls just below the
+    threshold run on the host, calls just above it on the GPU -- both equal to the reference compiled
+    in place (oracle/_ref/libplonkref.so), on canonical and raw bytes"""
+    from pyoracle import Reference
+    D, R = Reference(DROPIN), Reference()
+    assert hip.get_option("DROPIN_HOST_WORK") == 32768
+    rng = np.random.default_rng(21)
+    for la, lb in ((181, 181), (182, 182), (32768, 1), (32769, 1), (100, 400), (100, 500)):
+        for mod in (17, 256):
+            a = rng.integers(0, mod, la).astype(np.uint8)
+            b = rng.integers(0, mod, lb).astype(np.uint8)
+            assert D.poly_mul(a, b) == R.poly_mul(a, b), (la, lb, mod)
+    for n in (109, 110, 3000):                        # 300 n: host up to 109 points
+        pts, sc = gen.msm_inputs(n, n, "full")
+        assert D.msm(pts, sc) == R.msm(pts, sc), n
+    for nl, dl in ((4000, 4), (4200, 4), (9000, 2)):   # 2 (nl - dl + 1) dl around 32768
+        num = rng.integers(0, 17, nl).astype(np.uint8)
+        den = rng.integers(0, 17, dl).astype(np.uint8)
+        den[-1] = 5
+        assert D.poly_divide(num, den) == R.poly_divide(num, den), (nl, dl)
+    for ln in (16384, 16385, 100000):                 # 2 len around 32768
+        p = rng.integers(0, 256, ln).astype(np.uint8)
+        assert D.poly_eval(p, 7) == R.poly_eval(p, 7), ln
