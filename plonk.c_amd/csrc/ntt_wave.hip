@@ -125,6 +125,9 @@ namespace {
 #ifndef PLK_NTT_M17
 #define PLK_NTT_M17 1          // COLT byte outputs: 1 = mod 17 of the index through an LDS table, 0 = 24-bit arithmetic
 #endif
+#ifndef PLK_NTT_FIX_FILL
+#define PLK_NTT_FIX_FILL 0     // the shared-operand lo = 0 launch fills its last round of blocks with operands used once
+#endif
 #ifndef PLK_NTT_COLI_DERIVE
 #define PLK_NTT_COLI_DERIVE 1  // last inverse passes: scaled column factors from the lo / hi roots by products (0: the table)
 #endif
@@ -1819,6 +1822,23 @@ int wave_poly_mul_t(const WJobs& jobs, int nj, int k, uint32_t ninv, hipStream_t
       for (int j = 0; j < nj; j++) {
         if (cj.j[j].A == arrs.a[q].d) cj.j[j].afix = 1;
         if (!jobs.j[j].bfix && cj.j[j].B == arrs.a[q].d) cj.j[j].bfix = 1;
+      }
+    }
+    // (PLK_NTT_FIX_FILL) the launch runs ceil(ns tiles / resident) rounds of resident blocks: fill its
+    // last round with operands used once, whose lo = 0 pass then leaves the centre items
+    if (PLK_NTT_FIX_FILL && ns) {
+      const uint32_t per = std::max<uint32_t>(1u, center_blocks() / std::max<uint32_t>(tiles, 1u));
+      int extra = (int)(((uint32_t)ns + per - 1) / per * per) - ns;
+      for (int q = arrs.derive ? 1 : 0; q < na && extra > 0 && ns < WT_MAX_ARRS; q++) {
+        bool fixed = false;
+        for (int t = 0; t < ns; t++) fixed |= sh.a[t].d == arrs.a[q].d;
+        if (fixed) continue;
+        sh.a[ns++] = arrs.a[q];
+        extra--;
+        for (int j = 0; j < nj; j++) {
+          if (cj.j[j].A == arrs.a[q].d) cj.j[j].afix = 1;
+          if (!jobs.j[j].bfix && cj.j[j].B == arrs.a[q].d) cj.j[j].bfix = 1;
+        }
       }
     }
     if (ns) {
