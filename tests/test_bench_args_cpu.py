@@ -88,3 +88,29 @@ def test_bench_source_has_no_exec():
     with open(os.path.join(ROOT, "bench.py")) as f:
         src = f.read()
     assert "os.exec" not in src and "execv" not in src
+
+
+def test_roofline_accounting_of_a_launch_plan():
+    """plonkhip.roofline (shared by bench.py's C5 line and tools/ntt_roofline.py): the butterflies and
+    bytes of each kind of NTT launch record, priced against the peak of its kind and field"""
+    sys.path.insert(0, os.path.join(ROOT, "plonk.c_amd"))
+    from plonkhip import roofline as RL
+    pk = {"f29_dif_Gbfly_s": 6000.0, "f29_dit_Gbfly_s": 5000.0, "bb_dif_Gbfly_s": 4000.0, "bb_dit_Gbfly_s": 3000.0}
+    fwd = {"kind": 0, "tb": 13, "m": 8, "k": 21, "n": 15, "per_block": 8, "units": 0, "field": 0}
+    inv = {"kind": 1, "tb": 13, "m": 8, "k": 21, "n": 7, "per_block": 4, "units": 0, "field": 0}
+    cen = {"kind": 2, "tb": 13, "m": 13, "k": 21, "n": 9, "per_block": 1, "units": 22, "field": 0}
+    fix = {"kind": 3, "tb": 13, "m": 13, "k": 21, "n": 3, "per_block": 1, "units": 3, "field": 1}
+    tiles, half = 1 << 8, 1 << 12
+    assert RL.launch_butterflies(fwd) == tiles * 15 * 8 * half
+    assert RL.launch_butterflies(inv) == tiles * 7 * 8 * half
+    assert RL.launch_butterflies(cen) == tiles * 22 * 13 * half
+    assert RL.launch_butterflies(fix) == tiles * 3 * 13 * half
+    assert RL.launch_bytes(fwd) == (1 << 21) * 15 * 8 and RL.launch_bytes(cen) == (1 << 21) * 9 * 12
+    assert RL.peak_bfly_s(0, 0, pk) == 6000e9 and RL.peak_bfly_s(1, 0, pk) == 5000e9
+    assert RL.peak_bfly_s(3, 1, pk) == 4000e9
+    assert abs(RL.peak_bfly_s(2, 0, pk) - 3 / (2 / 6000e9 + 1 / 5000e9)) < 1
+    tot = RL.plan_roofline([fwd, inv, cen, fix], pk)
+    want = sum(RL.launch_butterflies(r) / RL.peak_bfly_s(r["kind"], r["field"], pk) for r in (fwd, inv, cen, fix))
+    assert tot["launches"] == 4 and abs(tot["roof_s"] - want) < 1e-15
+    # the committed peak file parses
+    assert RL.load_peaks(RL.PEAKS)["f29_dif_Gbfly_s"] > 1000
