@@ -122,6 +122,23 @@ def test_split_prover_exports_without_gpu():
     assert lib.plk_prover_rounds_multi_dev(None, polys, 1, chal, rnd, 0, out) == h.PLK_ERR_ARG
 
 
+def test_prover_measurement_exports_without_gpu():
+    """plk_prover_profile_dev / plk_prover_launches / plk_prover_alg_bytes (the bench line's C5
+    roofline) refuse a NULL prover or NULL outputs before touching a device"""
+    import ctypes as C
+
+    import plonkhip as h
+    lib = h.lib()
+    chal, rnd, out = (C.c_uint8 * 5)(), (C.c_uint8 * 9)(), (C.c_uint8 * 34)()
+    polys = (C.c_void_p * 13)()
+    ms = (C.c_double * 4)()
+    k, o = C.c_int(), C.c_int()
+    assert lib.plk_prover_profile_dev(None, polys, chal, rnd, 0, out, ms) == h.PLK_ERR_ARG
+    assert lib.plk_prover_launches(None, polys, chal, rnd, 0, C.byref(k), C.byref(o)) == h.PLK_ERR_ARG
+    assert lib.plk_prover_alg_bytes(None) == 0
+    assert "plk_prover_profile_dev" in h.last_error() or "plk_prover_launches" in h.last_error()
+
+
 def _gcc(args, **kw):
     return subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Werror", "-I", INCLUDE] + args,
                           capture_output=True, text=True, **kw)
